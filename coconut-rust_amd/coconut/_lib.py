@@ -1,0 +1,61 @@
+"""Loads libcoconut_hip.so (built in-tree by `make -C coconut-rust_amd`) and declares the C ABI
+of include/coconut_hip.h.  No fallback: a missing library is an ImportError."""
+import ctypes
+import os
+
+from .errors import CoconutError
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("COCONUT_HIP_LIB", os.path.join(os.path.dirname(_HERE), "libcoconut_hip.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"libcoconut_hip.so not built at {LIB_PATH}: run `make -C coconut-rust_amd` "
+                      "(or __graft_entry__.build()); there is no CPU fallback")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+c_sz = ctypes.c_size_t
+c_p = ctypes.c_void_p
+c_int = ctypes.c_int
+u8p = ctypes.c_char_p
+
+_SIGS = {
+    "cc_status_str": (ctypes.c_char_p, [c_int]),
+    "cc_version": (ctypes.c_char_p, []),
+    "cc_ctx_create": (c_int, [c_int, c_int, ctypes.POINTER(c_p)]),
+    "cc_ctx_destroy": (c_int, [c_p]),
+    "cc_ctx_mode": (c_int, [c_p, ctypes.POINTER(c_int)]),
+    "cc_set_params": (c_int, [c_p, c_p]),
+    "cc_set_verkey": (c_int, [c_p, c_p, c_p, c_sz]),
+    "cc_verify_batch": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int]),
+    "cc_verify_batch_device": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "cc_signature_aggregate_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p]),
+    "cc_verkey_aggregate_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p]),
+    "cc_pok_verify_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                    c_p, c_p]),
+    "cc_last_timing": (c_int, [c_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
+                               ctypes.POINTER(ctypes.c_float)]),
+    "cc_set_timing": (c_int, [c_p, c_int]),
+}
+
+for _name, (_res, _args) in _SIGS.items():
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+def check(status: int, what: str = ""):
+    if status != 0:
+        raise CoconutError(status, f"{what}: {lib.cc_status_str(status).decode()}")
+
+
+def buf(b):
+    """bytes/bytearray/numpy -> (ctypes pointer, keepalive)."""
+    if b is None:
+        return None, None
+    if isinstance(b, (bytes, bytearray)):
+        cb = ctypes.create_string_buffer(bytes(b), len(b)) if len(b) else ctypes.create_string_buffer(1)
+        return ctypes.cast(cb, c_p), cb
+    import numpy as np
+    a = np.ascontiguousarray(b)
+    return ctypes.c_void_p(a.ctypes.data), a

@@ -1,0 +1,229 @@
+"""Signature / Verkey / Params — host mirror of reference src/signature.rs (verifier side).
+
+The reference API (signature.rs:448-526) is kept name-for-name:
+
+* ``Signature.verify(messages, vk, params)``              -> signature.rs:473-478
+* ``Signature.aggregate(threshold, [(id, Signature)])``   -> signature.rs:448-470
+* ``Verkey.aggregate(threshold, [(id, Verkey)])``         -> signature.rs:483-526
+
+plus batch entry points (``verify_batch``, ``signature_aggregate_batch``,
+``verkey_aggregate_batch``) that hand whole batches to the GPU through the C ABI
+(include/coconut_hip.h).  Group elements are carried as amcl_wrapper ``to_bytes`` encodings
+(G1 97 B, G2 192 B), scalars as 48-byte big-endian Fr.  Where the reference panics (assert!,
+unwrap on PSError) these raise ``CoconutError`` with the matching kind.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from dataclasses import dataclass, field
+from typing import List, Sequence, Tuple, Union
+
+import numpy as np
+
+from ._lib import buf, check, lib
+from .errors import CoconutError
+
+FR_BYTES = 48
+G1_BYTES = 97
+G2_BYTES = 192
+GT_BYTES = 576
+R_ORDER = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+class GroupMode(enum.IntEnum):
+    """Reference src/lib.rs:3-4 feature mutex; SIG_G2 is the default build."""
+    SIG_G2 = 0  # sigma, g, h in G2; X~, Y~, g~ in G1
+    SIG_G1 = 1  # sigma, g, h in G1; X~, Y~, g~ in G2
+
+    @property
+    def sig_bytes(self) -> int:
+        return G2_BYTES if self == GroupMode.SIG_G2 else G1_BYTES
+
+    @property
+    def other_bytes(self) -> int:
+        return G1_BYTES if self == GroupMode.SIG_G2 else G2_BYTES
+
+
+def fr_bytes(m: Union[int, bytes]) -> bytes:
+    if isinstance(m, (bytes, bytearray)):
+        if len(m) != FR_BYTES:
+            raise CoconutError(-4, "Fr must be 48 bytes")
+        return bytes(m)
+    return int(m % R_ORDER).to_bytes(FR_BYTES, "big")
+
+
+@dataclass
+class Params:
+    """signature.rs:13-17.  Only g_tilde is read on the verify path."""
+    g: bytes
+    g_tilde: bytes
+    h: List[bytes] = field(default_factory=list)
+
+    def msg_count(self) -> int:
+        return len(self.h)
+
+
+@dataclass
+class Verkey:
+    """signature.rs:46-49."""
+    X_tilde: bytes
+    Y_tilde: List[bytes]
+
+    @staticmethod
+    def aggregate(threshold: int, keys: Sequence[Tuple[int, "Verkey"]], ctx: "Context" = None) -> "Verkey":
+        """signature.rs:483-526 (q+1 Lagrange-weighted MSMs over the first `threshold` keys)."""
+        ctx = ctx or Context.default()
+        if len(keys) < threshold:
+            raise CoconutError(-3, "keys.len() < threshold")
+        q = len(keys[0][1].Y_tilde)
+        for _, vk in keys[1:]:
+            if len(vk.Y_tilde) != q:
+                raise CoconutError(-3, "ragged verkeys (reference assert_eq! at signature.rs:486-488)")
+        ids = np.array([[i for i, _ in keys]], dtype=np.uint64)
+        X = b"".join(vk.X_tilde for _, vk in keys)
+        Y = b"".join(y for _, vk in keys for y in vk.Y_tilde)
+        oX, oY = verkey_aggregate_batch(ctx, 1, len(keys), threshold, q, ids, X, Y)
+        ob = ctx.mode.other_bytes
+        return Verkey(oX, [oY[j * ob:(j + 1) * ob] for j in range(q)])
+
+
+@dataclass
+class Signature:
+    """signature.rs:68-71."""
+    sigma_1: bytes
+    sigma_2: bytes
+
+    @staticmethod
+    def aggregate(threshold: int, sigs: Sequence[Tuple[int, "Signature"]], ctx: "Context" = None) -> "Signature":
+        """signature.rs:448-470: sigma_1 from entry 0, sigma_2 = sum l_i(0) sigma_2_i over the first t."""
+        ctx = ctx or Context.default()
+        if len(sigs) < threshold or not sigs:
+            raise CoconutError(-3, "sigs.len() < threshold")
+        ids = np.array([[i for i, _ in sigs]], dtype=np.uint64)
+        s1 = b"".join(s.sigma_1 for _, s in sigs)
+        s2 = b"".join(s.sigma_2 for _, s in sigs)
+        o1, o2 = signature_aggregate_batch(ctx, 1, len(sigs), threshold, ids, s1, s2)
+        return Signature(o1, o2)
+
+    def verify(self, messages: Sequence[Union[int, bytes]], vk: Verkey, params: Params,
+               ctx: "Context" = None) -> bool:
+        """signature.rs:473-478 -> ps_sig Signature::verify: one credential through the batch path."""
+        ctx = ctx or Context.default()
+        if len(vk.Y_tilde) != len(messages):
+            raise CoconutError(-1, f"Verkey valid for {len(vk.Y_tilde)} messages but given {len(messages)}")
+        ctx.set_params(params.g_tilde)
+        msgs = b"".join(fr_bytes(m) for m in messages)
+        v = verify_batch(ctx, 1, len(messages), self.sigma_1, self.sigma_2, msgs,
+                         vk=(vk.X_tilde, b"".join(vk.Y_tilde)))
+        return bool(v[0])
+
+
+class Context:
+    """One cc_ctx: a HIP device, a stream and device-resident params/verkey tables."""
+
+    _default = {}
+
+    def __init__(self, device: int = 0, mode: GroupMode = GroupMode.SIG_G2):
+        self.mode = GroupMode(mode)
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib.cc_ctx_create(device, int(self.mode), ctypes.byref(h)), "cc_ctx_create")
+        self.h = h
+        self._gtilde = None
+        self._vk = None
+
+    @classmethod
+    def default(cls, device: int = 0, mode: GroupMode = GroupMode.SIG_G2) -> "Context":
+        key = (device, int(mode))
+        if key not in cls._default:
+            cls._default[key] = Context(device, mode)
+        return cls._default[key]
+
+    def close(self):
+        if self.h:
+            lib.cc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_params(self, g_tilde: bytes):
+        if self._gtilde == g_tilde:
+            return
+        p, keep = buf(g_tilde)
+        check(lib.cc_set_params(self.h, p), "cc_set_params")
+        self._gtilde = g_tilde
+
+    def set_verkey(self, X: bytes, Y: Sequence[bytes]):
+        Yb = b"".join(Y) if not isinstance(Y, (bytes, bytearray)) else bytes(Y)
+        key = (bytes(X), Yb)
+        if self._vk == key:
+            return
+        q = len(Yb) // self.mode.other_bytes
+        px, k1 = buf(X)
+        py, k2 = buf(Yb)
+        check(lib.cc_set_verkey(self.h, px, py, q), "cc_set_verkey")
+        self._vk = key
+
+    def timing(self, enabled: bool = True):
+        check(lib.cc_set_timing(self.h, int(enabled)))
+
+    def last_timing(self):
+        a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
+        check(lib.cc_last_timing(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
+
+
+def verify_batch(ctx: Context, n: int, q: int, sigma1: bytes, sigma2: bytes, msgs: bytes, vk=None,
+                 want_gt: bool = False, rlc: bool = False):
+    """Batch Signature::verify.  vk=None uses the context's shared verkey (cc_set_verkey);
+    vk=(X_bytes, Y_bytes) gives one verkey per credential (n*ob, n*q*ob) or a single verkey
+    that is broadcast when len(X) == ob.  Returns verdicts (uint8[n]) [, gts (n*576 bytes)]."""
+    ob = ctx.mode.other_bytes
+    if vk is not None and len(vk[0]) == ob and n != 1:
+        ctx.set_verkey(vk[0], vk[1])
+        vk = None
+    verdicts = np.zeros(max(n, 1), dtype=np.uint8)
+    gts = np.zeros(max(n, 1) * GT_BYTES, dtype=np.uint8) if want_gt else None
+    p1, k1 = buf(sigma1)
+    p2, k2 = buf(sigma2)
+    pm, k3 = buf(msgs)
+    px, k4 = buf(vk[0]) if vk is not None else (None, None)
+    py, k5 = buf(vk[1]) if vk is not None else (None, None)
+    check(lib.cc_verify_batch(ctx.h, n, q, p1, p2, pm, px, py,
+                              ctypes.c_void_p(verdicts.ctypes.data),
+                              ctypes.c_void_p(gts.ctypes.data) if want_gt else None, int(rlc)),
+          "cc_verify_batch")
+    if want_gt:
+        return verdicts[:n], gts[:n * GT_BYTES].tobytes()
+    return verdicts[:n]
+
+
+def signature_aggregate_batch(ctx: Context, n: int, length: int, t: int, ids, sigma1: bytes, sigma2: bytes):
+    sb = ctx.mode.sig_bytes
+    ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64).reshape(n, length))
+    o1 = np.zeros(max(n, 1) * sb, dtype=np.uint8)
+    o2 = np.zeros(max(n, 1) * sb, dtype=np.uint8)
+    p1, k1 = buf(sigma1)
+    p2, k2 = buf(sigma2)
+    check(lib.cc_signature_aggregate_batch(ctx.h, n, length, t, ctypes.c_void_p(ids.ctypes.data), p1, p2,
+                                           ctypes.c_void_p(o1.ctypes.data), ctypes.c_void_p(o2.ctypes.data)),
+          "cc_signature_aggregate_batch")
+    return o1[:n * sb].tobytes(), o2[:n * sb].tobytes()
+
+
+def verkey_aggregate_batch(ctx: Context, n: int, length: int, t: int, q: int, ids, X: bytes, Y: bytes):
+    ob = ctx.mode.other_bytes
+    ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64).reshape(n, length))
+    oX = np.zeros(max(n, 1) * ob, dtype=np.uint8)
+    oY = np.zeros(max(n * q, 1) * ob, dtype=np.uint8)
+    px, k1 = buf(X)
+    py, k2 = buf(Y)
+    check(lib.cc_verkey_aggregate_batch(ctx.h, n, length, t, q, ctypes.c_void_p(ids.ctypes.data), px, py,
+                                        ctypes.c_void_p(oX.ctypes.data), ctypes.c_void_p(oY.ctypes.data)),
+          "cc_verkey_aggregate_batch")
+    return oX[:n * ob].tobytes(), oY[:n * q * ob].tobytes()

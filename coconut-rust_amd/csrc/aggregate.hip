@@ -1,0 +1,395 @@
+// Threshold aggregation and PoK-of-signature verification kernels for gfx950 (the product path).
+//
+//   k_lagrange     : secret_sharing `Polynomial::lagrange_basis_at_0` [EXT] over the de-duplicated
+//                    id set of the first t entries (reference src/signature.rs:454-463, 496-509)
+//   k_msm_tasks    : one Lagrange-weighted MSM per lane — Signature::aggregate (signature.rs:465,
+//                    SignatureGroup) and the q+1 MSMs of Verkey::aggregate (signature.rs:512-524,
+//                    OtherGroup); output encoded as amcl_wrapper `to_bytes`
+//   k_prep_pok     : ps_sig PoKOfSignatureProof::verify [EXT] (reference pok_sig.rs:103-105):
+//                    Schnorr check MSM(g~, Y~_hidden.., J; responses.., chal) == T, then
+//                    J' = X~ + J + sum_revealed Y~_i m_i, written in the verify kernels' Miller-loop
+//                    operand layout so k_miller_* / k_fexp finish the 2-pairing check.
+#include "codec.h"
+#include "pairing.h"
+
+using namespace cc;
+
+namespace {
+
+// ---------------------------------------------------------------- Fr (mod r) Montgomery, R = 2^256
+constexpr int NR = 8;
+#define CC_RR2 0xf3f29c6du, 0xc999e990u, 0x87925c23u, 0x2b6cedcbu, 0x7254398fu, 0x05d31496u, 0x9f59ff11u, 0x0748d9d9u
+#define CC_RONE 0xfffffffeu, 0x00000001u, 0x00034802u, 0x5884b7fau, 0xecbc4ff5u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u
+__constant__ static const uint32_t kRm2[NR] = {0xffffffffu, 0xfffffffeu, 0xfffe5bfeu, 0x53bda402u,
+                                               0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
+
+struct Fm {
+    uint32_t v[NR];
+};
+
+DEV uint32_t rl(int j) {
+    constexpr uint32_t Rl[NR] = {CC_R_LIMBS};
+    return Rl[j];
+}
+
+DEV void fm_reduce_once(Fm& r, const uint32_t t[NR]) {
+    uint32_t s[NR], br = 0;
+#pragma unroll
+    for (int j = 0; j < NR; j++) s[j] = __builtin_subc(t[j], rl(j), br, &br);
+#pragma unroll
+    for (int j = 0; j < NR; j++) r.v[j] = br ? t[j] : s[j];
+}
+
+static __device__ __noinline__ Fm fm_mul_v(Fm a, Fm b) {
+    uint32_t t[NR];
+#pragma unroll
+    for (int i = 0; i < NR; i++) {
+        const uint32_t bi = b.v[i];
+        uint64_t A = (uint64_t)a.v[0] * bi + (i ? t[0] : 0u);
+        const uint32_t t0 = (uint32_t)A;
+        const uint32_t m = t0 * 0xffffffffu;  // -r^-1 mod 2^32
+        uint64_t C = (uint64_t)m * rl(0) + t0;
+#pragma unroll
+        for (int j = 1; j < NR; j++) {
+            A = (uint64_t)a.v[j] * bi + (uint64_t)(i ? t[j] : 0u) + (A >> 32);
+            C = (uint64_t)m * rl(j) + (uint64_t)(uint32_t)A + (C >> 32);
+            t[j - 1] = (uint32_t)C;
+        }
+        t[NR - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+    }
+    Fm r;
+    fm_reduce_once(r, t);
+    return r;
+}
+
+DEV void fm_sub(Fm& r, const Fm& a, const Fm& b) {
+    uint32_t t[NR], br = 0;
+#pragma unroll
+    for (int j = 0; j < NR; j++) t[j] = __builtin_subc(a.v[j], b.v[j], br, &br);
+    uint32_t mask = 0u - br, c = 0;
+#pragma unroll
+    for (int j = 0; j < NR; j++) r.v[j] = __builtin_addc(t[j], rl(j) & mask, c, &c);
+}
+
+DEV Fm fm_from_u64(uint64_t x) {
+    constexpr uint32_t R2[NR] = {CC_RR2};
+    Fm a, r2;
+#pragma unroll
+    for (int j = 0; j < NR; j++) {
+        a.v[j] = 0;
+        r2.v[j] = R2[j];
+    }
+    a.v[0] = (uint32_t)x;
+    a.v[1] = (uint32_t)(x >> 32);
+    return fm_mul_v(a, r2);  // x < 2^64 < r
+}
+
+DEV Fm fm_one() {
+    constexpr uint32_t O[NR] = {CC_RONE};
+    Fm a;
+#pragma unroll
+    for (int j = 0; j < NR; j++) a.v[j] = O[j];
+    return a;
+}
+
+DEV Fm fm_inv(const Fm& a) {
+    Fm acc = a;
+    for (int bit = 254 - 1; bit >= 0; bit--) {  // r - 2 has its top bit at 254
+        acc = fm_mul_v(acc, acc);
+        if ((kRm2[bit >> 5] >> (bit & 31)) & 1u) acc = fm_mul_v(acc, a);
+    }
+    return acc;
+}
+
+DEV Fm fm_to_canon(const Fm& a) {
+    Fm one;
+#pragma unroll
+    for (int j = 0; j < NR; j++) one.v[j] = 0;
+    one.v[0] = 1;
+    return fm_mul_v(a, one);
+}
+
+// ---------------------------------------------------------------- SoA helpers (local copies)
+struct Soa {
+    uint32_t* p;
+    size_t n;
+};
+DEV void st_fp(const Soa& s, size_t slot, size_t i, const Fp& x) {
+#pragma unroll
+    for (int k = 0; k < NL; k++) s.p[(slot * NL + k) * s.n + i] = x.v[k];
+}
+DEV void ld_fp(Fp& x, const Soa& s, size_t slot, size_t i) {
+#pragma unroll
+    for (int k = 0; k < NL; k++) x.v[k] = s.p[(slot * NL + k) * s.n + i];
+}
+
+template <class F>
+DEV bool decode_pt(Aff<F>& a, const uint8_t* p);
+template <>
+DEV bool decode_pt<Fp>(Aff<Fp>& a, const uint8_t* p) { return g1_decode(a, p); }
+template <>
+DEV bool decode_pt<Fp2>(Aff<Fp2>& a, const uint8_t* p) { return g2_decode(a, p); }
+
+template <class F>
+DEV void encode_pt(uint8_t* p, const Aff<F>& a, bool finite);
+template <>
+DEV void encode_pt<Fp>(uint8_t* p, const Aff<Fp>& a, bool finite) { g1_encode(p, a, finite); }
+template <>
+DEV void encode_pt<Fp2>(uint8_t* p, const Aff<Fp2>& a, bool finite) { g2_encode(p, a, finite); }
+
+template <class F>
+constexpr int ebytes() { return sizeof(F) == sizeof(Fp) ? 97 : 192; }
+
+template <class F>
+DEV void ld_aff_aos(Aff<F>& a, const uint32_t* p) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(&a);
+    for (int k = 0; k < (int)(sizeof(Aff<F>) / 4); k++) d[k] = p[k];
+}
+
+constexpr int NWIN = 32, WENT = 255;
+
+// fixed-base: acc += k * B_j via the 8-bit window table of base j (k canonical, LE limbs)
+template <class F>
+DEV void add_fixed(Jac<F>& acc, const uint32_t kv[8], const uint32_t* table, int j) {
+    constexpr int EW = sizeof(Aff<F>) / 4;
+    const uint32_t* tj = table + (size_t)j * NWIN * WENT * EW;
+#pragma unroll 1
+    for (int w = 0; w < NWIN; w++) {
+        uint32_t d = (kv[w >> 2] >> (8 * (w & 3))) & 0xffu;
+        if (d) {
+            Aff<F> e;
+            ld_aff_aos<F>(e, tj + ((size_t)w * WENT + d - 1) * EW);
+            jac_add_aff(acc, acc, e);
+        }
+    }
+}
+
+}  // namespace
+
+// ================================================================ Lagrange coefficients
+// l[(cred * t + i) * 8 ..]: canonical l_i(0) for the i-th of the first t ids of credential `cred`.
+__global__ void k_lagrange(size_t n, size_t len, size_t t, const uint64_t* __restrict__ ids, uint32_t* __restrict__ l) {
+    size_t task = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (task >= n * t) return;
+    size_t cred = task / t, i = task % t;
+    const uint64_t* id = ids + cred * len;
+    const uint64_t xi = id[i];
+    Fm num = fm_one(), den = fm_one();
+    const Fm fxi = fm_from_u64(xi);
+    for (size_t j = 0; j < t; j++) {
+        const uint64_t xj = id[j];
+        if (xj == xi) continue;
+        bool dup = false;
+        for (size_t k = 0; k < j; k++)
+            if (id[k] == xj) { dup = true; break; }
+        if (dup) continue;  // HashSet semantics
+        Fm fxj = fm_from_u64(xj), d;
+        num = fm_mul_v(num, fxj);
+        fm_sub(d, fxj, fxi);
+        den = fm_mul_v(den, d);
+    }
+    Fm li = fm_to_canon(fm_mul_v(num, fm_inv(den)));
+    uint32_t* o = l + task * 8;
+    for (int k = 0; k < 8; k++) o[k] = li.v[k];
+}
+
+// ================================================================ Lagrange-weighted MSM tasks
+// task -> points at pts + (task / l_div) * pt_stride + (task % l_div) * pt_jstride + k * pt_step,
+// k < t; scalars l[(task / l_div) * t + k]; output encoding at out + task * ebytes.
+template <class F>
+__global__ __launch_bounds__(256) void k_msm_tasks(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
+                                                   size_t pt_stride, size_t pt_jstride, size_t pt_step,
+                                                   const uint32_t* __restrict__ l, size_t l_div,
+                                                   uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
+    size_t task = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (task >= ntask) return;
+    constexpr int FS = sizeof(F) / sizeof(Fp);
+    const size_t cred = task / l_div;
+    const uint8_t* base = pts + cred * pt_stride + (task % l_div) * pt_jstride;
+    const uint32_t* lk = l + cred * t * 8;
+    Soa S{scratch, ntask};
+    // decode once into the lane's scratch column (slot (k * 2FS + c)); inf flag in bit k of masks
+    for (size_t k = 0; k < t; k++) {
+        Aff<F> a;
+        bool ok = decode_pt<F>(a, base + k * pt_step);
+        if (!ok) {
+            // identity base contributes nothing: zero its scalar by marking x = y = 0 (flag below)
+        }
+        const Fp* pa = reinterpret_cast<const Fp*>(&a);
+        for (int c = 0; c < 2 * FS; c++) st_fp(S, k * 2 * FS + c, task, pa[c]);
+        // store flag in an extra slot word: use slot (t * 2FS) region, one word per k
+        S.p[(t * 2 * FS * NL + k) * S.n + task] = ok ? 0u : 1u;
+    }
+    Jac<F> acc;
+    jac_set_inf(acc);
+    for (int b = 254; b >= 0; b--) {
+        jac_dbl(acc, acc);
+        for (size_t k = 0; k < t; k++) {
+            uint32_t bit = (lk[k * 8 + (b >> 5)] >> (b & 31)) & 1u;
+            if (bit && !S.p[(t * 2 * FS * NL + k) * S.n + task]) {
+                Aff<F> a;
+                Fp* pa = reinterpret_cast<Fp*>(&a);
+                for (int c = 0; c < 2 * FS; c++) ld_fp(pa[c], S, k * 2 * FS + c, task);
+                jac_add_aff(acc, acc, a);
+            }
+        }
+    }
+    Aff<F> r;
+    bool fin = jac_to_aff(r, acc);
+    encode_pt<F>(out + task * ebytes<F>(), r, fin);
+}
+
+// ================================================================ PoK verify prep
+// Prep layout and flag bits as kernels.hip (Q1 0..3 | Q2 4..7 | P1 8..10 | P2 11..12),
+// plus flag bit3 = Schnorr check failed.
+enum { S_Q1 = 0, S_Q2 = 4, S_P1 = 8, S_P2 = 11 };
+
+template <class FS_, class FO>  // FS_: SignatureGroup field, FO: OtherGroup field
+__global__ __launch_bounds__(256) void k_prep_pok(size_t n, int q, int r, const uint8_t* __restrict__ s1b,
+                                                  const uint8_t* __restrict__ s2b, const uint8_t* __restrict__ Jb,
+                                                  const uint8_t* __restrict__ Tb, const uint8_t* __restrict__ resp,
+                                                  const uint8_t* __restrict__ chal,
+                                                  const uint8_t* __restrict__ rev_msgs,
+                                                  const uint32_t* __restrict__ rev_idx,
+                                                  const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                  const uint32_t* __restrict__ table,
+                                                  const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
+                                                  uint32_t* __restrict__ flags) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    constexpr bool kSigG2 = sizeof(FS_) == sizeof(Fp2);
+    constexpr int SB = ebytes<FS_>(), OB = ebytes<FO>();
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    // sigma'
+    {
+        Aff<FS_> a;
+        if (!decode_pt<FS_>(a, s1b + i * SB)) fl |= 1u;
+        const Fp* pa = reinterpret_cast<const Fp*>(&a);
+        if (kSigG2) {
+            for (int c = 0; c < 4; c++) st_fp(S, S_Q1 + c, i, pa[c]);
+        } else {
+            for (int c = 0; c < 2; c++) st_fp(S, S_P1 + c, i, pa[c]);
+        }
+        if (!decode_pt<FS_>(a, s2b + i * SB)) fl |= 2u;
+        FT<FS_>::neg(a.y, a.y);
+        if (kSigG2) {
+            for (int c = 0; c < 4; c++) st_fp(S, S_Q2 + c, i, pa[c]);
+        } else {
+            for (int c = 0; c < 2; c++) st_fp(S, S_P2 + c, i, pa[c]);
+        }
+    }
+    // Schnorr: acc = g~ * resp[0] + sum_hidden Y~_h * resp[k] + J * chal - T  ==  O ?
+    Aff<FO> Ja;
+    const bool Jok = decode_pt<FO>(Ja, Jb + i * OB);
+    Jac<FO> acc;
+    jac_set_inf(acc);
+    {
+        Fr k;
+        const uint8_t* rp = resp + i * (size_t)(q - r + 1) * 48;
+        fr_from_be48(k, rp);
+        if (!binf[q]) add_fixed<FO>(acc, k.v, table, q);  // table base q = g~
+        int slot = 1;
+        for (int h = 0; h < q; h++) {
+            bool revealed = false;
+            for (int z = 0; z < r; z++) revealed |= rev_idx[z] == (uint32_t)h;
+            if (revealed) continue;
+            fr_from_be48(k, rp + (size_t)slot * 48);
+            slot++;
+            if (!binf[h]) add_fixed<FO>(acc, k.v, table, h);
+        }
+        // J * chal (variable base)
+        fr_from_be48(k, chal + i * 48);
+        if (Jok) {
+            Jac<FO> s;
+            jac_set_inf(s);
+            for (int b = 254; b >= 0; b--) {
+                jac_dbl(s, s);
+                if ((k.v[b >> 5] >> (b & 31)) & 1u) jac_add_aff(s, s, Ja);
+            }
+            jac_add(acc, acc, s);
+        }
+        Aff<FO> Ta;
+        if (decode_pt<FO>(Ta, Tb + i * OB)) {
+            FT<FO>::neg(Ta.y, Ta.y);
+            jac_add_aff(acc, acc, Ta);
+        }
+        if (!jac_is_inf(acc)) fl |= 8u;
+    }
+    // J' = X~ + J + sum_revealed Y~_i m_i
+    Jac<FO> jp;
+    if (Xinf) {
+        jac_set_inf(jp);
+    } else {
+        Aff<FO> x;
+        ld_aff_aos<FO>(x, Xaff);
+        jac_from_aff(jp, x);
+    }
+    if (Jok) jac_add_aff(jp, jp, Ja);
+    for (int z = 0; z < r; z++) {
+        Fr m;
+        fr_from_be48(m, rev_msgs + ((size_t)i * r + z) * 48);
+        int h = (int)rev_idx[z];
+        if (!binf[h]) add_fixed<FO>(jp, m.v, table, h);
+    }
+    if (jac_is_inf(jp)) fl |= 4u;
+    if (kSigG2) {
+        // P1 = J' (G1) in line-evaluation form (X Z, Y, Z^3)
+        const Jac<Fp>& g = *reinterpret_cast<const Jac<Fp>*>(&jp);
+        Fp t;
+        fp_mul(t, g.x, g.z);
+        st_fp(S, S_P1, i, t);
+        st_fp(S, S_P1 + 1, i, g.y);
+        fp_sqr(t, g.z);
+        fp_mul(t, t, g.z);
+        st_fp(S, S_P1 + 2, i, t);
+    } else {
+        Aff<FO> a;
+        jac_to_aff(a, jp);
+        const Fp* pa = reinterpret_cast<const Fp*>(&a);
+        for (int c = 0; c < 4; c++) st_fp(S, S_Q1 + c, i, pa[c]);
+    }
+    flags[i] = fl;
+}
+
+static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+extern "C" {
+
+int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st) {
+    if (!n || !t) return 0;
+    hipLaunchKernelGGL(k_lagrange, dim3(nblocks(n * t, 64)), dim3(64), 0, st, n, len, t, d_ids, d_l);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// scratch: ntask * (t * 2 * FS * 12 + t) words
+int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
+                  size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
+                  hipStream_t st) {
+    if (!ntask) return 0;
+    dim3 g(nblocks(ntask, 64)), b(64);
+    if (group == 1)
+        hipLaunchKernelGGL(k_msm_tasks<Fp>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
+                           d_scratch, d_out);
+    else
+        hipLaunchKernelGGL(k_msm_tasks<Fp2>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
+                           d_scratch, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
+                 const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
+                 const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table,
+                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st) {
+    if (!n) return 0;
+    dim3 g(nblocks(n, 256)), b(256);
+    if (mode == 0)
+        hipLaunchKernelGGL((k_prep_pok<Fp2, Fp>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
+                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, d_binf, d_prep, d_flags);
+    else
+        hipLaunchKernelGGL((k_prep_pok<Fp, Fp2>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
+                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, d_binf, d_prep, d_flags);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,466 @@
+// C ABI implementation (include/coconut_hip.h): contexts, device tables, batch launches.
+// Host side of the MI355X engine; every compute step runs in the HIP kernels of kernels.hip /
+// aggregate.hip — there is no CPU fallback in this library.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/coconut_hip.h"
+
+extern "C" {
+int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_out, uint32_t* d_inf, hipStream_t st);
+int cck_build_table(int group, int nbases, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
+                    uint32_t* d_table, hipStream_t st);
+int cck_gtilde_lines(const uint32_t* d_gtilde_aff, uint32_t* d_lines, hipStream_t st);
+int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* d_Y, uint32_t* d_bases,
+                  uint32_t* d_binf, const uint8_t* d_msgs, uint8_t* d_msgs_canon, hipStream_t st);
+int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
+             const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, const uint32_t* d_binf_fixed,
+             uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
+int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
+               uint32_t* d_f, hipStream_t st);
+int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
+             uint8_t* d_gt, hipStream_t st);
+int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
+int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
+                  size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
+                  hipStream_t st);
+int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
+                 const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
+                 const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table,
+                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
+}
+
+namespace {
+
+constexpr int NWIN = 32, WENT = 255;
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t want) {
+        if (want <= bytes) return 0;
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (hipMalloc(&p, want) != hipSuccess) return -1;
+        bytes = want;
+        return 0;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+}  // namespace
+
+struct cc_ctx {
+    int device = 0;
+    int mode = 0;  // 0 SigG2, 1 SigG1
+    hipStream_t stream = nullptr;
+    // params
+    bool have_params = false;
+    DevBuf gtilde_aff;   // OtherGroup affine (Montgomery, AoS)
+    uint32_t gtilde_inf = 0;
+    DevBuf gtilde_lines; // SigG1: Miller lines of g~
+    // verkey
+    bool have_vk = false;
+    size_t q = 0;
+    DevBuf vk_aff;       // (q + 2) points: X~, Y~[q], g~ (AoS)
+    DevBuf vk_inf;       // (q + 2) flags
+    DevBuf table;        // fixed-base tables for Y~[0..q) and g~ (q + 1 bases)
+    DevBuf table_inf;    // q + 1 base flags
+    uint32_t X_inf = 0;
+    // workspaces
+    DevBuf in_s1, in_s2, in_msgs, in_vkX, in_vkY, in_aux[6];
+    DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, vkbinf, msgs_canon, lag;
+    // timing
+    bool timing = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float last_ms[3] = {0, 0, 0};
+};
+
+static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }
+static inline int oth_bytes(int mode) { return mode == 0 ? 97 : 192; }
+static inline int oth_group(int mode) { return mode == 0 ? 1 : 2; }
+static inline int sig_group(int mode) { return mode == 0 ? 2 : 1; }
+static inline size_t aff_words(int group) { return group == 1 ? 24 : 48; }
+
+#define HIPCK(x)                                  \
+    do {                                          \
+        if ((x) != hipSuccess) return CC_ERR_HIP; \
+    } while (0)
+#define KCK(x)                     \
+    do {                           \
+        if ((x) != 0) return CC_ERR_HIP; \
+    } while (0)
+
+extern "C" {
+
+const char* cc_status_str(int s) {
+    switch (s) {
+        case CC_OK: return "ok";
+        case CC_ERR_LEN: return "UnsupportedNoOfMessages";
+        case CC_ERR_BASES_EXPS: return "UnequalNoOfBasesExponents";
+        case CC_ERR_THRESHOLD: return "fewer entries than threshold";
+        case CC_ERR_DECODE: return "bad buffer / size";
+        case CC_ERR_HIP: return "HIP runtime error";
+        case CC_ERR_RCCL: return "RCCL error";
+        case CC_ERR_STATE: return "params/verkey not set";
+        default: return "unknown";
+    }
+}
+
+const char* cc_version(void) { return "coconut-mi355x 0.1.0 (gfx950)"; }
+
+cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
+    if (!out || (mode != CC_SIG_G2 && mode != CC_SIG_G1)) return CC_ERR_DECODE;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return CC_ERR_HIP;
+    HIPCK(hipSetDevice(device));
+    cc_ctx* c = new cc_ctx();
+    c->device = device;
+    c->mode = (int)mode;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return CC_ERR_HIP;
+    }
+    for (auto& e : c->ev) hipEventCreate(&e);
+    *out = c;
+    return CC_OK;
+}
+
+cc_status cc_ctx_destroy(cc_ctx* c) {
+    if (!c) return CC_OK;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
+                      &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
+                      &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag};
+    for (auto* b : bufs) b->release();
+    for (auto& b : c->in_aux) b.release();
+    for (auto& e : c->ev) if (e) hipEventDestroy(e);
+    hipStreamDestroy(c->stream);
+    delete c;
+    return CC_OK;
+}
+
+cc_status cc_ctx_mode(const cc_ctx* c, int* m) {
+    if (!c || !m) return CC_ERR_DECODE;
+    *m = c->mode;
+    return CC_OK;
+}
+
+cc_status cc_set_timing(cc_ctx* c, int enabled) {
+    if (!c) return CC_ERR_DECODE;
+    c->timing = enabled != 0;
+    return CC_OK;
+}
+
+cc_status cc_last_timing(const cc_ctx* c, float* a, float* b, float* d) {
+    if (!c) return CC_ERR_DECODE;
+    if (a) *a = c->last_ms[0];
+    if (b) *b = c->last_ms[1];
+    if (d) *d = c->last_ms[2];
+    return CC_OK;
+}
+
+static cc_status decode_points_host(cc_ctx* c, int group, size_t n, const uint8_t* bytes, uint32_t* d_out,
+                                    uint32_t* d_inf) {
+    size_t eb = group == 1 ? 97 : 192;
+    DevBuf tmp;
+    if (tmp.ensure(eb * n + 16)) return CC_ERR_HIP;
+    HIPCK(hipMemcpyAsync(tmp.p, bytes, eb * n, hipMemcpyHostToDevice, c->stream));
+    KCK(cck_decode_points(group, n, tmp.as<uint8_t>(), d_out, d_inf, c->stream));
+    HIPCK(hipStreamSynchronize(c->stream));
+    tmp.release();
+    return CC_OK;
+}
+
+static cc_status rebuild_tables(cc_ctx* c) {
+    // bases for the fixed-base tables: Y~[0..q) then g~ (PoK Schnorr base) -> q + 1 bases
+    int og = oth_group(c->mode);
+    size_t aw = aff_words(og);
+    int nb = (int)c->q + 1;
+    if (c->table.ensure((size_t)nb * NWIN * WENT * aw * 4)) return CC_ERR_HIP;
+    if (c->table_inf.ensure((size_t)nb * 4)) return CC_ERR_HIP;
+    // assemble [Y~..., g~] contiguous from vk_aff (X~ at 0, Y~ at 1..q, g~ at q+1)
+    HIPCK(hipMemcpyAsync(c->table_inf.p, c->vk_inf.as<uint32_t>() + 1, (size_t)nb * 4, hipMemcpyDeviceToDevice,
+                         c->stream));
+    DevBuf pw;
+    if (pw.ensure((size_t)nb * NWIN * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
+    KCK(cck_build_table(og, nb, c->vk_aff.as<uint32_t>() + aw, c->table_inf.as<uint32_t>(), pw.as<uint32_t>(),
+                        c->table.as<uint32_t>(), c->stream));
+    HIPCK(hipStreamSynchronize(c->stream));
+    pw.release();
+    return CC_OK;
+}
+
+cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
+    if (!c || !g_tilde) return CC_ERR_DECODE;
+    HIPCK(hipSetDevice(c->device));
+    int og = oth_group(c->mode);
+    size_t aw = aff_words(og);
+    if (c->gtilde_aff.ensure(aw * 4)) return CC_ERR_HIP;
+    DevBuf inf;
+    if (inf.ensure(4)) return CC_ERR_HIP;
+    cc_status s = decode_points_host(c, og, 1, g_tilde, c->gtilde_aff.as<uint32_t>(), inf.as<uint32_t>());
+    if (s) return s;
+    HIPCK(hipMemcpy(&c->gtilde_inf, inf.p, 4, hipMemcpyDeviceToHost));
+    inf.release();
+    if (c->mode == 1) {
+        if (c->gtilde_lines.ensure(68 * 72 * 4)) return CC_ERR_HIP;
+        KCK(cck_gtilde_lines(c->gtilde_aff.as<uint32_t>(), c->gtilde_lines.as<uint32_t>(), c->stream));
+        HIPCK(hipStreamSynchronize(c->stream));
+    }
+    c->have_params = true;
+    if (c->have_vk) {
+        // refresh g~ slot of the verkey block and its table
+        HIPCK(hipMemcpy(c->vk_aff.as<uint32_t>() + (c->q + 1) * aw, c->gtilde_aff.p, aw * 4, hipMemcpyDeviceToDevice));
+        HIPCK(hipMemcpy(c->vk_inf.as<uint32_t>() + (c->q + 1), &c->gtilde_inf, 4, hipMemcpyHostToDevice));
+        return rebuild_tables(c);
+    }
+    return CC_OK;
+}
+
+cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q) {
+    if (!c || !X || (q && !Y) || q > 4096) return CC_ERR_DECODE;
+    if (!c->have_params) return CC_ERR_STATE;
+    HIPCK(hipSetDevice(c->device));
+    int og = oth_group(c->mode);
+    size_t eb = (size_t)oth_bytes(c->mode), aw = aff_words(og);
+    std::vector<uint8_t> all((q + 1) * eb);
+    memcpy(all.data(), X, eb);
+    if (q) memcpy(all.data() + eb, Y, q * eb);
+    if (c->vk_aff.ensure((q + 2) * aw * 4) || c->vk_inf.ensure((q + 2) * 4)) return CC_ERR_HIP;
+    cc_status s = decode_points_host(c, og, q + 1, all.data(), c->vk_aff.as<uint32_t>(), c->vk_inf.as<uint32_t>());
+    if (s) return s;
+    HIPCK(hipMemcpy(c->vk_aff.as<uint32_t>() + (q + 1) * aw, c->gtilde_aff.p, aw * 4, hipMemcpyDeviceToDevice));
+    HIPCK(hipMemcpy(c->vk_inf.as<uint32_t>() + (q + 1), &c->gtilde_inf, 4, hipMemcpyHostToDevice));
+    HIPCK(hipMemcpy(&c->X_inf, c->vk_inf.p, 4, hipMemcpyDeviceToHost));
+    c->q = q;
+    c->have_vk = true;
+    return rebuild_tables(c);
+}
+
+static cc_status ensure_work(cc_ctx* c, size_t n) {
+    size_t words = n * 12;  // one Fp slot
+    if (c->prep.ensure(words * 4 * 13) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
+        c->scratch.ensure(words * 4 * 12) || c->verdicts.ensure(n))
+        return CC_ERR_HIP;
+    return CC_OK;
+}
+
+// the three verify launches on device buffers; timing per phase when enabled
+static cc_status launch_verify(cc_ctx* c, size_t n, size_t q, int fixed, const uint8_t* d_s1, const uint8_t* d_s2,
+                               const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
+    if (c->timing) hipEventRecord(c->ev[0], st);
+    KCK(cck_prep(c->mode, fixed, n, (int)q, d_s1, d_s2, d_msgs, c->vk_aff.as<uint32_t>(), c->X_inf,
+                 c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(), c->vkb.as<uint32_t>(),
+                 c->vkbinf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
+    if (c->timing) hipEventRecord(c->ev[1], st);
+    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
+    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
+    if (c->timing) hipEventRecord(c->ev[2], st);
+    KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(), d_verdicts, d_gt, st));
+    if (c->timing) hipEventRecord(c->ev[3], st);
+    return CC_OK;
+}
+
+static void collect_timing(cc_ctx* c) {
+    if (!c->timing) return;
+    hipEventSynchronize(c->ev[3]);
+    for (int k = 0; k < 3; k++) hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
+}
+
+cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s1, const uint8_t* d_s2,
+                                 const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt, void* stream) {
+    if (!c || (n && (!d_s1 || !d_s2 || !d_verdicts))) return CC_ERR_DECODE;
+    if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
+    if (q != c->q) return CC_ERR_LEN;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    cc_status s = ensure_work(c, n);
+    if (s) return s;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    s = launch_verify(c, n, q, 1, d_s1, d_s2, d_msgs, d_verdicts, d_gt, st);
+    if (s) return s;
+    if (c->timing) collect_timing(c);
+    return CC_OK;
+}
+
+cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, const uint8_t* s2, const uint8_t* msgs,
+                          const uint8_t* vkX, const uint8_t* vkY, uint8_t* verdicts, uint8_t* gt, int rlc) {
+    (void)rlc;  // RLC mode: see cc_verify_batch_rlc in rlc.cpp (per-credential here)
+    if (!c || (n && (!s1 || !s2 || !verdicts || (q && !msgs)))) return CC_ERR_DECODE;
+    if (!c->have_params) return CC_ERR_STATE;
+    const bool per_vk = vkX != nullptr;
+    if (per_vk && q && !vkY) return CC_ERR_DECODE;
+    if (!per_vk) {
+        if (!c->have_vk) return CC_ERR_STATE;
+        if (q != c->q) return CC_ERR_LEN;
+    }
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    size_t sb = (size_t)sig_bytes(c->mode), ob = (size_t)oth_bytes(c->mode);
+    if (c->in_s1.ensure(n * sb) || c->in_s2.ensure(n * sb) || c->in_msgs.ensure(n * q * 48 + 16) ||
+        c->verdicts.ensure(n) || (gt && c->gt.ensure(n * 576)))
+        return CC_ERR_HIP;
+    cc_status s = ensure_work(c, n);
+    if (s) return s;
+    hipStream_t st = c->stream;
+    HIPCK(hipMemcpyAsync(c->in_s1.p, s1, n * sb, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(c->in_s2.p, s2, n * sb, hipMemcpyHostToDevice, st));
+    if (q) HIPCK(hipMemcpyAsync(c->in_msgs.p, msgs, n * q * 48, hipMemcpyHostToDevice, st));
+    const uint8_t* d_msgs = c->in_msgs.as<uint8_t>();
+    if (per_vk) {
+        int og = oth_group(c->mode);
+        size_t fs = og == 1 ? 1 : 2;  // Fp slots per coordinate
+        if (c->in_vkX.ensure(n * ob) || c->in_vkY.ensure(n * q * ob + 16) ||
+            c->vkb.ensure(n * 12 * 4 * 2 * fs * (q + 1)) || c->vkbinf.ensure(n * 4 * (q + 1)) ||
+            c->msgs_canon.ensure(n * q * 48 + 16))
+            return CC_ERR_HIP;
+        HIPCK(hipMemcpyAsync(c->in_vkX.p, vkX, n * ob, hipMemcpyHostToDevice, st));
+        if (q) HIPCK(hipMemcpyAsync(c->in_vkY.p, vkY, n * q * ob, hipMemcpyHostToDevice, st));
+        KCK(cck_decode_vk(c->mode, n, (int)q, c->in_vkX.as<uint8_t>(), c->in_vkY.as<uint8_t>(), c->vkb.as<uint32_t>(),
+                          c->vkbinf.as<uint32_t>(), d_msgs, c->msgs_canon.as<uint8_t>(), st));
+        d_msgs = c->msgs_canon.as<uint8_t>();
+    }
+    s = launch_verify(c, n, q, per_vk ? 0 : 1, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), d_msgs,
+                      c->verdicts.as<uint8_t>(), gt ? c->gt.as<uint8_t>() : nullptr, st);
+    if (s) return s;
+    HIPCK(hipMemcpyAsync(verdicts, c->verdicts.p, n, hipMemcpyDeviceToHost, st));
+    if (gt) HIPCK(hipMemcpyAsync(gt, c->gt.p, n * 576, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    collect_timing(c);
+    return CC_OK;
+}
+
+cc_status cc_signature_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* ids,
+                                       const uint8_t* s1, const uint8_t* s2, uint8_t* out_s1, uint8_t* out_s2) {
+    if (!c || (n && (!ids || !s1 || !s2 || !out_s1 || !out_s2))) return CC_ERR_DECODE;
+    if (len < t || len == 0) return CC_ERR_THRESHOLD;  // reference: assert!(sigs.len() >= threshold) + sigs[0]
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    size_t sb = (size_t)sig_bytes(c->mode);
+    int sg = sig_group(c->mode);
+    size_t fs = sg == 1 ? 1 : 2;
+    hipStream_t st = c->stream;
+    DevBuf& d_ids = c->in_aux[0];
+    DevBuf& d_pts = c->in_aux[1];
+    DevBuf& d_out = c->in_aux[2];
+    if (d_ids.ensure(n * len * 8) || d_pts.ensure(n * len * sb) || d_out.ensure(n * sb) ||
+        c->lag.ensure(n * (t ? t : 1) * 32) || c->scratch.ensure(n * (t * 2 * fs * 12 + t + 1) * 4))
+        return CC_ERR_HIP;
+    HIPCK(hipMemcpyAsync(d_ids.p, ids, n * len * 8, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_pts.p, s2, n * len * sb, hipMemcpyHostToDevice, st));
+    KCK(cck_lagrange(n, len, t, d_ids.as<uint64_t>(), c->lag.as<uint32_t>(), st));
+    KCK(cck_msm_tasks(sg, n, t, d_pts.as<uint8_t>(), len * sb, 0, sb, c->lag.as<uint32_t>(), 1,
+                      c->scratch.as<uint32_t>(), d_out.as<uint8_t>(), st));
+    HIPCK(hipMemcpyAsync(out_s2, d_out.p, n * sb, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    for (size_t i = 0; i < n; i++) memcpy(out_s1 + i * sb, s1 + i * len * sb, sb);  // sigma_1 = sigs[0].sigma_1
+    return CC_OK;
+}
+
+cc_status cc_verkey_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, size_t q, const uint64_t* ids,
+                                    const uint8_t* X, const uint8_t* Y, uint8_t* outX, uint8_t* outY) {
+    if (!c || (n && (!ids || !X || !outX || (q && (!Y || !outY))))) return CC_ERR_DECODE;
+    if (len < t || len == 0) return CC_ERR_THRESHOLD;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    size_t ob = (size_t)oth_bytes(c->mode);
+    int og = oth_group(c->mode);
+    size_t fs = og == 1 ? 1 : 2;
+    hipStream_t st = c->stream;
+    DevBuf& d_ids = c->in_aux[0];
+    DevBuf& d_X = c->in_aux[1];
+    DevBuf& d_Y = c->in_aux[3];
+    DevBuf& d_oX = c->in_aux[2];
+    DevBuf& d_oY = c->in_aux[4];
+    size_t ntask_y = n * q;
+    size_t maxtask = ntask_y > n ? ntask_y : n;
+    if (d_ids.ensure(n * len * 8) || d_X.ensure(n * len * ob) || d_Y.ensure(n * len * q * ob + 16) ||
+        d_oX.ensure(n * ob) || d_oY.ensure(ntask_y * ob + 16) || c->lag.ensure(n * (t ? t : 1) * 32) ||
+        c->scratch.ensure(maxtask * (t * 2 * fs * 12 + t + 1) * 4))
+        return CC_ERR_HIP;
+    HIPCK(hipMemcpyAsync(d_ids.p, ids, n * len * 8, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_X.p, X, n * len * ob, hipMemcpyHostToDevice, st));
+    if (q) HIPCK(hipMemcpyAsync(d_Y.p, Y, n * len * q * ob, hipMemcpyHostToDevice, st));
+    KCK(cck_lagrange(n, len, t, d_ids.as<uint64_t>(), c->lag.as<uint32_t>(), st));
+    KCK(cck_msm_tasks(og, n, t, d_X.as<uint8_t>(), len * ob, 0, ob, c->lag.as<uint32_t>(), 1,
+                      c->scratch.as<uint32_t>(), d_oX.as<uint8_t>(), st));
+    if (q)
+        KCK(cck_msm_tasks(og, ntask_y, t, d_Y.as<uint8_t>(), len * q * ob, ob, q * ob, c->lag.as<uint32_t>(), q,
+                          c->scratch.as<uint32_t>(), d_oY.as<uint8_t>(), st));
+    HIPCK(hipMemcpyAsync(outX, d_oX.p, n * ob, hipMemcpyDeviceToHost, st));
+    if (q) HIPCK(hipMemcpyAsync(outY, d_oY.p, ntask_y * ob, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    return CC_OK;
+}
+
+cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nresp, const uint8_t* s1,
+                              const uint8_t* s2, const uint8_t* J, const uint8_t* T, const uint8_t* resp,
+                              const uint8_t* chal, const uint64_t* rev_idx, const uint8_t* rev_msgs,
+                              uint8_t* verdicts, uint8_t* gt) {
+    if (!c || (n && (!s1 || !s2 || !J || !T || !chal || !verdicts || (nresp && !resp) || (r && (!rev_idx || !rev_msgs)))))
+        return CC_ERR_DECODE;
+    if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
+    if (q != c->q) return CC_ERR_LEN;
+    std::vector<uint32_t> idx(r ? r : 1);
+    for (size_t z = 0; z < r; z++) {
+        if (rev_idx[z] >= q) return CC_ERR_LEN;  // reference would index out of bounds (panic)
+        for (size_t y = 0; y < z; y++)
+            if (rev_idx[y] == rev_idx[z]) return CC_ERR_DECODE;  // HashMap keys are unique
+        idx[z] = (uint32_t)rev_idx[z];
+    }
+    if (nresp != q - r + 1) return CC_ERR_BASES_EXPS;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    size_t sb = (size_t)sig_bytes(c->mode), ob = (size_t)oth_bytes(c->mode);
+    hipStream_t st = c->stream;
+    DevBuf& dJ = c->in_aux[0];
+    DevBuf& dT = c->in_aux[1];
+    DevBuf& dR = c->in_aux[2];
+    DevBuf& dC = c->in_aux[3];
+    DevBuf& dM = c->in_aux[4];
+    DevBuf& dI = c->in_aux[5];
+    if (c->in_s1.ensure(n * sb) || c->in_s2.ensure(n * sb) || dJ.ensure(n * ob) || dT.ensure(n * ob) ||
+        dR.ensure(n * nresp * 48 + 16) || dC.ensure(n * 48) || dM.ensure(n * r * 48 + 16) || dI.ensure(r * 4 + 4) ||
+        c->verdicts.ensure(n) || (gt && c->gt.ensure(n * 576)))
+        return CC_ERR_HIP;
+    cc_status s = ensure_work(c, n);
+    if (s) return s;
+    HIPCK(hipMemcpyAsync(c->in_s1.p, s1, n * sb, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(c->in_s2.p, s2, n * sb, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(dJ.p, J, n * ob, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(dT.p, T, n * ob, hipMemcpyHostToDevice, st));
+    if (nresp) HIPCK(hipMemcpyAsync(dR.p, resp, n * nresp * 48, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(dC.p, chal, n * 48, hipMemcpyHostToDevice, st));
+    if (r) {
+        HIPCK(hipMemcpyAsync(dM.p, rev_msgs, n * r * 48, hipMemcpyHostToDevice, st));
+        HIPCK(hipMemcpyAsync(dI.p, idx.data(), r * 4, hipMemcpyHostToDevice, st));
+    }
+    KCK(cck_prep_pok(c->mode, n, (int)q, (int)r, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), dJ.as<uint8_t>(),
+                     dT.as<uint8_t>(), dR.as<uint8_t>(), dC.as<uint8_t>(), dM.as<uint8_t>(), dI.as<uint32_t>(),
+                     c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(),
+                     c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
+    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
+    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
+    KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(),
+                 c->verdicts.as<uint8_t>(), gt ? c->gt.as<uint8_t>() : nullptr, st));
+    HIPCK(hipMemcpyAsync(verdicts, c->verdicts.p, n, hipMemcpyDeviceToHost, st));
+    if (gt) HIPCK(hipMemcpyAsync(gt, c->gt.p, n * 576, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    return CC_OK;
+}
+
+}  // extern "C"

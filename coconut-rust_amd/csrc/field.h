@@ -1,0 +1,451 @@
+// BLS12-381 field tower for gfx950 — device code (the product path).
+//
+// Replaces AMCL v3.2 FP/FP2/FP4/FP12 (reached by the reference through amcl_wrapper 0.1.7,
+// reference Cargo.toml:16-19).  Same tower as AMCL so GT elements serialise
+// in AMCL's byte order directly:
+//     Fp2  = Fp[i]/(i^2 + 1)
+//     Fp4  = Fp2[s]/(s^2 - xi),  xi = 1 + i
+//     Fp12 = Fp4[w]/(w^3 - s)
+//
+// One field element per lane: 12 x 32-bit limbs in VGPRs, Montgomery form R = 2^384.
+// Multiplication is CIOS with the "no final carry" shortcut (p's top limb < 2^31 - 1), each
+// inner step a v_mad_u64_u32 chain.  All limb loops are fully unrolled so limbs stay in registers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DEV __device__ __forceinline__
+
+namespace cc {
+
+constexpr int NL = 12;  // limbs per Fp
+
+// p, little-endian 32-bit limbs
+#define CC_P_LIMBS                                                                              \
+    0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, \
+        0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau
+// R mod p (Montgomery one)
+#define CC_ONE_LIMBS                                                                            \
+    0x0002fffdu, 0x76090000u, 0xc40c0002u, 0xebf4000bu, 0x53c758bau, 0x5f489857u, 0x70525745u, \
+        0x77ce5853u, 0xa256ec6du, 0x5c071a97u, 0xfa80e493u, 0x15f65ec3u
+// R^2 mod p
+#define CC_R2_LIMBS                                                                             \
+    0x1c341746u, 0xf4df1f34u, 0x09d104f1u, 0x0a76e6a6u, 0x4c95b6d5u, 0x8de5476cu, 0x939d83c0u, \
+        0x67eb88a9u, 0xb519952du, 0x9a793e85u, 0x92cae3aau, 0x11988fe5u
+constexpr uint32_t N0 = 0xfffcfffdu;  // -p^-1 mod 2^32
+
+__constant__ static const uint32_t kP[NL] = {CC_P_LIMBS};
+
+struct Fp {
+    uint32_t v[NL];
+};
+
+DEV uint32_t p_limb(int j) {
+    constexpr uint32_t P[NL] = {CC_P_LIMBS};
+    return P[j];
+}
+
+DEV void fp_zero(Fp& r) {
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.v[j] = 0;
+}
+
+DEV void fp_one(Fp& r) {
+    constexpr uint32_t O[NL] = {CC_ONE_LIMBS};
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.v[j] = O[j];
+}
+
+DEV bool fp_is_zero(const Fp& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) o |= a.v[j];
+    return o == 0;
+}
+
+DEV bool fp_eq(const Fp& a, const Fp& b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) o |= a.v[j] ^ b.v[j];
+    return o == 0;
+}
+
+DEV bool fp_is_one(const Fp& a) {
+    constexpr uint32_t O[NL] = {CC_ONE_LIMBS};
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) o |= a.v[j] ^ O[j];
+    return o == 0;
+}
+
+// r = t >= p ? t - p : t   (t < 2p)
+DEV void fp_reduce_once(Fp& r, const uint32_t t[NL]) {
+    uint32_t s[NL];
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) s[j] = __builtin_subc(t[j], p_limb(j), br, &br);
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.v[j] = br ? t[j] : s[j];
+}
+
+DEV void fp_add(Fp& r, const Fp& a, const Fp& b) {
+    uint32_t t[NL];
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) t[j] = __builtin_addc(a.v[j], b.v[j], c, &c);
+    fp_reduce_once(r, t);  // a + b < 2p < 2^384: no carry out
+}
+
+DEV void fp_dbl(Fp& r, const Fp& a) { fp_add(r, a, a); }
+
+DEV void fp_sub(Fp& r, const Fp& a, const Fp& b) {
+    uint32_t t[NL];
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) t[j] = __builtin_subc(a.v[j], b.v[j], br, &br);
+    uint32_t mask = 0u - br;
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.v[j] = __builtin_addc(t[j], p_limb(j) & mask, c, &c);
+}
+
+DEV void fp_neg(Fp& r, const Fp& a) {
+    Fp z;
+    fp_zero(z);
+    fp_sub(r, z, a);
+}
+
+// Montgomery multiplication, CIOS without the extra carry words (gnark's no-carry variant).
+// Out of line with value semantics: keeps kernels compact (instruction-cache friendly) and stops
+// the scheduler from interleaving dozens of 12-limb products (which explodes register pressure).
+static __device__ __noinline__ Fp fp_mul_v(Fp a, Fp b) {
+    uint32_t t[NL];
+#pragma unroll
+    for (int i = 0; i < NL; i++) {
+        const uint32_t bi = b.v[i];
+        uint64_t A = (uint64_t)a.v[0] * bi + (i ? t[0] : 0u);
+        const uint32_t t0 = (uint32_t)A;
+        const uint32_t m = t0 * N0;
+        uint64_t C = (uint64_t)m * p_limb(0) + t0;
+#pragma unroll
+        for (int j = 1; j < NL; j++) {
+            A = (uint64_t)a.v[j] * bi + (uint64_t)(i ? t[j] : 0u) + (A >> 32);
+            C = (uint64_t)m * p_limb(j) + (uint64_t)(uint32_t)A + (C >> 32);
+            t[j - 1] = (uint32_t)C;
+        }
+        t[NL - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
+    }
+    Fp r;
+    fp_reduce_once(r, t);
+    return r;
+}
+
+DEV void fp_mul(Fp& r, const Fp& a, const Fp& b) { r = fp_mul_v(a, b); }
+
+DEV void fp_sqr(Fp& r, const Fp& a) { fp_mul(r, a, a); }
+
+// a * small constant via additions (k <= 12)
+DEV void fp_mul_small(Fp& r, const Fp& a, int k) {
+    Fp acc = a;
+    for (int i = 1; i < k; i++) fp_add(acc, acc, a);
+    r = acc;
+}
+
+// convert canonical integer (< p) to Montgomery
+DEV void fp_to_mont(Fp& r, const Fp& a) {
+    constexpr uint32_t R2[NL] = {CC_R2_LIMBS};
+    Fp r2;
+#pragma unroll
+    for (int j = 0; j < NL; j++) r2.v[j] = R2[j];
+    fp_mul(r, a, r2);
+}
+
+DEV void fp_from_mont(Fp& r, const Fp& a) {
+    Fp one;
+    fp_zero(one);
+    one.v[0] = 1;
+    fp_mul(r, a, one);
+}
+
+// is the raw integer a (< 2^384) >= p ?
+DEV bool fp_raw_geq_p(const Fp& a) {
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) (void)__builtin_subc(a.v[j], p_limb(j), br, &br);
+    return br == 0;
+}
+
+// raw integer mod p (AMCL FP::new_big reduces); the loop runs only for non-canonical encodings
+DEV void fp_raw_reduce(Fp& a) {
+    while (fp_raw_geq_p(a)) {
+        uint32_t br = 0;
+#pragma unroll
+        for (int j = 0; j < NL; j++) a.v[j] = __builtin_subc(a.v[j], p_limb(j), br, &br);
+    }
+}
+
+// a^(p-2) (Fermat inversion); the exponent is a compile-time constant so every lane branches alike.
+__constant__ static const uint32_t kPm2[NL] = {0xffffaaa9u, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u,
+                                0xf38512bfu, 0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau};
+
+DEV void fp_inv(Fp& r, const Fp& a) {
+    Fp acc = a;
+    // top limb 0x1a0111ea: highest set bit is bit 28
+    for (int bit = 32 * (NL - 1) + 28 - 1; bit >= 0; bit--) {
+        fp_sqr(acc, acc);
+        if ((kPm2[bit >> 5] >> (bit & 31)) & 1u) fp_mul(acc, acc, a);
+    }
+    r = acc;
+}
+
+// ============================== Fp2 ==============================
+struct Fp2 {
+    Fp a, b;  // a + b i
+};
+
+DEV void f2_zero(Fp2& r) { fp_zero(r.a); fp_zero(r.b); }
+DEV void f2_one(Fp2& r) { fp_one(r.a); fp_zero(r.b); }
+DEV bool f2_is_zero(const Fp2& x) { return fp_is_zero(x.a) && fp_is_zero(x.b); }
+DEV bool f2_eq(const Fp2& x, const Fp2& y) { return fp_eq(x.a, y.a) && fp_eq(x.b, y.b); }
+DEV void f2_add(Fp2& r, const Fp2& x, const Fp2& y) { fp_add(r.a, x.a, y.a); fp_add(r.b, x.b, y.b); }
+DEV void f2_sub(Fp2& r, const Fp2& x, const Fp2& y) { fp_sub(r.a, x.a, y.a); fp_sub(r.b, x.b, y.b); }
+DEV void f2_dbl(Fp2& r, const Fp2& x) { fp_dbl(r.a, x.a); fp_dbl(r.b, x.b); }
+DEV void f2_neg(Fp2& r, const Fp2& x) { fp_neg(r.a, x.a); fp_neg(r.b, x.b); }
+DEV void f2_conj(Fp2& r, const Fp2& x) { r.a = x.a; fp_neg(r.b, x.b); }
+
+DEV void f2_mul(Fp2& r, const Fp2& x, const Fp2& y) {
+    Fp t0, t1, s0, s1;
+    fp_mul(t0, x.a, y.a);
+    fp_mul(t1, x.b, y.b);
+    fp_add(s0, x.a, x.b);
+    fp_add(s1, y.a, y.b);
+    fp_mul(s0, s0, s1);
+    fp_sub(s0, s0, t0);
+    fp_sub(r.b, s0, t1);
+    fp_sub(r.a, t0, t1);
+}
+
+DEV void f2_sqr(Fp2& r, const Fp2& x) {
+    Fp s, d, m;
+    fp_add(s, x.a, x.b);
+    fp_sub(d, x.a, x.b);
+    fp_mul(m, x.a, x.b);
+    fp_mul(r.a, s, d);
+    fp_dbl(r.b, m);
+}
+
+DEV void f2_mul_fp(Fp2& r, const Fp2& x, const Fp& k) { fp_mul(r.a, x.a, k); fp_mul(r.b, x.b, k); }
+
+// x * xi, xi = 1 + i
+DEV void f2_mul_xi(Fp2& r, const Fp2& x) {
+    Fp t;
+    fp_sub(t, x.a, x.b);
+    fp_add(r.b, x.a, x.b);
+    r.a = t;
+}
+
+DEV void f2_inv(Fp2& r, const Fp2& x) {
+    Fp n, t;
+    fp_sqr(n, x.a);
+    fp_sqr(t, x.b);
+    fp_add(n, n, t);
+    fp_inv(n, n);
+    fp_mul(r.a, x.a, n);
+    fp_mul(t, x.b, n);
+    fp_neg(r.b, t);
+}
+
+// ============================== Fp4 = Fp2[s]/(s^2 - xi) ==============================
+struct Fp4 {
+    Fp2 a, b;  // a + b s
+};
+
+DEV void f4_zero(Fp4& r) { f2_zero(r.a); f2_zero(r.b); }
+DEV void f4_one(Fp4& r) { f2_one(r.a); f2_zero(r.b); }
+DEV void f4_add(Fp4& r, const Fp4& x, const Fp4& y) { f2_add(r.a, x.a, y.a); f2_add(r.b, x.b, y.b); }
+DEV void f4_sub(Fp4& r, const Fp4& x, const Fp4& y) { f2_sub(r.a, x.a, y.a); f2_sub(r.b, x.b, y.b); }
+DEV void f4_dbl(Fp4& r, const Fp4& x) { f2_dbl(r.a, x.a); f2_dbl(r.b, x.b); }
+DEV void f4_neg(Fp4& r, const Fp4& x) { f2_neg(r.a, x.a); f2_neg(r.b, x.b); }
+DEV void f4_conj(Fp4& r, const Fp4& x) { r.a = x.a; f2_neg(r.b, x.b); }  // a - b s
+
+DEV void f4_mul(Fp4& r, const Fp4& x, const Fp4& y) {
+    Fp2 t0, t1, s0, s1;
+    f2_mul(t0, x.a, y.a);
+    f2_mul(t1, x.b, y.b);
+    f2_add(s0, x.a, x.b);
+    f2_add(s1, y.a, y.b);
+    f2_mul(s0, s0, s1);
+    f2_sub(s0, s0, t0);
+    f2_sub(r.b, s0, t1);
+    f2_mul_xi(t1, t1);
+    f2_add(r.a, t0, t1);
+}
+
+// (a + b s)^2 = (a^2 + xi b^2) + 2ab s
+DEV void f4_sqr(Fp4& r, const Fp4& x) {
+    Fp2 ab, s0, s1;
+    f2_mul(ab, x.a, x.b);
+    f2_add(s0, x.a, x.b);
+    f2_mul_xi(s1, x.b);
+    f2_add(s1, s1, x.a);
+    f2_mul(s0, s0, s1);  // (a + b)(a + xi b) = a^2 + xi b^2 + ab (1 + xi)
+    f2_sub(s0, s0, ab);
+    f2_mul_xi(s1, ab);
+    f2_sub(r.a, s0, s1);
+    f2_dbl(r.b, ab);
+}
+
+// x * s = xi b + a s
+DEV void f4_mul_s(Fp4& r, const Fp4& x) {
+    Fp2 t;
+    f2_mul_xi(t, x.b);
+    r.b = x.a;
+    r.a = t;
+}
+
+// x * (c, 0) with c in Fp2
+DEV void f4_mul_f2(Fp4& r, const Fp4& x, const Fp2& c) {
+    f2_mul(r.a, x.a, c);
+    f2_mul(r.b, x.b, c);
+}
+
+DEV void f4_inv(Fp4& r, const Fp4& x) {
+    Fp2 n, t;
+    f2_sqr(n, x.a);
+    f2_sqr(t, x.b);
+    f2_mul_xi(t, t);
+    f2_sub(n, n, t);  // a^2 - xi b^2
+    f2_inv(n, n);
+    f2_mul(r.a, x.a, n);
+    f2_mul(t, x.b, n);
+    f2_neg(r.b, t);
+}
+
+// ============================== Fp12 = Fp4[w]/(w^3 - s) ==============================
+struct Fp12 {
+    Fp4 a, b, c;  // a + b w + c w^2
+};
+
+DEV void f12_one(Fp12& r) { f4_one(r.a); f4_zero(r.b); f4_zero(r.c); }
+
+DEV bool f12_is_one(const Fp12& x) {
+    return fp_is_one(x.a.a.a) && fp_is_zero(x.a.a.b) && f2_is_zero(x.a.b) && f2_is_zero(x.b.a) &&
+           f2_is_zero(x.b.b) && f2_is_zero(x.c.a) && f2_is_zero(x.c.b);
+}
+
+// conj = x^(p^6): w -> -w, s -> -s
+DEV void f12_conj(Fp12& r, const Fp12& x) {
+    f4_conj(r.a, x.a);
+    Fp4 t;
+    f4_conj(t, x.b);
+    f4_neg(r.b, t);
+    f4_conj(r.c, x.c);
+}
+
+DEV void f12_mul(Fp12& r, const Fp12& x, const Fp12& y) {
+    Fp4 t0, t1, t2, s, u, ra, rb, rc;
+    f4_mul(t0, x.a, y.a);
+    f4_mul(t1, x.b, y.b);
+    f4_mul(t2, x.c, y.c);
+    f4_add(s, x.b, x.c);
+    f4_add(u, y.b, y.c);
+    f4_mul(s, s, u);
+    f4_sub(s, s, t1);
+    f4_sub(s, s, t2);
+    f4_mul_s(s, s);
+    f4_add(ra, s, t0);
+    f4_add(s, x.a, x.b);
+    f4_add(u, y.a, y.b);
+    f4_mul(s, s, u);
+    f4_sub(s, s, t0);
+    f4_sub(s, s, t1);
+    f4_mul_s(u, t2);
+    f4_add(rb, s, u);
+    f4_add(s, x.a, x.c);
+    f4_add(u, y.a, y.c);
+    f4_mul(s, s, u);
+    f4_sub(s, s, t0);
+    f4_sub(s, s, t2);
+    f4_add(rc, s, t1);
+    r.a = ra;
+    r.b = rb;
+    r.c = rc;
+}
+
+// Chung-Hasan SQR2 over the cubic extension
+DEV void f12_sqr(Fp12& r, const Fp12& x) {
+    Fp4 s0, s1, s2, s3, s4, t;
+    f4_sqr(s0, x.a);
+    f4_mul(s1, x.a, x.b);
+    f4_dbl(s1, s1);
+    f4_sub(t, x.a, x.b);
+    f4_add(t, t, x.c);
+    f4_sqr(s2, t);
+    f4_mul(s3, x.b, x.c);
+    f4_dbl(s3, s3);
+    f4_sqr(s4, x.c);
+    Fp4 ra, rb, rc;
+    f4_mul_s(t, s3);
+    f4_add(ra, s0, t);
+    f4_mul_s(t, s4);
+    f4_add(rb, s1, t);
+    f4_add(rc, s1, s2);
+    f4_add(rc, rc, s3);
+    f4_sub(rc, rc, s0);
+    f4_sub(rc, rc, s4);
+    r.a = ra;
+    r.b = rb;
+    r.c = rc;
+}
+
+// Granger-Scott squaring for elements of the cyclotomic subgroup (AMCL FP12::usqr):
+// a' = 3a^2 - 2 conj(a), b' = 3 s c^2 + 2 conj(b), c' = 3 b^2 - 2 conj(c)
+DEV void f12_cyc_sqr(Fp12& r, const Fp12& x) {
+    Fp4 A, B, C, t;
+    f4_sqr(A, x.a);
+    f4_sqr(B, x.c);
+    f4_mul_s(B, B);
+    f4_sqr(C, x.b);
+    // a'
+    f4_conj(t, x.a);
+    f4_sub(t, A, t);
+    f4_dbl(t, t);
+    f4_add(r.a, t, A);
+    // b'
+    f4_conj(t, x.b);
+    f4_add(t, B, t);
+    f4_dbl(t, t);
+    f4_add(r.b, t, B);
+    // c'
+    f4_conj(t, x.c);
+    f4_sub(t, C, t);
+    f4_dbl(t, t);
+    f4_add(r.c, t, C);
+}
+
+DEV void f12_inv(Fp12& r, const Fp12& x) {
+    Fp4 A, B, C, F, t;
+    f4_sqr(A, x.a);
+    f4_mul(t, x.b, x.c);
+    f4_mul_s(t, t);
+    f4_sub(A, A, t);  // a^2 - s bc
+    f4_sqr(B, x.c);
+    f4_mul_s(B, B);
+    f4_mul(t, x.a, x.b);
+    f4_sub(B, B, t);  // s c^2 - ab
+    f4_sqr(C, x.b);
+    f4_mul(t, x.a, x.c);
+    f4_sub(C, C, t);  // b^2 - ac
+    f4_mul(F, x.c, B);
+    f4_mul(t, x.b, C);
+    f4_add(F, F, t);
+    f4_mul_s(F, F);
+    f4_mul(t, x.a, A);
+    f4_add(F, F, t);
+    f4_inv(F, F);
+    f4_mul(r.a, A, F);
+    f4_mul(r.b, B, F);
+    f4_mul(r.c, C, F);
+}
+
+}  // namespace cc

@@ -1,0 +1,122 @@
+/* coconut_hip.h — C ABI of the MI355X batch-verification engine for Coconut credentials.
+ *
+ * Drop-in boundary for the reference's verifier hot path (3for/coconut-rust, read-only at
+ * /root/reference).  The reference has no FFI of its own; these entry points are what its Rust
+ * API would bind through `extern "C"` (binding shown in INTEGRATION.md):
+ *
+ *   cc_verify_batch / cc_verify_batch_device
+ *        replaces  Signature::verify              src/signature.rs:473-478
+ *                  (-> ps_sig Signature::verify [EXT], via transforms signature.rs:83-104)
+ *   cc_signature_aggregate_batch
+ *        replaces  Signature::aggregate           src/signature.rs:448-470
+ *   cc_verkey_aggregate_batch
+ *        replaces  Verkey::aggregate              src/signature.rs:483-526
+ *   cc_pok_verify_batch
+ *        replaces  ps_sig PoKOfSignatureProof::verify [EXT], called at src/pok_sig.rs:103-105
+ *   cc_set_params / cc_set_verkey
+ *        the Params (src/signature.rs:13-17, only g_tilde is read by verify) and Verkey
+ *        (src/signature.rs:46-49) a batch is checked against
+ *
+ * Encodings are amcl_wrapper's `to_bytes`:
+ *   Fr 48 B big-endian | G1 97 B = 0x04||x||y | G2 192 B = x.a||x.b||y.a||y.b | GT 576 B (AMCL FP12)
+ * Group assignment (reference src/lib.rs:3-4,12-13): CC_SIG_G2 = the reference default build
+ * (sigma, g, h in G2; X~, Y~, g~ in G1), CC_SIG_G1 = the other feature.
+ *
+ * All host pointers are caller-owned, read during the call and never retained.  A context owns
+ * one HIP device, one stream and the device tables; use one context per calling thread.
+ * Errors mirror the reference's failure modes (src/errors.rs:6-24): where the reference panics
+ * (assert!/unwrap) the C ABI returns a code instead.
+ */
+#ifndef COCONUT_HIP_H
+#define COCONUT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+    CC_OK = 0,
+    CC_ERR_LEN = -1,          /* CoconutErrorKind::UnsupportedNoOfMessages (verkey q != msgs)   */
+    CC_ERR_BASES_EXPS = -2,   /* CoconutErrorKind::UnequalNoOfBasesExponents (PoK responses)    */
+    CC_ERR_THRESHOLD = -3,    /* len < threshold: reference assert! panics (signature.rs:449,484) */
+    CC_ERR_DECODE = -4,       /* malformed buffer sizes / missing params                           */
+    CC_ERR_HIP = -5,          /* HIP runtime failure                                               */
+    CC_ERR_RCCL = -6,         /* collective failure (RLC gather)                                   */
+    CC_ERR_STATE = -7         /* call order: params / verkey not set                               */
+} cc_status;
+
+typedef enum { CC_SIG_G2 = 0, CC_SIG_G1 = 1 } cc_group_mode;
+
+typedef struct cc_ctx cc_ctx;
+
+const char* cc_status_str(int status);
+const char* cc_version(void);
+
+cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out);
+cc_status cc_ctx_destroy(cc_ctx* ctx);
+cc_status cc_ctx_mode(const cc_ctx* ctx, int* mode_out);
+
+/* Params: only g_tilde (OtherGroup encoding) is used on the verify path. */
+cc_status cc_set_params(cc_ctx* ctx, const uint8_t* g_tilde);
+
+/* Shared verkey (X~, Y~[q]) for cc_verify_batch with vk == NULL: builds fixed-base tables on the
+ * device (one-time cost, reported separately from batch throughput). */
+cc_status cc_set_verkey(cc_ctx* ctx, const uint8_t* X, const uint8_t* Y, size_t q);
+
+/* Batch Signature::verify.
+ *   sigma1, sigma2 : n x SignatureGroup encodings
+ *   msgs           : n x q x 48 B
+ *   vk_X, vk_Y     : NULL => the shared verkey from cc_set_verkey; else n x OtherGroup and
+ *                    n x q x OtherGroup (one verkey per credential)
+ *   verdicts       : n bytes, 1 = verify() returned true
+ *   gt_or_null     : n x 576 B, e(.,.)*e(.,.) as amcl_wrapper GT::to_bytes, or NULL
+ *   rlc            : 0 = per-credential; 1 = random-linear-combination batch (all-or-fallback)
+ * Returns CC_ERR_LEN if q differs from the shared verkey's q (the reference panics there). */
+cc_status cc_verify_batch(cc_ctx* ctx, size_t n, size_t q, const uint8_t* sigma1, const uint8_t* sigma2,
+                          const uint8_t* msgs, const uint8_t* vk_X, const uint8_t* vk_Y, uint8_t* verdicts,
+                          uint8_t* gt_or_null, int rlc);
+
+/* Same, with every buffer already in device memory (HBM-resident batch; the timed bench path).
+ * Shared verkey only.  `stream` is a hipStream_t or NULL for the context's stream.  The call is
+ * asynchronous with respect to the host; synchronise the stream before reading verdicts. */
+cc_status cc_verify_batch_device(cc_ctx* ctx, size_t n, size_t q, const uint8_t* d_sigma1, const uint8_t* d_sigma2,
+                                 const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt_or_null, void* stream);
+
+/* Batch Signature::aggregate: n independent aggregations of `len` (id, Signature) entries each;
+ * only the first t entries are used, sigma_1 comes from entry 0, Lagrange over the de-duplicated
+ * id set (signature.rs:448-470).  ids: n x len; sigma1/sigma2: n x len encodings;
+ * out_sigma1/out_sigma2: n encodings. */
+cc_status cc_signature_aggregate_batch(cc_ctx* ctx, size_t n, size_t len, size_t t, const uint64_t* ids,
+                                       const uint8_t* sigma1, const uint8_t* sigma2, uint8_t* out_sigma1,
+                                       uint8_t* out_sigma2);
+
+/* Batch Verkey::aggregate (signature.rs:483-526): X: n x len, Y: n x len x q; outX: n; outY: n x q. */
+cc_status cc_verkey_aggregate_batch(cc_ctx* ctx, size_t n, size_t len, size_t t, size_t q, const uint64_t* ids,
+                                    const uint8_t* X, const uint8_t* Y, uint8_t* outX, uint8_t* outY);
+
+/* Batch PoKOfSignatureProof::verify against the shared verkey and params.
+ *   sigma1, sigma2  : n x SignatureGroup (sigma'_1, sigma'_2)
+ *   J, T            : n x OtherGroup (J and the Schnorr commitment)
+ *   responses       : n x (q - r + 1) x 48 B, order [g~, Y~_i for hidden i ascending]
+ *   chal            : n x 48 B
+ *   revealed_idx    : r indices (shared by the batch, ascending, < q)
+ *   revealed_msgs   : n x r x 48 B
+ * CC_ERR_BASES_EXPS if nresp != q - r + 1 (ps_sig returns UnequalNoOfBasesExponents). */
+cc_status cc_pok_verify_batch(cc_ctx* ctx, size_t n, size_t q, size_t r, size_t nresp, const uint8_t* sigma1,
+                              const uint8_t* sigma2, const uint8_t* J, const uint8_t* T, const uint8_t* responses,
+                              const uint8_t* chal, const uint64_t* revealed_idx, const uint8_t* revealed_msgs,
+                              uint8_t* verdicts, uint8_t* gt_or_null);
+
+/* Kernel timing of the last cc_verify_batch_device call (HIP events on the context stream):
+ * milliseconds per phase {prep, miller, fexp}.  Used by bench.py for the roofline figure. */
+cc_status cc_last_timing(const cc_ctx* ctx, float* prep_ms, float* miller_ms, float* fexp_ms);
+cc_status cc_set_timing(cc_ctx* ctx, int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* COCONUT_HIP_H */

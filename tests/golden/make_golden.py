@@ -1,0 +1,256 @@
+"""Generate the committed golden fixtures under tests/golden/ from the Python oracle.
+
+    python tests/golden/make_golden.py          (~2-4 minutes, single core)
+
+The reference holds no golden vectors or known-answer tests (all its tests use an unseeded RNG;
+SURVEY.md §4, §8c), so every fixture here is produced by the CPU restatement in `oracle/` from a
+seeded SHAKE256 DRBG and is pinned by the algebraic identities the reference's tests assert
+(see tests/test_oracle.py).  Files are data (inputs + expected outputs), hex-encoded JSON.
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+from oracle import bls12_381 as B          # noqa: E402
+from oracle import coconut_ref as C        # noqa: E402
+
+
+def hx(b: bytes) -> str:
+    return b.hex()
+
+
+def fr_hex(k: int) -> str:
+    return B.fr_to_bytes(k).hex()
+
+
+def setup(mode, q, t, n, seed):
+    grp = C.Groups(mode)
+    rng = C.Drbg(seed)
+    params = C.params_from_rng(grp, q, rng)
+    sx, sy, signers = C.trusted_party_sss_keygen(grp, t, n, params, rng)
+    vk = C.verkey_aggregate(grp, t, [(s["id"], s["vk"]) for s in signers])
+    return grp, rng, params, sx, sy, signers, vk
+
+
+def vk_json(grp, vk):
+    return {"X": hx(grp.oth_to_bytes(vk[0])), "Y": [hx(grp.oth_to_bytes(y)) for y in vk[1]]}
+
+
+KINDS = ["valid", "sigma2_plus_g", "msg_plus_1", "swapped", "sigma1_inf", "sigma2_inf",
+         "wrong_key", "both_inf", "offcurve_sigma1", "neg_sigma2"]
+
+
+def make_verify(mode, q, ncred, seed, per_cred_vk=False):
+    t, n = 3, 5
+    grp, rng, params, sx, sy, signers, vk = setup(mode, q, t, n, seed)
+    secret = (sx, sy)
+    # a second key pair for "wrong_key"
+    wrong = (rng.fr(), [rng.fr() for _ in range(q)])
+    creds = []
+    for c in range(ncred):
+        kind = "valid" if (c % 3 != 1) else KINDS[1 + (c // 3) % (len(KINDS) - 1)]
+        if per_cred_vk:
+            sk = (rng.fr(), [rng.fr() for _ in range(q)])
+            cvk = (grp.other.mul(params["g_tilde"], sk[0]),
+                   [grp.other.mul(params["g_tilde"], y) for y in sk[1]])
+        else:
+            sk, cvk = secret, vk
+        msgs = [rng.fr() for _ in range(q)]
+        h = grp.sig.mul(grp.sig.gen, rng.fr())
+        sig = C.sign(grp, sk, msgs, h)
+        s1b = grp.sig_to_bytes(sig[0])
+        s2b = grp.sig_to_bytes(sig[1])
+        if kind == "sigma2_plus_g":
+            sig = (sig[0], grp.sig.add(sig[1], grp.sig.gen))
+        elif kind == "msg_plus_1":
+            j = c % q
+            msgs = list(msgs)
+            msgs[j] = (msgs[j] + 1) % B.R
+        elif kind == "swapped":
+            sig = (sig[1], sig[0])
+        elif kind == "sigma1_inf":
+            sig = (None, sig[1])
+        elif kind == "sigma2_inf":
+            sig = (sig[0], None)
+        elif kind == "wrong_key":
+            sig = C.sign(grp, wrong, msgs, h)
+        elif kind == "both_inf":
+            sig = (None, None)
+        elif kind == "neg_sigma2":
+            sig = (sig[0], grp.sig.neg(sig[1]))
+        s1b = grp.sig_to_bytes(sig[0])
+        s2b = grp.sig_to_bytes(sig[1])
+        if kind == "offcurve_sigma1":
+            # flip a bit of y: not on the curve -> AMCL decodes to infinity -> reject
+            bb = bytearray(s1b)
+            bb[-1] ^= 1
+            s1b = bytes(bb)
+        s1 = grp.sig_from_bytes(s1b)
+        s2 = grp.sig_from_bytes(s2b)
+        verdict, gt = C.verify_gt(grp, (s1, s2), msgs, cvk, params["g_tilde"])
+        if kind == "valid":
+            assert verdict, "valid credential rejected by the oracle"
+        else:
+            assert not verdict, kind
+        rec = {"kind": kind, "sigma1": hx(s1b), "sigma2": hx(s2b),
+               "msgs": [fr_hex(m) for m in msgs], "verdict": int(verdict),
+               "gt": hx(B.gt_to_bytes(gt))}
+        if per_cred_vk:
+            rec["vk"] = vk_json(grp, cvk)
+        creds.append(rec)
+        print(f"  verify {mode} q={q} cred {c} {kind} -> {int(verdict)}", flush=True)
+    out = {"mode": mode, "q": q, "seed": seed, "threshold": t, "total": n,
+           "g_tilde": hx(grp.oth_to_bytes(params["g_tilde"])),
+           "creds": creds}
+    if not per_cred_vk:
+        out["vk"] = vk_json(grp, vk)
+    return out
+
+
+def make_aggregate(mode, seed, q=6, t=3, n=6, big=False):
+    """Config 1-style keygen + the reference's aggregation test shapes
+    (signature.rs:537-580 ids 1..t and gaps {1,3,5}; 761-822 sig set {1,3,5} vs vk set {2,4,6};
+    duplicate ids; more than t entries)."""
+    grp, rng, params, sx, sy, signers, _ = setup(mode, q, t, n, seed)
+    msgs = [rng.fr() for _ in range(q)]
+    h = grp.sig.mul(grp.sig.gen, rng.fr())
+    partial = {s["id"]: C.sign(grp, s["sk"], msgs, h) for s in signers}
+    cases = []
+    id_lists = [[1, 2, 3], [1, 3, 5], [2, 4, 6], [5, 1, 3, 2, 6], [1, 1, 3], [6, 5, 4, 3]]
+    if big:
+        id_lists = [list(range(1, n + 1))[:t]]
+    for ids in id_lists:
+        sigs = [(i, partial[i]) for i in ids]
+        keys = [(i, signers[i - 1]["vk"]) for i in ids]
+        asig = C.signature_aggregate(grp, t, sigs)
+        avk = C.verkey_aggregate(grp, t, keys)
+        distinct = len(set(ids[:t])) == t
+        if distinct:
+            # signature.rs:554-559 — aggregated vk == g~ * secret
+            assert avk[0] == grp.other.mul(params["g_tilde"], sx)
+            assert all(avk[1][j] == grp.other.mul(params["g_tilde"], sy[j]) for j in range(q))
+            assert C.verify(grp, asig, msgs, avk, params["g_tilde"])
+        cases.append({
+            "ids": ids,
+            "sigma1": [hx(grp.sig_to_bytes(partial[i][0])) for i in ids],
+            "sigma2": [hx(grp.sig_to_bytes(partial[i][1])) for i in ids],
+            "X": [hx(grp.oth_to_bytes(signers[i - 1]["vk"][0])) for i in ids],
+            "Y": [[hx(grp.oth_to_bytes(y)) for y in signers[i - 1]["vk"][1]] for i in ids],
+            "out_sigma1": hx(grp.sig_to_bytes(asig[0])),
+            "out_sigma2": hx(grp.sig_to_bytes(asig[1])),
+            "out_X": hx(grp.oth_to_bytes(avk[0])),
+            "out_Y": [hx(grp.oth_to_bytes(y)) for y in avk[1]],
+            "lagrange": [fr_hex(C.lagrange_basis_at_0(set(ids[:t]), i)) for i in ids[:t]],
+            "verifies": int(C.verify(grp, asig, msgs, avk, params["g_tilde"])),
+        })
+        print(f"  aggregate {mode} ids={ids[:8]}", flush=True)
+    return {"mode": mode, "q": q, "threshold": t, "total": n, "seed": seed,
+            "g_tilde": hx(grp.oth_to_bytes(params["g_tilde"])),
+            "msgs": [fr_hex(m) for m in msgs],
+            "secret_X": hx(grp.oth_to_bytes(grp.other.mul(params["g_tilde"], sx))),
+            "secret_Y": [hx(grp.oth_to_bytes(grp.other.mul(params["g_tilde"], y))) for y in sy],
+            "cases": cases}
+
+
+POK_KINDS = ["valid", "valid", "bad_chal", "bad_revealed", "bad_response", "sigma1_inf",
+             "bad_J", "valid"]
+
+
+def make_pok(mode, q, revealed, nproof, seed):
+    t, n = 3, 5
+    grp, rng, params, sx, sy, signers, vk = setup(mode, q, t, n, seed)
+    proofs = []
+    for c in range(nproof):
+        kind = POK_KINDS[c % len(POK_KINDS)]
+        msgs = [rng.fr() for _ in range(q)]
+        h = grp.sig.mul(grp.sig.gen, rng.fr())
+        sig = C.sign(grp, (sx, sy), msgs, h)
+        pok = C.pok_init(grp, sig, vk, params["g_tilde"], msgs, set(revealed), rng)
+        chal = int.from_bytes(__import__("hashlib").shake_256(C.pok_to_bytes(grp, pok)).digest(48),
+                              "big") % B.R
+        proof = C.pok_gen_proof(pok, chal)
+        rev = {i: msgs[i] for i in revealed}
+        if kind == "bad_chal":
+            chal = (chal + 1) % B.R
+        elif kind == "bad_revealed":
+            i0 = revealed[0]
+            rev[i0] = (rev[i0] + 1) % B.R
+        elif kind == "bad_response":
+            proof["responses"] = list(proof["responses"])
+            proof["responses"][-1] = (proof["responses"][-1] + 5) % B.R
+        elif kind == "sigma1_inf":
+            proof["sig"] = (None, proof["sig"][1])
+        elif kind == "bad_J":
+            proof["J"] = grp.other.add(proof["J"], grp.other.gen)
+        verdict, gt = C.pok_verify_gt(grp, proof, vk, params["g_tilde"], rev, chal)
+        assert verdict == kind.startswith("valid"), kind
+        proofs.append({
+            "kind": kind,
+            "sigma1": hx(grp.sig_to_bytes(proof["sig"][0])),
+            "sigma2": hx(grp.sig_to_bytes(proof["sig"][1])),
+            "J": hx(grp.oth_to_bytes(proof["J"])),
+            "T": hx(grp.oth_to_bytes(proof["T"])),
+            "responses": [fr_hex(x) for x in proof["responses"]],
+            "chal": fr_hex(chal),
+            "revealed_msgs": [fr_hex(rev[i]) for i in revealed],
+            "verdict": int(verdict),
+            "gt": hx(B.gt_to_bytes(gt)) if gt is not None else None,
+        })
+        print(f"  pok {mode} q={q} proof {c} {kind} -> {int(verdict)}", flush=True)
+    return {"mode": mode, "q": q, "revealed": list(revealed), "seed": seed,
+            "g_tilde": hx(grp.oth_to_bytes(params["g_tilde"])), "vk": vk_json(grp, vk),
+            "proofs": proofs}
+
+
+def make_pairing_kat(seed):
+    """Single-pairing KATs: e(a*G1, b*G2) bytes + the generator pairing."""
+    rng = C.Drbg(seed)
+    out = []
+    for k in range(4):
+        a, b = (1, 1) if k == 0 else (rng.fr(), rng.fr())
+        Pp = B.G1.mul(B.G1.gen, a)
+        Qq = B.G2.mul(B.G2.gen, b)
+        gt = B.pairing(Pp, Qq)
+        ml = B.miller_loop(Qq, Pp)
+        out.append({"a": fr_hex(a), "b": fr_hex(b), "P": hx(B.g1_to_bytes(Pp)),
+                    "Q": hx(B.g2_to_bytes(Qq)), "gt": hx(B.gt_to_bytes(gt)),
+                    "miller_fexp_check": hx(B.gt_to_bytes(B.final_exp(ml)))})
+    return {"pairings": out}
+
+
+def write(name, obj):
+    path = os.path.join(HERE, name)
+    with open(path, "w") as f:
+        json.dump(obj, f, indent=0, sort_keys=True)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def main():
+    which = set(sys.argv[1:])
+
+    def want(tag):
+        return not which or tag in which
+
+    if want("kat"):
+        write("pairing_kat.json", make_pairing_kat(11))
+    for mode in ("G2", "G1"):
+        if want("verify"):
+            write(f"verify_{mode.lower()}_q6.json", make_verify(mode, 6, 30, 2))
+            write(f"verify_{mode.lower()}_q16_pervk.json", make_verify(mode, 16, 6, 3, per_cred_vk=True))
+        if want("aggregate"):
+            write(f"aggregate_{mode.lower()}.json", make_aggregate(mode, 4))
+        if want("pok"):
+            write(f"pok_{mode.lower()}_q6.json", make_pok(mode, 6, [3, 5], 8, 5))
+            write(f"pok_{mode.lower()}_q32.json", make_pok(mode, 32, [3, 5, 7, 11, 13, 17, 19, 23], 4, 6))
+    if want("aggbig"):
+        write("aggregate_g2_t67.json", make_aggregate("G2", 7, q=6, t=67, n=100, big=True))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,65 @@
+"""CPU tests of the drop-in boundary: libcoconut_hip.so loads and exports every symbol that
+include/coconut_hip.h declares; host-side argument checking; no compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+HDR = os.path.join(ROOT, "include", "coconut_hip.h")
+LIB = os.path.join(ROOT, "coconut-rust_amd", "libcoconut_hip.so")
+
+
+def declared_symbols():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(cc_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("cc_ctx_create", "cc_set_params", "cc_set_verkey", "cc_verify_batch", "cc_verify_batch_device",
+              "cc_signature_aggregate_batch", "cc_verkey_aggregate_batch", "cc_pok_verify_batch"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    assert os.path.exists(LIB), "build first: make -C coconut-rust_amd"
+    lib = ctypes.CDLL(LIB)
+    missing = [s for s in declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_status_strings_and_version():
+    from coconut._lib import lib
+    assert lib.cc_status_str(0) == b"ok"
+    assert lib.cc_status_str(-1) == b"UnsupportedNoOfMessages"
+    assert lib.cc_status_str(-2) == b"UnequalNoOfBasesExponents"
+    assert b"gfx950" in lib.cc_version()
+
+
+def test_null_and_bad_arguments_rejected_without_gpu():
+    from coconut._lib import lib
+    assert lib.cc_ctx_create(0, 7, None) == -4        # bad mode / null out
+    assert lib.cc_verify_batch(None, 1, 6, None, None, None, None, None, None, None, 0) == -4
+    assert lib.cc_set_params(None, None) == -4
+
+
+def test_ctx_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from coconut import Context, CoconutError
+    with pytest.raises(CoconutError):
+        Context(0)
+
+
+def test_package_import_requires_built_library(tmp_path):
+    import subprocess
+    import sys
+    env = dict(os.environ, COCONUT_HIP_LIB=str(tmp_path / "missing.so"))
+    r = subprocess.run([sys.executable, "-c", "import coconut"], cwd=os.path.join(ROOT, "coconut-rust_amd"),
+                       env=env, capture_output=True, text=True)
+    assert r.returncode != 0 and "no CPU fallback" in r.stderr

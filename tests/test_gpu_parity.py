@@ -1,0 +1,212 @@
+"""GPU parity tests (run on the MI355X box: pytest -m gpu).  The HIP path, called through the C ABI,
+must reproduce the oracle bit-for-bit: verdicts, GT bytes (AMCL order) and aggregated group
+elements, on the committed golden fixtures and on generated batches (checked against the C oracle
+and against verdicts known by construction)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden, oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+MODES = {"G2": 0, "G1": 1}
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    import coconut
+    c = {m: coconut.Context(0, coconut.GroupMode(v)) for m, v in MODES.items()}
+    yield c
+    for x in c.values():
+        x.close()
+
+
+def _cat(hexes):
+    return b"".join(bytes.fromhex(h) for h in hexes)
+
+
+@pytest.mark.parametrize("name", ["verify_g2_q6.json", "verify_g1_q6.json"])
+def test_verify_shared_vk_golden(ctxs, name):
+    from coconut import verify_batch
+    d = golden(name)
+    ctx = ctxs[d["mode"]]
+    cr = d["creds"]
+    ctx.set_params(bytes.fromhex(d["g_tilde"]))
+    ctx.set_verkey(bytes.fromhex(d["vk"]["X"]), [bytes.fromhex(y) for y in d["vk"]["Y"]])
+    v, gts = verify_batch(ctx, len(cr), d["q"], _cat(c["sigma1"] for c in cr), _cat(c["sigma2"] for c in cr),
+                          _cat(m for c in cr for m in c["msgs"]), want_gt=True)
+    for i, c in enumerate(cr):
+        assert v[i] == c["verdict"], (i, c["kind"])
+        assert gts[576 * i:576 * (i + 1)].hex() == c["gt"], (i, c["kind"])
+
+
+@pytest.mark.parametrize("name", ["verify_g2_q16_pervk.json", "verify_g1_q16_pervk.json"])
+def test_verify_per_credential_vk_golden(ctxs, name):
+    from coconut import verify_batch
+    d = golden(name)
+    ctx = ctxs[d["mode"]]
+    cr = d["creds"]
+    ctx.set_params(bytes.fromhex(d["g_tilde"]))
+    X = _cat(c["vk"]["X"] for c in cr)
+    Y = _cat(y for c in cr for y in c["vk"]["Y"])
+    v, gts = verify_batch(ctx, len(cr), d["q"], _cat(c["sigma1"] for c in cr), _cat(c["sigma2"] for c in cr),
+                          _cat(m for c in cr for m in c["msgs"]), vk=(X, Y), want_gt=True)
+    for i, c in enumerate(cr):
+        assert v[i] == c["verdict"], (i, c["kind"])
+        assert gts[576 * i:576 * (i + 1)].hex() == c["gt"], (i, c["kind"])
+
+
+def test_single_signature_verify_api(ctxs):
+    """The reference's per-call API (signature.rs:473) through a batch of one."""
+    from coconut import Params, Signature, Verkey
+    d = golden("verify_g2_q6.json")
+    ctx = ctxs["G2"]
+    vk = Verkey(bytes.fromhex(d["vk"]["X"]), [bytes.fromhex(y) for y in d["vk"]["Y"]])
+    params = Params(g=b"", g_tilde=bytes.fromhex(d["g_tilde"]))
+    for c in d["creds"][:4]:
+        sig = Signature(bytes.fromhex(c["sigma1"]), bytes.fromhex(c["sigma2"]))
+        assert sig.verify([bytes.fromhex(m) for m in c["msgs"]], vk, params, ctx=ctx) == bool(c["verdict"])
+
+
+def test_verify_length_mismatch_is_an_error(ctxs):
+    from coconut import CoconutError, verify_batch
+    d = golden("verify_g2_q6.json")
+    ctx = ctxs["G2"]
+    ctx.set_params(bytes.fromhex(d["g_tilde"]))
+    ctx.set_verkey(bytes.fromhex(d["vk"]["X"]), [bytes.fromhex(y) for y in d["vk"]["Y"]])
+    c = d["creds"][0]
+    with pytest.raises(CoconutError) as e:
+        verify_batch(ctx, 1, 5, bytes.fromhex(c["sigma1"]), bytes.fromhex(c["sigma2"]), _cat(c["msgs"][:5]))
+    assert e.value.code == -1
+
+
+@pytest.mark.parametrize("name", ["aggregate_g2.json", "aggregate_g1.json", "aggregate_g2_t67.json"])
+def test_aggregate_golden(ctxs, name):
+    from coconut import signature_aggregate_batch, verkey_aggregate_batch
+    d = golden(name)
+    ctx = ctxs[d["mode"]]
+    t, q = d["threshold"], d["q"]
+    ob = ctx.mode.other_bytes
+    for case in d["cases"]:
+        ids = case["ids"]
+        L = len(ids)
+        o1, o2 = signature_aggregate_batch(ctx, 1, L, t, [ids], _cat(case["sigma1"]), _cat(case["sigma2"]))
+        assert o1.hex() == case["out_sigma1"] and o2.hex() == case["out_sigma2"], ids
+        oX, oY = verkey_aggregate_batch(ctx, 1, L, t, q, [ids], _cat(case["X"]),
+                                        _cat(y for row in case["Y"] for y in row))
+        assert oX.hex() == case["out_X"], ids
+        assert [oY[j * ob:(j + 1) * ob].hex() for j in range(q)] == case["out_Y"], ids
+
+
+def test_aggregate_api_and_threshold_error(ctxs):
+    from coconut import CoconutError, Signature, Verkey
+    d = golden("aggregate_g2.json")
+    ctx = ctxs["G2"]
+    case = d["cases"][1]
+    sigs = [(i, Signature(bytes.fromhex(a), bytes.fromhex(b)))
+            for i, a, b in zip(case["ids"], case["sigma1"], case["sigma2"])]
+    s = Signature.aggregate(d["threshold"], sigs, ctx=ctx)
+    assert s.sigma_2.hex() == case["out_sigma2"]
+    keys = [(i, Verkey(bytes.fromhex(x), [bytes.fromhex(y) for y in ys]))
+            for i, x, ys in zip(case["ids"], case["X"], case["Y"])]
+    vk = Verkey.aggregate(d["threshold"], keys, ctx=ctx)
+    assert vk.X_tilde.hex() == d["secret_X"]
+    with pytest.raises(CoconutError):
+        Signature.aggregate(5, sigs, ctx=ctx)
+
+
+@pytest.mark.parametrize("name", ["pok_g2_q6.json", "pok_g1_q6.json", "pok_g2_q32.json", "pok_g1_q32.json"])
+def test_pok_verify_golden(ctxs, name):
+    from coconut import pok_verify_batch
+    d = golden(name)
+    ctx = ctxs[d["mode"]]
+    ctx.set_params(bytes.fromhex(d["g_tilde"]))
+    ctx.set_verkey(bytes.fromhex(d["vk"]["X"]), [bytes.fromhex(y) for y in d["vk"]["Y"]])
+    pr = d["proofs"]
+    nresp = len(pr[0]["responses"])
+    v, gts = pok_verify_batch(ctx, len(pr), d["q"], d["revealed"], nresp, _cat(p["sigma1"] for p in pr),
+                              _cat(p["sigma2"] for p in pr), _cat(p["J"] for p in pr), _cat(p["T"] for p in pr),
+                              _cat(x for p in pr for x in p["responses"]), _cat(p["chal"] for p in pr),
+                              _cat(m for p in pr for m in p["revealed_msgs"]), want_gt=True)
+    for i, p in enumerate(pr):
+        assert v[i] == p["verdict"], (i, p["kind"])
+        if p["gt"] is not None:
+            assert gts[576 * i:576 * (i + 1)].hex() == p["gt"], (i, p["kind"])
+
+
+def _gen_batch(mode, n, q, seed, bad_every=16):
+    """Valid-by-construction credentials (sigma1 = k G, sigma2 = k (x + sum y m) G) generated by the
+    C oracle; every `bad_every`-th has sigma2 off by G.  Returns inputs and expected verdicts."""
+    from oracle import coconut_ref as C
+    oc = oracle_lib()
+    rng = np.random.default_rng(seed)
+    R = C.R
+    x = int(rng.integers(1, 2**62)) * 7919 % R
+    y = [int(rng.integers(1, 2**62)) * (j + 3) % R for j in range(q)]
+    g_other = 2 if mode == 0 else 1  # OtherGroup generator (G1 for SigG2)
+    sig_group = 2 if mode == 0 else 1
+    ob, sb = (97, 192) if mode == 0 else (192, 97)
+    gt_k = (123456789).to_bytes(48, "big")
+    scal = [x] + y + [int.from_bytes(gt_k, "big")]
+    pts = ctypes.create_string_buffer(ob * (q + 2))
+    oc.oc_gen_mul(g_other, ctypes.c_size_t(q + 2), b"".join(s.to_bytes(48, "big") for s in scal), pts)
+    X, Y, gtil = pts.raw[:ob], pts.raw[ob:ob * (q + 1)], pts.raw[ob * (q + 1):]
+    msgs = rng.integers(0, 2**63, size=(n, q), dtype=np.int64)
+    ks = rng.integers(1, 2**63, size=n, dtype=np.int64)
+    e1, e2, expect = [], [], np.ones(n, dtype=np.uint8)
+    for i in range(n):
+        k = int(ks[i])
+        s = (x + sum(y[j] * int(msgs[i, j]) for j in range(q))) % R
+        e = k * s % R
+        if i % bad_every == bad_every - 1:
+            e = (e + 1) % R
+            expect[i] = 0
+        e1.append(k.to_bytes(48, "big"))
+        e2.append(e.to_bytes(48, "big"))
+    nth = min(64, os.cpu_count() or 8)
+    s1 = ctypes.create_string_buffer(sb * n)
+    s2 = ctypes.create_string_buffer(sb * n)
+    oc.oc_gen_mul_mt(sig_group, ctypes.c_size_t(n), b"".join(e1), s1, nth)
+    oc.oc_gen_mul_mt(sig_group, ctypes.c_size_t(n), b"".join(e2), s2, nth)
+    mb = b"".join(int(m).to_bytes(48, "big") for m in msgs.reshape(-1))
+    return dict(X=X, Y=Y, g_tilde=gtil, s1=s1.raw, s2=s2.raw, msgs=mb, expect=expect)
+
+
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_generated_batch_against_c_oracle(ctxs, mode):
+    """4,096 generated credentials: verdicts by construction; GT bytes of a 256-credential sample
+    against the C oracle (independent representation)."""
+    from coconut import verify_batch
+    m = MODES[mode]
+    q, n = 6, 4096
+    b = _gen_batch(m, n, q, seed=7 + m)
+    ctx = ctxs[mode]
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    v, gts = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], want_gt=True)
+    assert np.array_equal(v, b["expect"])
+    oc = oracle_lib()
+    sb = 192 if m == 0 else 97
+    k = 256
+    ver = ctypes.create_string_buffer(k)
+    ref = ctypes.create_string_buffer(576 * k)
+    oc.oc_verify_batch(m, ctypes.c_size_t(k), ctypes.c_size_t(q), b["s1"][:k * sb], b["s2"][:k * sb],
+                       b["msgs"][:k * q * 48], b["X"], b["Y"], 0, b["g_tilde"], ver, ref, min(64, os.cpu_count()))
+    assert ref.raw == gts[:576 * k]
+    assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v[:k])
+
+
+def test_full_size_batch_config2(ctxs):
+    """BASELINE config 2 size (65,536 credentials, q = 6, shared vk): every verdict equals the one
+    known by construction (size-independent property; 1/16 corrupted)."""
+    from coconut import verify_batch
+    q, n = 6, 65536
+    b = _gen_batch(0, n, q, seed=2)
+    ctx = ctxs["G2"]
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    v = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"])
+    assert np.array_equal(v, b["expect"])
