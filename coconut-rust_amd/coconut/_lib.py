@@ -33,6 +33,7 @@ _SIGS = {
     "cc_verkey_aggregate_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p]),
     "cc_pok_verify_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                     c_p, c_p]),
+    "cc_fixed_base_mul": (c_int, [c_p, c_int, c_p, c_sz, c_p, c_p]),
     "cc_last_timing": (c_int, [c_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                ctypes.POINTER(ctypes.c_float)]),
     "cc_set_timing": (c_int, [c_p, c_int]),

@@ -227,3 +227,26 @@ def verkey_aggregate_batch(ctx: Context, n: int, length: int, t: int, q: int, id
                                         ctypes.c_void_p(oX.ctypes.data), ctypes.c_void_p(oY.ctypes.data)),
           "cc_verkey_aggregate_batch")
     return oX[:n * ob].tobytes(), oY[:n * q * ob].tobytes()
+
+
+# Standard BLS12-381 generators (amcl_wrapper encodings) — public curve constants.
+G1_GENERATOR = bytes.fromhex(
+    "04"
+    "17f1d3a73197d7942695638c4fa9ac0fc3688c4f9774b905a14e3a3f171bac586c55e83ff97a1aeffb3af00adb22c6bb"
+    "08b3f481e3aaa0f1a09e30ed741d8ae4fcf5e095d5d00af600db18cb2c04b3edd03cc744a2888ae40caa232946c5e7e1")
+G2_GENERATOR = bytes.fromhex(
+    "024aa2b2f08f0a91260805272dc51051c6e47ad4fa403b02b4510b647ae3d1770bac0326a805bbefd48056c8c121bdb8"
+    "13e02b6052719f607dacd3a088274f65596bd0d09920b61ab5da61bbdc7f5049334cf11213945d57e5ac7d055d042b7e"
+    "0ce5d527727d6e118cc9cdc6da2e351aadfd9baa8cbdd3a76d429a695160d12c923ac9cc3baca289e193548608b82801"
+    "0606c4a02ea734cc32acd2b02bc28b99cb3e287e85a763af267492ab572e99ab3f370d275cec1da1aaa9075ff05f79be")
+
+
+def fixed_base_mul(ctx: Context, group: int, base: bytes, scalars: bytes) -> bytes:
+    """out_i = k_i * base on the GPU (group 1 = G1, 2 = G2); scalars n x 48 B big-endian."""
+    n = len(scalars) // FR_BYTES
+    eb = G1_BYTES if group == 1 else G2_BYTES
+    out = np.zeros(max(n, 1) * eb, dtype=np.uint8)
+    pb, k1 = buf(base)
+    ps, k2 = buf(scalars)
+    check(lib.cc_fixed_base_mul(ctx.h, group, pb, n, ps, ctypes.c_void_p(out.ctypes.data)), "cc_fixed_base_mul")
+    return out[:n * eb].tobytes()

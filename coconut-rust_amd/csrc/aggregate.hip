@@ -352,6 +352,27 @@ __global__ __launch_bounds__(256) void k_prep_pok(size_t n, int q, int r, const 
     flags[i] = fl;
 }
 
+// ================================================================ fixed-base scalar multiplication
+// out_i = k_i * B for one base B with a prebuilt 8-bit window table (keygen-style derivations:
+// reference keygen.rs:27-32 g~ * x_i, and issuer-side h * e).  Scalars are 48-byte BE Fr.
+template <class F>
+__global__ __launch_bounds__(256) void k_fixed_mul(size_t n, const uint8_t* __restrict__ ks,
+                                                   const uint32_t* __restrict__ table, uint32_t base_inf,
+                                                   uint8_t* __restrict__ out) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Jac<F> acc;
+    jac_set_inf(acc);
+    if (!base_inf) {
+        Fr k;
+        fr_from_be48(k, ks + i * 48);
+        add_fixed<F>(acc, k.v, table, 0);
+    }
+    Aff<F> r;
+    bool fin = jac_to_aff(r, acc);
+    encode_pt<F>(out + i * ebytes<F>(), r, fin);
+}
+
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 extern "C" {
@@ -389,6 +410,17 @@ int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const ui
     else
         hipLaunchKernelGGL((k_prep_pok<Fp, Fp2>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
                            d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, d_binf, d_prep, d_flags);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
+                  uint8_t* d_out, hipStream_t st) {
+    if (!n) return 0;
+    dim3 g(nblocks(n, 256)), b(256);
+    if (group == 1)
+        hipLaunchKernelGGL(k_fixed_mul<Fp>, g, b, 0, st, n, d_ks, d_table, base_inf, d_out);
+    else
+        hipLaunchKernelGGL(k_fixed_mul<Fp2>, g, b, 0, st, n, d_ks, d_table, base_inf, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

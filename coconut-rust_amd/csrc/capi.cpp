@@ -27,6 +27,8 @@ int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t
 int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
                   size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
                   hipStream_t st);
+int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
+                  uint8_t* d_out, hipStream_t st);
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
                  const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table,
@@ -341,6 +343,29 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
     if (gt) HIPCK(hipMemcpyAsync(gt, c->gt.p, n * 576, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     collect_timing(c);
+    return CC_OK;
+}
+
+cc_status cc_fixed_base_mul(cc_ctx* c, int group, const uint8_t* base, size_t n, const uint8_t* scalars,
+                            uint8_t* out) {
+    if (!c || !base || (n && (!scalars || !out)) || (group != 1 && group != 2)) return CC_ERR_DECODE;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    size_t eb = group == 1 ? 97 : 192, aw = aff_words(group);
+    hipStream_t st = c->stream;
+    DevBuf aff, inf, pw, table, ks, o;
+    if (aff.ensure(aw * 4) || inf.ensure(4) || pw.ensure((size_t)NWIN * (group == 1 ? 36 : 72) * 4) ||
+        table.ensure((size_t)NWIN * WENT * aw * 4) || ks.ensure(n * 48) || o.ensure(n * eb))
+        return CC_ERR_HIP;
+    cc_status s = decode_points_host(c, group, 1, base, aff.as<uint32_t>(), inf.as<uint32_t>());
+    if (s) return s;
+    uint32_t binf = 0;
+    HIPCK(hipMemcpy(&binf, inf.p, 4, hipMemcpyDeviceToHost));
+    KCK(cck_build_table(group, 1, aff.as<uint32_t>(), inf.as<uint32_t>(), pw.as<uint32_t>(), table.as<uint32_t>(), st));
+    HIPCK(hipMemcpyAsync(ks.p, scalars, n * 48, hipMemcpyHostToDevice, st));
+    KCK(cck_fixed_mul(group, n, ks.as<uint8_t>(), table.as<uint32_t>(), binf, o.as<uint8_t>(), st));
+    HIPCK(hipMemcpyAsync(out, o.p, n * eb, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
     return CC_OK;
 }
 

@@ -110,6 +110,12 @@ cc_status cc_pok_verify_batch(cc_ctx* ctx, size_t n, size_t q, size_t r, size_t 
                               const uint8_t* chal, const uint64_t* revealed_idx, const uint8_t* revealed_msgs,
                               uint8_t* verdicts, uint8_t* gt_or_null);
 
+/* Batch fixed-base scalar multiplication out_i = k_i * base (group 1 = G1, 2 = G2); scalars n x 48 B
+ * big-endian Fr, out n encodings.  The keygen derivation g~ * x_i (reference src/keygen.rs:27-32)
+ * and the issuer's h^e (src/signature.rs:423-428) in batch form. */
+cc_status cc_fixed_base_mul(cc_ctx* ctx, int group, const uint8_t* base, size_t n, const uint8_t* scalars,
+                            uint8_t* out);
+
 /* Kernel timing of the last cc_verify_batch_device call (HIP events on the context stream):
  * milliseconds per phase {prep, miller, fexp}.  Used by bench.py for the roofline figure. */
 cc_status cc_last_timing(const cc_ctx* ctx, float* prep_ms, float* miller_ms, float* fexp_ms);

@@ -751,15 +751,16 @@ int oc_verify_batch(int mode, size_t n, size_t q, const uint8_t* s1, const uint8
     if ((size_t)nthreads > n) nthreads = (int)(n ? n : 1);
     pthread_t th[256];
     vjob jobs[256];
+    int started[256];
     if (nthreads > 256) nthreads = 256;
     for (int t = 0; t < nthreads; t++) {
         jobs[t] = (vjob){mode, q, n * t / nthreads, n * (t + 1) / nthreads, s1, s2, msgs, X, Y, gtilde,
                          per_cred_vk, verdicts, gts};
-        if (nthreads == 1) vworker(&jobs[t]);
-        else pthread_create(&th[t], NULL, vworker, &jobs[t]);
+        started[t] = nthreads > 1 && pthread_create(&th[t], NULL, vworker, &jobs[t]) == 0;
+        if (!started[t]) vworker(&jobs[t]);
     }
-    if (nthreads > 1)
-        for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < nthreads; t++)
+        if (started[t]) pthread_join(th[t], NULL);
     return 0;
 }
 
@@ -812,11 +813,14 @@ int oc_gen_mul_mt(int group, size_t n, const uint8_t* ks, uint8_t* out, int nthr
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
     gjob jobs[256];
+    int started[256];
     for (int t = 0; t < nthreads; t++) {
         jobs[t] = (gjob){group, n * t / nthreads, n * (t + 1) / nthreads, ks, out};
-        pthread_create(&th[t], NULL, gworker, &jobs[t]);
+        started[t] = pthread_create(&th[t], NULL, gworker, &jobs[t]) == 0;
+        if (!started[t]) gworker(&jobs[t]);
     }
-    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    for (int t = 0; t < nthreads; t++)
+        if (started[t]) pthread_join(th[t], NULL);
     return 0;
 }
 

@@ -35,3 +35,12 @@ def oracle_lib():
 @pytest.fixture(scope="session")
 def oc():
     return oracle_lib()
+
+
+def host_threads():
+    """Worker threads for CPU-side helpers: the GPU box grants ~16 cores per GPU (OMP_NUM_THREADS)."""
+    try:
+        n = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        n = 0
+    return max(1, min(n or (os.cpu_count() or 8), 16))

@@ -8,7 +8,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import golden, oracle_lib
+from conftest import golden, host_threads, oracle_lib
 
 pytestmark = pytest.mark.gpu
 
@@ -146,11 +146,11 @@ def _gen_batch(mode, n, q, seed, bad_every=16):
     R = C.R
     x = int(rng.integers(1, 2**62)) * 7919 % R
     y = [int(rng.integers(1, 2**62)) * (j + 3) % R for j in range(q)]
-    g_other = 2 if mode == 0 else 1  # OtherGroup generator (G1 for SigG2)
+    g_other = 1 if mode == 0 else 2  # OtherGroup generator (G1 for SigG2)
     sig_group = 2 if mode == 0 else 1
     ob, sb = (97, 192) if mode == 0 else (192, 97)
-    gt_k = (123456789).to_bytes(48, "big")
-    scal = [x] + y + [int.from_bytes(gt_k, "big")]
+    gk = 123456789
+    scal = [x * gk % R] + [yj * gk % R for yj in y] + [gk]  # X = x g~, Y_j = y_j g~ with g~ = gk G
     pts = ctypes.create_string_buffer(ob * (q + 2))
     oc.oc_gen_mul(g_other, ctypes.c_size_t(q + 2), b"".join(s.to_bytes(48, "big") for s in scal), pts)
     X, Y, gtil = pts.raw[:ob], pts.raw[ob:ob * (q + 1)], pts.raw[ob * (q + 1):]
@@ -166,7 +166,7 @@ def _gen_batch(mode, n, q, seed, bad_every=16):
             expect[i] = 0
         e1.append(k.to_bytes(48, "big"))
         e2.append(e.to_bytes(48, "big"))
-    nth = min(64, os.cpu_count() or 8)
+    nth = host_threads()
     s1 = ctypes.create_string_buffer(sb * n)
     s2 = ctypes.create_string_buffer(sb * n)
     oc.oc_gen_mul_mt(sig_group, ctypes.c_size_t(n), b"".join(e1), s1, nth)
@@ -194,7 +194,7 @@ def test_generated_batch_against_c_oracle(ctxs, mode):
     ver = ctypes.create_string_buffer(k)
     ref = ctypes.create_string_buffer(576 * k)
     oc.oc_verify_batch(m, ctypes.c_size_t(k), ctypes.c_size_t(q), b["s1"][:k * sb], b["s2"][:k * sb],
-                       b["msgs"][:k * q * 48], b["X"], b["Y"], 0, b["g_tilde"], ver, ref, min(64, os.cpu_count()))
+                       b["msgs"][:k * q * 48], b["X"], b["Y"], 0, b["g_tilde"], ver, ref, host_threads())
     assert ref.raw == gts[:576 * k]
     assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v[:k])
 
