@@ -19,8 +19,10 @@ int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* 
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
-int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-               uint32_t* d_f, hipStream_t st);
+int cck_miller_g2(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
+                  uint32_t* d_f, hipStream_t st);
+int cck_miller_g1(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
+                  uint32_t* d_f, hipStream_t st);
 int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
              uint8_t* d_gt, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
@@ -38,6 +40,7 @@ int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const ui
 namespace {
 
 constexpr int NWIN = 32, WENT = 255;
+constexpr int PREP_SLOTS = 14;  // soa.h
 
 struct DevBuf {
     void* p = nullptr;
@@ -89,6 +92,14 @@ struct cc_ctx {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_ms[3] = {0, 0, 0};
 };
+
+// mode 0 (SigG2): d_const = g~ affine G1 (24 words); mode 1 (SigG1): g~ Miller lines (68 x 72 words).
+// lane2: pair 1's G1 point is per lane (prep slots S_P2.., Jacobian evaluation form; RLC mode).
+static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
+                      uint32_t* d_f, hipStream_t st, int lane2 = 0) {
+    return mode == 0 ? cck_miller_g2(lane2, n, d_prep, d_flags, d_const, d_f, st)
+                     : cck_miller_g1(lane2, n, d_prep, d_flags, d_const, d_f, st);
+}
 
 static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }
 static inline int oth_bytes(int mode) { return mode == 0 ? 97 : 192; }
@@ -255,8 +266,8 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
 
 static cc_status ensure_work(cc_ctx* c, size_t n) {
     size_t words = n * 12;  // one Fp slot
-    if (c->prep.ensure(words * 4 * 13) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
-        c->scratch.ensure(words * 4 * 12) || c->verdicts.ensure(n))
+    if (c->prep.ensure(words * 4 * PREP_SLOTS) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
+        c->scratch.ensure(words * 4 * 48) || c->verdicts.ensure(n))
         return CC_ERR_HIP;
     return CC_OK;
 }

@@ -27,10 +27,10 @@ struct FT<Fp> {
     static DEV void zero(Fp& r) { fp_zero(r); }
     static DEV void one(Fp& r) { fp_one(r); }
     static DEV void inv(Fp& r, const Fp& a) { fp_inv(r, a); }
-    // curve constant b = 4
+    // curve constant b = 4 (Montgomery, R = 2^406; tools/gen_constants.py)
     static DEV void curve_b(Fp& r) {
-        constexpr uint32_t B[NL] = {0x000cfff3u, 0xaa270000u, 0xfc34000au, 0x53cc0032u, 0x6b0a807fu, 0x478fe97au,
-                                    0xe6ba24d7u, 0xb1d37ebeu, 0xbf78ab2fu, 0x8ec9733bu, 0x3d83de7eu, 0x09d64551u};
+        constexpr uint32_t B[NL] = {0x0ea898bau, 0xa1d20348u, 0x27c9288fu, 0x47c6b37cu, 0x0c52aee5u, 0xdddb86ecu,
+                                    0x23d53606u, 0x7ec46095u, 0xb8dea933u, 0xbf713fa0u, 0x5b838ba6u, 0x18c3ccefu};
 #pragma unroll
         for (int j = 0; j < NL; j++) r.v[j] = B[j];
     }

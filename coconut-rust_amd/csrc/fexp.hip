@@ -1,0 +1,118 @@
+// Final-exponentiation kernel for gfx950 (AMCL `pair::fexp` via amcl_wrapper `GT::ate_2_pairing`,
+// reference src/lib.rs:13) plus the RLC product reduction.
+//
+// CC_FP_INLINE: the multiplications are inlined inside each step function; the steps themselves are
+// out of line and exchange Fp12 values through a per-lane SoA scratch (one load/store per step,
+// against thousands of Fp multiplications per step), so each step's code exists once.
+// (CC_FP_INLINE: see field.h — off until the Fp12 code is register-lean enough to inline)
+#include "codec.h"
+#include "pairing.h"
+#include "soa.h"
+
+using namespace cc;
+
+// ================================================================ final exponentiation
+// f^((p^6-1)(p^2+1)) then the hard part 3 + (x-1)^2 [p^3 + x p^2 + (x^2-1) p + x^3 - x]
+// (= 3*Phi_12(p)/r, AMCL's exponent).  Each step below is one out-of-line function reading its
+// Fp12 operands from, and writing its result to, a per-lane SoA slot (12 Fp slots each).
+enum FxOp { OP_ID = 0, OP_CONJ = 1, OP_FROB = 2, OP_FROB2 = 3 };
+
+DEV void fx_apply(Fp12& x, int op) {
+    if (op == OP_CONJ) {
+        f12_conj(x, x);
+    } else if (op == OP_FROB) {
+        Fp12 t = x;
+        f12_frob(x, t);
+    } else if (op == OP_FROB2) {
+        Fp12 t = x;
+        f12_frob2(x, t);
+    }
+}
+
+// dst <- src^-1
+static __device__ __noinline__ void fx_inv(Soa src, Soa dst, size_t i) {
+    Fp12 f, t;
+    ld_f12(f, src, i);
+    f12_inv(t, f);
+    st_f12(dst, i, t);
+}
+
+// dst <- src^3 (cyclotomic)
+static __device__ __noinline__ void fx_cube(Soa src, Soa dst, size_t i) {
+    Fp12 f, r;
+    ld_f12(f, src, i);
+    f12_cyc_sqr(r, f);
+    f12_mul(r, r, f);
+    st_f12(dst, i, r);
+}
+
+// dst <- src^x, x = -|x| (cyclotomic square-and-multiply, then conj)
+static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, size_t i) {
+    Fp12 y, r;
+    ld_f12(y, src, i);
+    cyc_pow_x(r, y);
+    st_f12(dst, i, r);
+}
+
+// dst <- op_a(a) * op_b(b)
+static __device__ __noinline__ void fx_mul(Soa a, int opa, Soa b, int opb, Soa dst, size_t i) {
+    Fp12 x, y;
+    ld_f12(x, a, i);
+    fx_apply(x, opa);
+    ld_f12(y, b, i);
+    fx_apply(y, opb);
+    f12_mul(x, x, y);
+    st_f12(dst, i, x);
+}
+
+// fbuf: Miller output f (12 slots); scratch: 4 x 12 slots (T, A, S, R)
+__global__ __launch_bounds__(256) void k_fexp(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
+                                              const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
+                                              uint8_t* __restrict__ gt_out) {
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Soa F{fbuf, n};
+    const Soa T{scratch, n}, A{scratch + (size_t)12 * NL * n, n}, S{scratch + (size_t)24 * NL * n, n},
+        R{scratch + (size_t)36 * NL * n, n};
+    fx_inv(F, T, i);
+    fx_mul(F, OP_CONJ, T, OP_ID, F, i);  // f^(p^6 - 1)
+    fx_mul(F, OP_FROB2, F, OP_ID, F, i); // ^(p^2 + 1)
+    fx_cube(F, R, i);                    // res = f^3
+    fx_pow_x(F, T, i);
+    fx_mul(T, OP_ID, F, OP_CONJ, T, i);  // t = f^(x-1)
+    fx_pow_x(T, A, i);
+    fx_mul(A, OP_ID, T, OP_CONJ, A, i);  // a = f^((x-1)^2)
+    fx_mul(A, OP_FROB2, A, OP_CONJ, S, i);
+    fx_mul(S, OP_FROB, R, OP_ID, R, i);  // res *= (a^(p^2) a^-1)^p
+    fx_pow_x(A, T, i);                   // b = a^x
+    fx_mul(T, OP_FROB2, T, OP_CONJ, S, i);
+    fx_mul(S, OP_ID, R, OP_ID, R, i);    // res *= b^(p^2) b^-1
+    fx_pow_x(T, A, i);                   // c = b^x
+    fx_mul(A, OP_FROB, R, OP_ID, R, i);  // res *= c^p
+    fx_pow_x(A, T, i);                   // d = c^x
+    fx_mul(T, OP_ID, R, OP_ID, R, i);    // res *= d
+    Fp12 res;
+    ld_f12(res, R, i);
+    const uint32_t fl = flags ? flags[i] : 0u;
+    const bool ok = f12_is_one(res) && (fl & 11u) == 0;  // sigma_1/sigma_2 = O or PoK Schnorr failure
+    verdicts[i] = ok ? 1 : 0;
+    if (gt_out) {
+        const Fp* v = reinterpret_cast<const Fp*>(&res);
+        uint8_t* o = gt_out + i * 576;
+        for (int k = 0; k < 12; k++) {
+            Fp c;
+            fp_from_mont(c, v[k]);
+            store_be48_aligned(o + 48 * k, c);
+        }
+    }
+}
+
+static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+extern "C" int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
+                        uint8_t* d_gt, hipStream_t st) {
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_fexp, dim3(nblocks(n, 256)), dim3(256), 0, st, n, d_f, d_scratch, d_flags, d_verdicts,
+                       d_gt);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

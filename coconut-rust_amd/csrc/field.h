@@ -7,9 +7,13 @@
 //     Fp4  = Fp2[s]/(s^2 - xi),  xi = 1 + i
 //     Fp12 = Fp4[w]/(w^3 - s)
 //
-// One field element per lane: 12 x 32-bit limbs in VGPRs, Montgomery form R = 2^384.
-// Multiplication is CIOS with the "no final carry" shortcut (p's top limb < 2^31 - 1), each
-// inner step a v_mad_u64_u32 chain.  All limb loops are fully unrolled so limbs stay in registers.
+// One field element per lane: 12 x 32-bit limbs in VGPRs (storage form, canonical, < p).
+// Montgomery form with R = 2^406: multiplication converts its operands to radix 2^29 (14 limbs)
+// and runs product scanning, so every column is ONE chain of v_mad_u64_u32 into a 64-bit
+// accumulator (no carry words: 28 products of < 2^58 fit), then converts back and subtracts p once.
+// Measured (tools/ubench_fpmul.hip, profiles/r01_ubench_fpmul.jsonl): 5.4e10 Fp mul/s chip-wide
+// inlined at one wave per SIMD vs 2.4e10 for the 12x32 CIOS form it replaces.  Constants in
+// Montgomery form come from tools/gen_constants.py.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -24,15 +28,21 @@ constexpr int NL = 12;  // limbs per Fp
 #define CC_P_LIMBS                                                                              \
     0xffffaaabu, 0xb9feffffu, 0xb153ffffu, 0x1eabfffeu, 0xf6b0f624u, 0x6730d2a0u, 0xf38512bfu, \
         0x64774b84u, 0x434bacd7u, 0x4b1ba7b6u, 0x397fe69au, 0x1a0111eau
-// R mod p (Montgomery one)
+// R mod p (Montgomery one), R = 2^406
 #define CC_ONE_LIMBS                                                                            \
-    0x0002fffdu, 0x76090000u, 0xc40c0002u, 0xebf4000bu, 0x53c758bau, 0x5f489857u, 0x70525745u, \
-        0x77ce5853u, 0xa256ec6du, 0x5c071a97u, 0xfa80e493u, 0x15f65ec3u
+    0x03a9fb84u, 0xc57400d2u, 0x629c4a23u, 0x6147acdeu, 0x7e6d26cbu, 0x6b0f4b0bu, 0xc2b7d6e1u, \
+        0x91ecbde7u, 0x4fdd80b8u, 0xd56a23c3u, 0xf3a0d636u, 0x13317c30u
 // R^2 mod p
 #define CC_R2_LIMBS                                                                             \
-    0x1c341746u, 0xf4df1f34u, 0x09d104f1u, 0x0a76e6a6u, 0x4c95b6d5u, 0x8de5476cu, 0x939d83c0u, \
-        0x67eb88a9u, 0xb519952du, 0x9a793e85u, 0x92cae3aau, 0x11988fe5u
-constexpr uint32_t N0 = 0xfffcfffdu;  // -p^-1 mod 2^32
+    0xd5bef7aeu, 0xa20639a1u, 0x918b764fu, 0xcd249131u, 0x9b54e6e2u, 0x3976e2d0u, 0x712d8c5cu, \
+        0x36639944u, 0x8a6de8fbu, 0xb47e72f3u, 0xb13c5b3fu, 0x19ea66a2u
+// p in radix 2^29 and -p^-1 mod 2^29
+#define CC_P29_LIMBS                                                                                     \
+    0x1fffaaabu, 0x0ff7ffffu, 0x14ffffeeu, 0x17fffd62u, 0x0f6241eau, 0x09507b58u, 0x0afd9cc3u, 0x109e70a2u, \
+        0x1764774bu, 0x121a5d66u, 0x12c6e9edu, 0x12ffcd34u, 0x00111ea3u, 0x0000000du
+constexpr uint32_t N0_29 = 0x1ffcfffdu;
+constexpr int L29 = 14;
+constexpr uint32_t M29 = 0x1fffffffu;
 
 __constant__ static const uint32_t kP[NL] = {CC_P_LIMBS};
 
@@ -115,34 +125,153 @@ DEV void fp_neg(Fp& r, const Fp& a) {
     fp_sub(r, z, a);
 }
 
-// Montgomery multiplication, CIOS without the extra carry words (gnark's no-carry variant).
-// Out of line with value semantics: keeps kernels compact (instruction-cache friendly) and stops
-// the scheduler from interleaving dozens of 12-limb products (which explodes register pressure).
-static __device__ __noinline__ Fp fp_mul_v(Fp a, Fp b) {
-    uint32_t t[NL];
-#pragma unroll
-    for (int i = 0; i < NL; i++) {
-        const uint32_t bi = b.v[i];
-        uint64_t A = (uint64_t)a.v[0] * bi + (i ? t[0] : 0u);
-        const uint32_t t0 = (uint32_t)A;
-        const uint32_t m = t0 * N0;
-        uint64_t C = (uint64_t)m * p_limb(0) + t0;
-#pragma unroll
-        for (int j = 1; j < NL; j++) {
-            A = (uint64_t)a.v[j] * bi + (uint64_t)(i ? t[j] : 0u) + (A >> 32);
-            C = (uint64_t)m * p_limb(j) + (uint64_t)(uint32_t)A + (C >> 32);
-            t[j - 1] = (uint32_t)C;
-        }
-        t[NL - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
-    }
-    Fp r;
-    fp_reduce_once(r, t);
+// ---------------------------------------------------------------- Montgomery multiplication
+DEV uint32_t p29(int j) {
+    constexpr uint32_t Q[L29] = {CC_P29_LIMBS};
+    return Q[j];
+}
+
+// c + a*b as one v_mad_u64_u32 (carry-out into VCC, unused).  Inline asm keeps the long mad
+// chains opaque to the IR combiners, which otherwise take minutes per kernel on them.
+DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+    uint64_t r;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) : "vcc");
+    return r;
+}
+// same with a wave-uniform multiplier (a limb of p) in an SGPR
+DEV uint64_t mad64s(uint32_t a, uint32_t b, uint64_t c) {
+    uint64_t r;
+    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c) : "vcc");
     return r;
 }
 
-DEV void fp_mul(Fp& r, const Fp& a, const Fp& b) { r = fp_mul_v(a, b); }
+// 12 x 32 -> 14 x 29 (value < 2^384)
+DEV void to29(uint32_t o[L29], const Fp& x) {
+    o[0] = x.v[0] & M29;
+#pragma unroll
+    for (int k = 1; k < L29 - 1; k++) {
+        const int bit = 29 * k, w = bit >> 5, s = bit & 31;
+        o[k] = (s ? __builtin_amdgcn_alignbit(x.v[w + 1], x.v[w], s) : x.v[w]) & M29;
+    }
+    o[L29 - 1] = x.v[NL - 1] >> 25;
+}
 
-DEV void fp_sqr(Fp& r, const Fp& a) { fp_mul(r, a, a); }
+// 14 x 29 (normalised limbs, value < 2p) -> canonical 12 x 32
+DEV void from29(Fp& r, const uint32_t t[L29]) {
+    uint32_t w32[NL];
+#pragma unroll
+    for (int w = 0; w < NL; w++) {
+        const int bit = 32 * w, k = bit / 29, s = bit % 29;
+        uint32_t x = t[k] >> s;
+        if (k + 1 < L29) x |= t[k + 1] << (29 - s);
+        if (s > 26 && k + 2 < L29) x |= t[k + 2] << (58 - s);
+        w32[w] = x;
+    }
+    fp_reduce_once(r, w32);
+}
+
+// Montgomery reduction columns shared by mul and sqr: the caller has added column k's a*b terms
+// to acc; this adds the m*p terms, derives m_k (k < 14) or emits limb k - 14, and shifts.
+DEV void redc_column(int k, uint64_t& acc, uint32_t m[L29], uint32_t r[L29]) {
+#pragma unroll
+    for (int i = 0; i < L29; i++) {
+        const int j = k - i;
+        if (i >= k || j < 0 || j >= L29) continue;
+        acc = mad64s(m[i], p29(j), acc);
+    }
+    if (k < L29) {
+        m[k] = ((uint32_t)acc * N0_29) & M29;
+        acc = mad64s(m[k], p29(0), acc);
+    } else {
+        r[k - L29] = (uint32_t)acc & M29;
+    }
+    acc >>= 29;
+}
+
+// a * b * 2^-406 mod p, canonical.  a, b < 2^384; column sums < 28 * 2^58 + 2^35 < 2^64.
+DEV Fp fp_mul_v(const Fp& A, const Fp& B) {
+    uint32_t a[L29], b[L29], m[L29], r[L29];
+    to29(a, A);
+    to29(b, B);
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * L29 - 1; k++) {
+#pragma unroll
+        for (int i = 0; i < L29; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= L29) continue;
+            acc = mad64(a[i], b[j], acc);
+        }
+        redc_column(k, acc, m, r);
+    }
+    r[L29 - 1] = (uint32_t)acc;
+    Fp o;
+    from29(o, r);
+    return o;
+}
+
+// a^2 * 2^-406 mod p: off-diagonal products once against the doubled operand (105 + 196 mads)
+DEV Fp fp_sqr_v(const Fp& A) {
+    uint32_t a[L29], a2[L29], m[L29], r[L29];
+    to29(a, A);
+#pragma unroll
+    for (int i = 0; i < L29; i++) a2[i] = a[i] << 1;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * L29 - 1; k++) {
+#pragma unroll
+        for (int i = 0; i < L29; i++) {
+            const int j = k - i;
+            if (j <= i || j >= L29) continue;
+            acc = mad64(a2[i], a[j], acc);
+        }
+        if (!(k & 1) && k / 2 < L29) acc = mad64(a[k / 2], a[k / 2], acc);
+        redc_column(k, acc, m, r);
+    }
+    r[L29 - 1] = (uint32_t)acc;
+    Fp o;
+    from29(o, r);
+    return o;
+}
+
+// Translation units holding the hot loops (Miller loop, final exponentiation) define CC_FP_INLINE and
+// get the multiplication inlined at every site; everywhere else it is one out-of-line copy called
+// with its 24 limbs in argument VGPRs (compile time and code size stay small).
+#ifdef CC_FP_INLINE
+// Each inlined multiplication sits in its own basic block (a loop that runs once on an opaque,
+// wave-uniform condition): instruction selection and scheduling work per block, and blocks of
+// tens of thousands of instructions (a Miller step) make their compile time explode.
+DEV bool cc_opaque_false() {
+    uint32_t x;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(x));
+    return x != 0;
+}
+DEV void fp_mul(Fp& r, const Fp& a, const Fp& b) {
+    do {
+        r = fp_mul_v(a, b);
+    } while (cc_opaque_false());
+}
+DEV void fp_sqr(Fp& r, const Fp& a) {
+    do {
+        r = fp_sqr_v(a);
+    } while (cc_opaque_false());
+}
+#else
+#define CC_L12(x) uint32_t x##0, uint32_t x##1, uint32_t x##2, uint32_t x##3, uint32_t x##4, uint32_t x##5, \
+    uint32_t x##6, uint32_t x##7, uint32_t x##8, uint32_t x##9, uint32_t x##10, uint32_t x##11
+#define CC_V12(x) x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11
+#define CC_E12(x) x.v[0], x.v[1], x.v[2], x.v[3], x.v[4], x.v[5], x.v[6], x.v[7], x.v[8], x.v[9], x.v[10], x.v[11]
+static __device__ __noinline__ Fp fp_mul_call(CC_L12(a), CC_L12(b)) {
+    const Fp A = {{CC_V12(a)}}, B = {{CC_V12(b)}};
+    return fp_mul_v(A, B);
+}
+static __device__ __noinline__ Fp fp_sqr_call(CC_L12(a)) {
+    const Fp A = {{CC_V12(a)}};
+    return fp_sqr_v(A);
+}
+DEV void fp_mul(Fp& r, const Fp& a, const Fp& b) { r = fp_mul_call(CC_E12(a), CC_E12(b)); }
+DEV void fp_sqr(Fp& r, const Fp& a) { r = fp_sqr_call(CC_E12(a)); }
+#endif
 
 // a * small constant via additions (k <= 12)
 DEV void fp_mul_small(Fp& r, const Fp& a, int k) {

@@ -14,6 +14,7 @@
 // or SigG1 (sigma in G1, vk in G2).
 #include "codec.h"
 #include "pairing.h"
+#include "soa.h"
 
 using namespace cc;
 
@@ -22,34 +23,6 @@ namespace {
 constexpr int WIN = 8;                 // fixed-base window bits
 constexpr int NWIN = 32;               // 256 / WIN windows per scalar
 constexpr int WENT = (1 << WIN) - 1;   // entries per window (digit 1..255)
-
-// ---------------------------------------------------------------- SoA helpers
-struct Soa {
-    uint32_t* p;
-    size_t n;  // stride between limbs (= batch capacity)
-};
-
-DEV void st_fp(const Soa& s, int slot, size_t i, const Fp& x) {
-#pragma unroll
-    for (int k = 0; k < NL; k++) s.p[((size_t)slot * NL + k) * s.n + i] = x.v[k];
-}
-DEV void ld_fp(Fp& x, const Soa& s, int slot, size_t i) {
-#pragma unroll
-    for (int k = 0; k < NL; k++) x.v[k] = s.p[((size_t)slot * NL + k) * s.n + i];
-}
-DEV void st_f2(const Soa& s, int slot, size_t i, const Fp2& x) { st_fp(s, slot, i, x.a); st_fp(s, slot + 1, i, x.b); }
-DEV void ld_f2(Fp2& x, const Soa& s, int slot, size_t i) { ld_fp(x.a, s, slot, i); ld_fp(x.b, s, slot + 1, i); }
-
-DEV void st_f12(const Soa& s, size_t i, const Fp12& x) {
-    const Fp* v = reinterpret_cast<const Fp*>(&x);
-#pragma unroll
-    for (int k = 0; k < 12; k++) st_fp(s, k, i, v[k]);
-}
-DEV void ld_f12(Fp12& x, const Soa& s, size_t i) {
-    Fp* v = reinterpret_cast<Fp*>(&x);
-#pragma unroll
-    for (int k = 0; k < 12; k++) ld_fp(v[k], s, k, i);
-}
 
 // AoS point loads (table entries, constants): F words contiguous
 template <class F>
@@ -70,15 +43,6 @@ DEV void ld_aff_aos(Aff<F>& a, const uint32_t* p) {
     }
 }
 
-DEV void ld_f2_aos(Fp2& a, const uint32_t* p) {
-    const uint4* q = reinterpret_cast<const uint4*>(p);
-    uint32_t* d = reinterpret_cast<uint32_t*>(&a);
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-        uint4 t = q[k];
-        d[4 * k] = t.x; d[4 * k + 1] = t.y; d[4 * k + 2] = t.z; d[4 * k + 3] = t.w;
-    }
-}
 
 template <class F>
 DEV void st_aff_aos(uint32_t* p, const Aff<F>& a) {
@@ -115,7 +79,7 @@ constexpr int enc_bytes() { return sizeof(F) == sizeof(Fp) ? 97 : 192; }
 // ================================================================ point decode (setup path)
 // out: AoS affine (2*W words per point, Montgomery) + inf flags
 template <class F>
-__global__ void k_decode_points(size_t n, const uint8_t* __restrict__ bytes, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(64) void k_decode_points(size_t n, const uint8_t* __restrict__ bytes, uint32_t* __restrict__ out,
                                 uint32_t* __restrict__ inf) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -128,7 +92,7 @@ __global__ void k_decode_points(size_t n, const uint8_t* __restrict__ bytes, uin
 // ================================================================ fixed-base tables
 // T1: per (base j, window w): 2^(8w) * B_j (Jacobian, AoS)
 template <class F>
-__global__ void k_table_pow2(int nbases, const uint32_t* __restrict__ bases, const uint32_t* __restrict__ inf,
+__global__ __launch_bounds__(64) void k_table_pow2(int nbases, const uint32_t* __restrict__ bases, const uint32_t* __restrict__ inf,
                              uint32_t* __restrict__ pw) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= nbases * NWIN) return;
@@ -147,7 +111,7 @@ __global__ void k_table_pow2(int nbases, const uint32_t* __restrict__ bases, con
 
 // T2: per (j, w, d): d * 2^(8w) * B_j, affine AoS entry
 template <class F>
-__global__ void k_table_fill(int nbases, const uint32_t* __restrict__ pw, uint32_t* __restrict__ table) {
+__global__ __launch_bounds__(64) void k_table_fill(int nbases, const uint32_t* __restrict__ pw, uint32_t* __restrict__ table) {
     size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (t >= (size_t)nbases * NWIN * WENT) return;
     int d = (int)(t % WENT) + 1;
@@ -232,7 +196,7 @@ DEV void msm_var(Jac<F>& acc, const uint8_t* msgs, int q, const Soa& bases, cons
 
 // per-credential verkey decode into SoA scratch (+ canonicalised message copy)
 template <class F>
-__global__ void k_decode_vk(size_t n, int q, const uint8_t* __restrict__ X, const uint8_t* __restrict__ Y,
+__global__ __launch_bounds__(64) void k_decode_vk(size_t n, int q, const uint8_t* __restrict__ X, const uint8_t* __restrict__ Y,
                             uint32_t* __restrict__ bases, size_t stride, uint32_t* __restrict__ binf,
                             const uint8_t* __restrict__ msgs, uint8_t* __restrict__ msgs_canon) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -258,9 +222,6 @@ __global__ void k_decode_vk(size_t n, int q, const uint8_t* __restrict__ X, cons
 }
 
 // ================================================================ prep kernels
-// Prep SoA slots: Q1 0..3 | Q2 4..7 | P1 8..10 (px, py, pz) | P2 11..12 ; flags word per lane:
-//   bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 pair-1 degenerate (pr = O)
-enum { S_Q1 = 0, S_Q2 = 4, S_P1 = 8, S_P2 = 11, PREP_SLOTS = 13 };
 
 // SigG2: sigma in G2 (192 B), verkey in G1
 template <bool kFixed>
@@ -343,88 +304,9 @@ __global__ __launch_bounds__(256) void k_prep_sigg1(size_t n, int q, const uint8
     flags[i] = fl;
 }
 
-// ================================================================ Miller loops
-DEV void neutralise(Fp2& a0, Fp2& a2, Fp2& a3, bool skip) {
-    if (skip) {
-        f2_one(a0);
-        f2_zero(a2);
-        f2_zero(a3);
-    }
-}
-
-// SigG2: pair 1 = (Q sigma_1, P pr [Jacobian eval]), pair 2 = (Q -sigma_2, P g~ [constant])
-__global__ __launch_bounds__(256) void k_miller_sigg2(size_t n, const uint32_t* __restrict__ prep,
-                                                      const uint32_t* __restrict__ flags,
-                                                      const uint32_t* __restrict__ gtilde,
-                                                      uint32_t* __restrict__ fout) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Soa S{const_cast<uint32_t*>(prep), n};
-    const uint32_t fl = flags[i];
-    const bool skip1 = (fl & 5u) != 0;  // sigma_1 = O or pr = O
-    const bool skip2 = (fl & 2u) != 0;  // sigma_2 = O
-    G2Proj T1, T2;
-    ld_f2(T1.x, S, S_Q1, i);
-    ld_f2(T1.y, S, S_Q1 + 2, i);
-    f2_one(T1.z);
-    ld_f2(T2.x, S, S_Q2, i);
-    ld_f2(T2.y, S, S_Q2 + 2, i);
-    f2_one(T2.z);
-    G1Eval P1, P2;
-    ld_fp(P1.px, S, S_P1, i);
-    ld_fp(P1.py, S, S_P1 + 1, i);
-    ld_fp(P1.pz, S, S_P1 + 2, i);
-#pragma unroll
-    for (int k = 0; k < NL; k++) {
-        P2.px.v[k] = gtilde[k];
-        P2.py.v[k] = gtilde[NL + k];
-    }
-    Fp12 f;
-    f12_one(f);
-#pragma unroll 1
-    for (int b = 62; b >= 0; b--) {
-        if (b != 62) f12_sqr(f, f);
-        Fp2 l0, l2, l3, a0, a2, a3;
-        line_dbl(T1, l0, l2, l3);
-        f2_mul_fp(a0, l0, P1.pz);
-        f2_mul_fp(a2, l2, P1.px);
-        f2_mul_fp(a3, l3, P1.py);
-        neutralise(a0, a2, a3, skip1);
-        f12_mul_line(f, a0, a2, a3);
-        line_dbl(T2, l0, l2, l3);
-        f2_mul_fp(a2, l2, P2.px);
-        f2_mul_fp(a3, l3, P2.py);
-        a0 = l0;
-        neutralise(a0, a2, a3, skip2);
-        f12_mul_line(f, a0, a2, a3);
-        if ((X_ABS >> b) & 1ull) {
-            Aff<Fp2> Q;
-            ld_f2(Q.x, S, S_Q1, i);
-            ld_f2(Q.y, S, S_Q1 + 2, i);
-            line_add(T1, Q, l0, l2, l3);
-            f2_mul_fp(a0, l0, P1.pz);
-            f2_mul_fp(a2, l2, P1.px);
-            f2_mul_fp(a3, l3, P1.py);
-            neutralise(a0, a2, a3, skip1);
-            f12_mul_line(f, a0, a2, a3);
-            ld_f2(Q.x, S, S_Q2, i);
-            ld_f2(Q.y, S, S_Q2 + 2, i);
-            line_add(T2, Q, l0, l2, l3);
-            f2_mul_fp(a2, l2, P2.px);
-            f2_mul_fp(a3, l3, P2.py);
-            a0 = l0;
-            neutralise(a0, a2, a3, skip2);
-            f12_mul_line(f, a0, a2, a3);
-        }
-    }
-    f12_conj(f, f);
-    st_f12(Soa{fout, n}, i, f);
-}
-
 // Fixed-argument lines for the constant G2 point g~ (SigG1): per Miller step, (l0, l2c, l3c)
 // — 63 doubling + 5 addition steps, stored in loop order.  One thread computes them at setup.
-constexpr int NLINES = 68;
-__global__ void k_gtilde_lines(const uint32_t* __restrict__ gtilde, uint32_t* __restrict__ lines) {
+__global__ __launch_bounds__(64) void k_gtilde_lines(const uint32_t* __restrict__ gtilde, uint32_t* __restrict__ lines) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     Aff<Fp2> Q;
     ld_aff_aos<Fp2>(Q, gtilde);
@@ -452,148 +334,6 @@ __global__ void k_gtilde_lines(const uint32_t* __restrict__ gtilde, uint32_t* __
         if ((X_ABS >> b) & 1ull) {
             line_add(T, Q, l0, l2, l3);
             put(l0, l2, l3);
-        }
-    }
-}
-
-// SigG1: pair 1 = (Q pr, P sigma_1), pair 2 = (Q g~ [precomputed lines], P -sigma_2)
-__global__ __launch_bounds__(256) void k_miller_sigg1(size_t n, const uint32_t* __restrict__ prep,
-                                                      const uint32_t* __restrict__ flags,
-                                                      const uint32_t* __restrict__ glines,
-                                                      uint32_t* __restrict__ fout) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Soa S{const_cast<uint32_t*>(prep), n};
-    const uint32_t fl = flags[i];
-    const bool skip1 = (fl & 5u) != 0;
-    const bool skip2 = (fl & 2u) != 0;
-    G2Proj T1;
-    ld_f2(T1.x, S, S_Q1, i);
-    ld_f2(T1.y, S, S_Q1 + 2, i);
-    f2_one(T1.z);
-    G1Eval P1, P2;
-    ld_fp(P1.px, S, S_P1, i);
-    ld_fp(P1.py, S, S_P1 + 1, i);
-    ld_fp(P2.px, S, S_P2, i);
-    ld_fp(P2.py, S, S_P2 + 1, i);
-    Fp12 f;
-    f12_one(f);
-    int k = 0;
-#pragma unroll 1
-    for (int b = 62; b >= 0; b--) {
-        if (b != 62) f12_sqr(f, f);
-        Fp2 l0, l2, l3, a0, a2, a3;
-        line_dbl(T1, l0, l2, l3);
-        f2_mul_fp(a2, l2, P1.px);
-        f2_mul_fp(a3, l3, P1.py);
-        a0 = l0;
-        neutralise(a0, a2, a3, skip1);
-        f12_mul_line(f, a0, a2, a3);
-        {
-            const uint32_t* L = glines + (size_t)k * 72;
-            ld_f2_aos(l0, L);
-            ld_f2_aos(l2, L + 24);
-            ld_f2_aos(l3, L + 48);
-            k++;
-        }
-        f2_mul_fp(a2, l2, P2.px);
-        f2_mul_fp(a3, l3, P2.py);
-        a0 = l0;
-        neutralise(a0, a2, a3, skip2);
-        f12_mul_line(f, a0, a2, a3);
-        if ((X_ABS >> b) & 1ull) {
-            Aff<Fp2> Q;
-            ld_f2(Q.x, S, S_Q1, i);
-            ld_f2(Q.y, S, S_Q1 + 2, i);
-            line_add(T1, Q, l0, l2, l3);
-            f2_mul_fp(a2, l2, P1.px);
-            f2_mul_fp(a3, l3, P1.py);
-            a0 = l0;
-            neutralise(a0, a2, a3, skip1);
-            f12_mul_line(f, a0, a2, a3);
-            {
-                const uint32_t* L = glines + (size_t)k * 72;
-                ld_f2_aos(l0, L);
-                ld_f2_aos(l2, L + 24);
-                ld_f2_aos(l3, L + 48);
-                k++;
-            }
-            f2_mul_fp(a2, l2, P2.px);
-            f2_mul_fp(a3, l3, P2.py);
-            a0 = l0;
-            neutralise(a0, a2, a3, skip2);
-            f12_mul_line(f, a0, a2, a3);
-        }
-    }
-    f12_conj(f, f);
-    st_f12(Soa{fout, n}, i, f);
-}
-
-// ================================================================ final exponentiation
-// easy part then 3 + (x-1)^2 [p^3 + x p^2 + (x^2-1) p + x^3 - x]  (= 3*Phi_12(p)/r, AMCL's);
-// `res` is parked in a scratch SoA between its five updates to keep register pressure down.
-__global__ __launch_bounds__(256) void k_fexp(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
-                                              const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
-                                              uint8_t* __restrict__ gt_out) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Soa F{fbuf, n}, R{scratch, n};
-    Fp12 f, t, res;
-    ld_f12(f, F, i);
-    // easy part
-    f12_inv(t, f);
-    f12_conj(f, f);
-    f12_mul(f, f, t);     // f^(p^6 - 1)
-    f12_frob2(t, f);
-    f12_mul(f, t, f);     // ^(p^2 + 1)
-    // res = f^3
-    f12_cyc_sqr(res, f);
-    f12_mul(res, res, f);
-    st_f12(R, i, res);
-    // t = f^(x-1)
-    cyc_pow_x(t, f);
-    f12_conj(f, f);
-    f12_mul(t, t, f);
-    // a = t^(x-1) = f^((x-1)^2)
-    cyc_pow_x(f, t);
-    f12_conj(t, t);
-    f12_mul(f, f, t);     // f := a
-    // res *= frob(frob2(a) * conj(a))
-    f12_frob2(t, f);
-    f12_conj(res, f);
-    f12_mul(t, t, res);
-    f12_frob(t, t);
-    ld_f12(res, R, i);
-    f12_mul(res, res, t);
-    st_f12(R, i, res);
-    // b = a^x ; res *= frob2(b) * conj(b)
-    cyc_pow_x(f, f);
-    f12_frob2(t, f);
-    f12_conj(res, f);
-    f12_mul(t, t, res);
-    ld_f12(res, R, i);
-    f12_mul(res, res, t);
-    st_f12(R, i, res);
-    // c = b^x ; res *= frob(c)
-    cyc_pow_x(f, f);
-    f12_frob(t, f);
-    ld_f12(res, R, i);
-    f12_mul(res, res, t);
-    st_f12(R, i, res);
-    // d = c^x ; res *= d
-    cyc_pow_x(f, f);
-    ld_f12(res, R, i);
-    f12_mul(res, res, f);
-    const uint32_t fl = flags ? flags[i] : 0u;
-    bool ok = f12_is_one(res) && (fl & 11u) == 0;  // sigma_1/sigma_2 = O or PoK Schnorr failure
-    verdicts[i] = ok ? 1 : 0;
-    if (gt_out) {
-        const Fp* v = reinterpret_cast<const Fp*>(&res);
-        uint8_t* o = gt_out + i * 576;
-        for (int k = 0; k < 12; k++) {
-            Fp c;
-            fp_from_mont(c, v[k]);
-            store_be48_aligned(o + 48 * k, c);
         }
     }
 }
@@ -676,28 +416,6 @@ int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const ui
             hipLaunchKernelGGL(k_prep_sigg1<false>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
                                d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
     }
-    CC_CHECK(hipGetLastError());
-    return 0;
-}
-
-// mode 0: d_const = g~ affine G1 (24 words); mode 1: d_const = g~ Miller lines (68 x 72 words)
-int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-               uint32_t* d_f, hipStream_t st) {
-    if (!n) return 0;
-    dim3 g(nblocks(n, 256)), b(256);
-    if (mode == 0)
-        hipLaunchKernelGGL(k_miller_sigg2, g, b, 0, st, n, d_prep, d_flags, d_const, d_f);
-    else
-        hipLaunchKernelGGL(k_miller_sigg1, g, b, 0, st, n, d_prep, d_flags, d_const, d_f);
-    CC_CHECK(hipGetLastError());
-    return 0;
-}
-
-int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
-             uint8_t* d_gt, hipStream_t st) {
-    if (!n) return 0;
-    hipLaunchKernelGGL(k_fexp, dim3(nblocks(n, 256)), dim3(256), 0, st, n, d_f, d_scratch, d_flags, d_verdicts,
-                       d_gt);
     CC_CHECK(hipGetLastError());
     return 0;
 }
