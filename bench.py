@@ -151,7 +151,10 @@ def main():
     d_s2 = torch.frombuffer(bytearray(batch["s2"]), dtype=torch.uint8).to(dev)
     d_m = torch.frombuffer(bytearray(batch["msgs"]), dtype=torch.uint8).to(dev)
     d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated (non-null) stream, ordered after the uploads; a NULL handle would select the
+    # context's own non-blocking stream
+    stream = torch.cuda.Stream(dev)
+    stream.wait_stream(torch.cuda.current_stream(dev))
     sh = ctypes.c_void_p(stream.cuda_stream)
     lib = coconut._lib.lib
 

@@ -34,6 +34,8 @@ _SIGS = {
     "cc_pok_verify_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
                                     c_p, c_p]),
     "cc_fixed_base_mul": (c_int, [c_p, c_int, c_p, c_sz, c_p, c_p]),
+    "cc_rlc_partial_device": (c_int, [c_p, c_sz, c_sz, ctypes.c_uint64, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "cc_rlc_finish_device": (c_int, [c_p, c_sz, c_p, c_p, c_p, c_p]),
     "cc_last_timing": (c_int, [c_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                ctypes.POINTER(ctypes.c_float)]),
     "cc_set_timing": (c_int, [c_p, c_int]),

@@ -1,0 +1,132 @@
+"""Multi-GPU batch verification: one process per GPU over torch.distributed (backend "nccl" is RCCL
+on ROCm, riding xGMI between the GPUs of a node).  SURVEY.md §8e.
+
+The batch shards by credential (credentials are independent):
+
+* per-credential mode — every rank verifies its own contiguous slice; no collective on the data
+  path (verdicts stay with the rank that owns the slice);
+* RLC mode — every rank reduces its slice to one 145-word partial (the Fp12 Miller product of its
+  delta-weighted pairs + an identity flag, ``cc_rlc_partial_device``); ONE all-gather of the partials
+  (580 B per rank) is the only exchange; every rank multiplies the gathered partials and runs the
+  single final exponentiation (``cc_rlc_finish_device``), so all ranks reach the same accept/reject
+  decision without a second collective.  On reject every rank falls back to per-credential
+  verification of its own slice, so verdicts always equal the reference's
+  (``Signature::verify``, reference src/signature.rs:473-478, per credential).
+
+Engines decouple this control flow from the device: ``DeviceEngine`` drives libcoconut_hip.so on
+device-resident tensors; tests substitute a CPU engine to exercise the same sharding, gather and
+decision logic over the gloo backend.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+PARTIAL_WORDS = 145  # 144 Fp12 Montgomery words + identity flag
+
+
+def shard_bounds(n: int, world: int, rank: int):
+    """Contiguous slice [lo, hi) of an n-credential batch owned by `rank` of `world`."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def _dist():
+    import torch.distributed as dist
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
+def gather_partials(part, group=None):
+    """All-gather the per-rank partials (one tensor of PARTIAL_WORDS int32 each) -> (stacked, k)."""
+    import torch
+    dist = _dist()
+    world = dist.get_world_size(group) if dist else 1
+    if world == 1:
+        return part.reshape(1, -1), 1
+    parts = [torch.empty_like(part) for _ in range(world)]
+    dist.all_gather(parts, part, group=group)
+    return torch.stack(parts), world
+
+
+def rlc_accept(engine, group=None) -> bool:
+    """One RLC decision for the whole (sharded) batch: partial -> all-gather -> finish."""
+    part = engine.partial()
+    allp, k = gather_partials(part, group)
+    return engine.finish(allp, k)
+
+
+def verify_sharded(engine, rlc: bool = True, group=None) -> np.ndarray:
+    """Verdicts (uint8) for this rank's slice; RLC first when requested, per-credential fallback."""
+    if rlc and rlc_accept(engine, group):
+        return np.ones(engine.n, dtype=np.uint8)
+    return engine.per_credential()
+
+
+class DeviceEngine:
+    """One rank's slice, resident in HBM as torch tensors, checked through the C ABI."""
+
+    def __init__(self, ctx, n: int, q: int, d_s1, d_s2, d_msgs, base_index: int = 0,
+                 seed: Optional[bytes] = None, stream=None):
+        import torch
+        from ._lib import lib
+        self.lib, self.ctx, self.n, self.q = lib, ctx, n, q
+        self.d_s1, self.d_s2, self.d_msgs = d_s1, d_s2, d_msgs
+        self.base_index = base_index
+        self.seed = seed
+        self.dev = d_s1.device
+        # a real (non-null) stream: a NULL handle would select the context's own non-blocking stream,
+        # which is not ordered against torch's default stream
+        self.stream = stream if stream is not None else torch.cuda.Stream(self.dev)
+        self._sh = ctypes.c_void_p(self.stream.cuda_stream)
+        self.part = torch.empty(PARTIAL_WORDS, dtype=torch.int32, device=self.dev)
+        self.accept = torch.zeros(1, dtype=torch.uint8, device=self.dev)
+        self.verdicts = torch.zeros(n, dtype=torch.uint8, device=self.dev)
+
+    def _enter(self):
+        import torch
+        self.stream.wait_stream(torch.cuda.current_stream(self.dev))
+
+    def _leave(self):
+        import torch
+        torch.cuda.current_stream(self.dev).wait_stream(self.stream)
+
+    def _check(self, st, what):
+        if st != 0:
+            from .errors import CoconutError
+            raise CoconutError(st, f"{what}: {self.lib.cc_status_str(st).decode()}")
+
+    def partial(self):
+        seed = self.seed if self.seed is not None else os.urandom(32)
+        self._enter()
+        self._check(self.lib.cc_rlc_partial_device(self.ctx.h, self.n, self.q, self.base_index, seed,
+                                                   ctypes.c_void_p(self.d_s1.data_ptr()),
+                                                   ctypes.c_void_p(self.d_s2.data_ptr()),
+                                                   ctypes.c_void_p(self.d_msgs.data_ptr()),
+                                                   ctypes.c_void_p(self.part.data_ptr()), self._sh),
+                    "cc_rlc_partial_device")
+        self._leave()
+        return self.part
+
+    def finish(self, allp, k: int, sync: bool = True):
+        allp = allp.contiguous()
+        self._enter()
+        self._check(self.lib.cc_rlc_finish_device(self.ctx.h, k, ctypes.c_void_p(allp.data_ptr()),
+                                                  ctypes.c_void_p(self.accept.data_ptr()), None, self._sh),
+                    "cc_rlc_finish_device")
+        self._leave()
+        if not sync:
+            return None
+        return bool(self.accept.item())
+
+    def per_credential(self) -> np.ndarray:
+        self._enter()
+        self._check(self.lib.cc_verify_batch_device(self.ctx.h, self.n, self.q,
+                                                    ctypes.c_void_p(self.d_s1.data_ptr()),
+                                                    ctypes.c_void_p(self.d_s2.data_ptr()),
+                                                    ctypes.c_void_p(self.d_msgs.data_ptr()),
+                                                    ctypes.c_void_p(self.verdicts.data_ptr()), None, self._sh),
+                    "cc_verify_batch_device")
+        self._leave()
+        return self.verdicts.cpu().numpy()

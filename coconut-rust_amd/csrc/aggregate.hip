@@ -10,104 +10,12 @@
 //                    J' = X~ + J + sum_revealed Y~_i m_i, written in the verify kernels' Miller-loop
 //                    operand layout so k_miller_* / k_fexp finish the 2-pairing check.
 #include "codec.h"
+#include "fr.h"
 #include "pairing.h"
 
 using namespace cc;
 
 namespace {
-
-// ---------------------------------------------------------------- Fr (mod r) Montgomery, R = 2^256
-constexpr int NR = 8;
-#define CC_RR2 0xf3f29c6du, 0xc999e990u, 0x87925c23u, 0x2b6cedcbu, 0x7254398fu, 0x05d31496u, 0x9f59ff11u, 0x0748d9d9u
-#define CC_RONE 0xfffffffeu, 0x00000001u, 0x00034802u, 0x5884b7fau, 0xecbc4ff5u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u
-__constant__ static const uint32_t kRm2[NR] = {0xffffffffu, 0xfffffffeu, 0xfffe5bfeu, 0x53bda402u,
-                                               0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
-
-struct Fm {
-    uint32_t v[NR];
-};
-
-DEV uint32_t rl(int j) {
-    constexpr uint32_t Rl[NR] = {CC_R_LIMBS};
-    return Rl[j];
-}
-
-DEV void fm_reduce_once(Fm& r, const uint32_t t[NR]) {
-    uint32_t s[NR], br = 0;
-#pragma unroll
-    for (int j = 0; j < NR; j++) s[j] = __builtin_subc(t[j], rl(j), br, &br);
-#pragma unroll
-    for (int j = 0; j < NR; j++) r.v[j] = br ? t[j] : s[j];
-}
-
-static __device__ __noinline__ Fm fm_mul_v(Fm a, Fm b) {
-    uint32_t t[NR];
-#pragma unroll
-    for (int i = 0; i < NR; i++) {
-        const uint32_t bi = b.v[i];
-        uint64_t A = (uint64_t)a.v[0] * bi + (i ? t[0] : 0u);
-        const uint32_t t0 = (uint32_t)A;
-        const uint32_t m = t0 * 0xffffffffu;  // -r^-1 mod 2^32
-        uint64_t C = (uint64_t)m * rl(0) + t0;
-#pragma unroll
-        for (int j = 1; j < NR; j++) {
-            A = (uint64_t)a.v[j] * bi + (uint64_t)(i ? t[j] : 0u) + (A >> 32);
-            C = (uint64_t)m * rl(j) + (uint64_t)(uint32_t)A + (C >> 32);
-            t[j - 1] = (uint32_t)C;
-        }
-        t[NR - 1] = (uint32_t)(C >> 32) + (uint32_t)(A >> 32);
-    }
-    Fm r;
-    fm_reduce_once(r, t);
-    return r;
-}
-
-DEV void fm_sub(Fm& r, const Fm& a, const Fm& b) {
-    uint32_t t[NR], br = 0;
-#pragma unroll
-    for (int j = 0; j < NR; j++) t[j] = __builtin_subc(a.v[j], b.v[j], br, &br);
-    uint32_t mask = 0u - br, c = 0;
-#pragma unroll
-    for (int j = 0; j < NR; j++) r.v[j] = __builtin_addc(t[j], rl(j) & mask, c, &c);
-}
-
-DEV Fm fm_from_u64(uint64_t x) {
-    constexpr uint32_t R2[NR] = {CC_RR2};
-    Fm a, r2;
-#pragma unroll
-    for (int j = 0; j < NR; j++) {
-        a.v[j] = 0;
-        r2.v[j] = R2[j];
-    }
-    a.v[0] = (uint32_t)x;
-    a.v[1] = (uint32_t)(x >> 32);
-    return fm_mul_v(a, r2);  // x < 2^64 < r
-}
-
-DEV Fm fm_one() {
-    constexpr uint32_t O[NR] = {CC_RONE};
-    Fm a;
-#pragma unroll
-    for (int j = 0; j < NR; j++) a.v[j] = O[j];
-    return a;
-}
-
-DEV Fm fm_inv(const Fm& a) {
-    Fm acc = a;
-    for (int bit = 254 - 1; bit >= 0; bit--) {  // r - 2 has its top bit at 254
-        acc = fm_mul_v(acc, acc);
-        if ((kRm2[bit >> 5] >> (bit & 31)) & 1u) acc = fm_mul_v(acc, a);
-    }
-    return acc;
-}
-
-DEV Fm fm_to_canon(const Fm& a) {
-    Fm one;
-#pragma unroll
-    for (int j = 0; j < NR; j++) one.v[j] = 0;
-    one.v[0] = 1;
-    return fm_mul_v(a, one);
-}
 
 // ---------------------------------------------------------------- SoA helpers (local copies)
 struct Soa {

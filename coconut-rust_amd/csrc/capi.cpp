@@ -3,6 +3,7 @@
 // aggregate.hip — there is no CPU fallback in this library.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <vector>
@@ -31,6 +32,12 @@ int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_
                   hipStream_t st);
 int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
                   uint8_t* d_out, hipStream_t st);
+int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
+                 const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, const uint32_t* d_binf,
+                 uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, hipStream_t st);
+int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any, uint32_t* d_partial,
+                   hipStream_t st);
+int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t* d_flag, hipStream_t st);
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
                  const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table,
@@ -79,14 +86,17 @@ struct cc_ctx {
     // verkey
     bool have_vk = false;
     size_t q = 0;
-    DevBuf vk_aff;       // (q + 2) points: X~, Y~[q], g~ (AoS)
-    DevBuf vk_inf;       // (q + 2) flags
-    DevBuf table;        // fixed-base tables for Y~[0..q) and g~ (q + 1 bases)
-    DevBuf table_inf;    // q + 1 base flags
+    DevBuf vk_aff;       // (q + 3) points: X~, Y~[q], g~, X~ (AoS)
+    DevBuf vk_inf;       // (q + 3) flags
+    DevBuf table;        // fixed-base tables for Y~[0..q), g~ and X~ (q + 2 bases; X~ for RLC)
+    DevBuf table_inf;    // q + 2 base flags
     uint32_t X_inf = 0;
     // workspaces
     DevBuf in_s1, in_s2, in_msgs, in_vkX, in_vkY, in_aux[6];
     DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, vkbinf, msgs_canon, lag;
+    // RLC batch mode: ChaCha20 key, identity flag word, partial / gathered partials, verdict
+    DevBuf rlc_key, rlc_any, rlc_part, rlc_flag, rlc_accept;
+    uint32_t rlc_key_host[8] = {0};
     // timing
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -157,7 +167,8 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
-                      &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag};
+                      &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag,
+                      &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept};
     for (auto* b : bufs) b->release();
     for (auto& b : c->in_aux) b.release();
     for (auto& e : c->ev) if (e) hipEventDestroy(e);
@@ -199,13 +210,13 @@ static cc_status decode_points_host(cc_ctx* c, int group, size_t n, const uint8_
 }
 
 static cc_status rebuild_tables(cc_ctx* c) {
-    // bases for the fixed-base tables: Y~[0..q) then g~ (PoK Schnorr base) -> q + 1 bases
+    // bases for the fixed-base tables: Y~[0..q), g~ (PoK Schnorr base), X~ (RLC) -> q + 2 bases
     int og = oth_group(c->mode);
     size_t aw = aff_words(og);
-    int nb = (int)c->q + 1;
+    int nb = (int)c->q + 2;
     if (c->table.ensure((size_t)nb * NWIN * WENT * aw * 4)) return CC_ERR_HIP;
     if (c->table_inf.ensure((size_t)nb * 4)) return CC_ERR_HIP;
-    // assemble [Y~..., g~] contiguous from vk_aff (X~ at 0, Y~ at 1..q, g~ at q+1)
+    // [Y~..., g~, X~] are contiguous in vk_aff (X~ at 0, Y~ at 1..q, g~ at q+1, X~ again at q+2)
     HIPCK(hipMemcpyAsync(c->table_inf.p, c->vk_inf.as<uint32_t>() + 1, (size_t)nb * 4, hipMemcpyDeviceToDevice,
                          c->stream));
     DevBuf pw;
@@ -253,11 +264,13 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
     std::vector<uint8_t> all((q + 1) * eb);
     memcpy(all.data(), X, eb);
     if (q) memcpy(all.data() + eb, Y, q * eb);
-    if (c->vk_aff.ensure((q + 2) * aw * 4) || c->vk_inf.ensure((q + 2) * 4)) return CC_ERR_HIP;
+    if (c->vk_aff.ensure((q + 3) * aw * 4) || c->vk_inf.ensure((q + 3) * 4)) return CC_ERR_HIP;
     cc_status s = decode_points_host(c, og, q + 1, all.data(), c->vk_aff.as<uint32_t>(), c->vk_inf.as<uint32_t>());
     if (s) return s;
     HIPCK(hipMemcpy(c->vk_aff.as<uint32_t>() + (q + 1) * aw, c->gtilde_aff.p, aw * 4, hipMemcpyDeviceToDevice));
     HIPCK(hipMemcpy(c->vk_inf.as<uint32_t>() + (q + 1), &c->gtilde_inf, 4, hipMemcpyHostToDevice));
+    HIPCK(hipMemcpy(c->vk_aff.as<uint32_t>() + (q + 2) * aw, c->vk_aff.p, aw * 4, hipMemcpyDeviceToDevice));
+    HIPCK(hipMemcpy(c->vk_inf.as<uint32_t>() + (q + 2), c->vk_inf.p, 4, hipMemcpyDeviceToDevice));
     HIPCK(hipMemcpy(&c->X_inf, c->vk_inf.p, 4, hipMemcpyDeviceToHost));
     c->q = q;
     c->have_vk = true;
@@ -310,9 +323,76 @@ cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d
     return CC_OK;
 }
 
+
+// ---------------------------------------------------------------- RLC batch mode (rlc.hip)
+static int fresh_seed(uint8_t seed[32]) {
+    FILE* f = fopen("/dev/urandom", "rb");
+    if (!f) return -1;
+    size_t got = fread(seed, 1, 32, f);
+    fclose(f);
+    return got == 32 ? 0 : -1;
+}
+
+cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_index, const uint8_t* seed32,
+                                const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs, uint32_t* d_partial,
+                                void* stream) {
+    if (!c || !seed32 || !d_partial || (n && (!d_s1 || !d_s2 || (q && !d_msgs)))) return CC_ERR_DECODE;
+    if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
+    if (q != c->q) return CC_ERR_LEN;
+    if (!n) return CC_ERR_DECODE;
+    HIPCK(hipSetDevice(c->device));
+    cc_status s = ensure_work(c, n);
+    if (s) return s;
+    if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4)) return CC_ERR_HIP;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    memcpy(c->rlc_key_host, seed32, 32);
+    HIPCK(hipMemcpyAsync(c->rlc_key.p, c->rlc_key_host, 32, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
+    if (c->timing) hipEventRecord(c->ev[0], st);
+    KCK(cck_prep_rlc(c->mode, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
+                     c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
+                     c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), st));
+    if (c->timing) hipEventRecord(c->ev[1], st);
+    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
+    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st, 1));
+    if (c->timing) hipEventRecord(c->ev[2], st);
+    KCK(cck_rlc_reduce(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,
+                       st));
+    if (c->timing) hipEventRecord(c->ev[3], st);
+    return CC_OK;
+}
+
+cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_partials, uint8_t* d_accept,
+                               uint8_t* d_gt, void* stream) {
+    if (!c || !nparts || !d_partials || !d_accept) return CC_ERR_DECODE;
+    HIPCK(hipSetDevice(c->device));
+    cc_status s = ensure_work(c, 1);
+    if (s) return s;
+    if (c->rlc_flag.ensure(4)) return CC_ERR_HIP;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    KCK(cck_rlc_combine(nparts, d_partials, c->fbuf.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), st));
+    // one final exponentiation; flags[0] bit0 (a sigma was the identity somewhere) forces a reject
+    KCK(cck_fexp(1, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), d_accept, d_gt, st));
+    return CC_OK;
+}
+
+// single-GPU RLC over host buffers: returns accept (1) / reject (0) in *accept
+static cc_status rlc_host(cc_ctx* c, size_t n, size_t q, uint8_t* accept) {
+    uint8_t seed[32];
+    if (fresh_seed(seed)) return CC_ERR_HIP;
+    if (c->rlc_part.ensure(145 * 4) || c->rlc_accept.ensure(1)) return CC_ERR_HIP;
+    cc_status s = cc_rlc_partial_device(c, n, q, 0, seed, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(),
+                                        c->in_msgs.as<uint8_t>(), c->rlc_part.as<uint32_t>(), c->stream);
+    if (s) return s;
+    s = cc_rlc_finish_device(c, 1, c->rlc_part.as<uint32_t>(), c->rlc_accept.as<uint8_t>(), nullptr, c->stream);
+    if (s) return s;
+    HIPCK(hipMemcpyAsync(accept, c->rlc_accept.p, 1, hipMemcpyDeviceToHost, c->stream));
+    HIPCK(hipStreamSynchronize(c->stream));
+    return CC_OK;
+}
+
 cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, const uint8_t* s2, const uint8_t* msgs,
                           const uint8_t* vkX, const uint8_t* vkY, uint8_t* verdicts, uint8_t* gt, int rlc) {
-    (void)rlc;  // RLC mode: see cc_verify_batch_rlc in rlc.cpp (per-credential here)
     if (!c || (n && (!s1 || !s2 || !verdicts || (q && !msgs)))) return CC_ERR_DECODE;
     if (!c->have_params) return CC_ERR_STATE;
     const bool per_vk = vkX != nullptr;
@@ -334,6 +414,17 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
     HIPCK(hipMemcpyAsync(c->in_s2.p, s2, n * sb, hipMemcpyHostToDevice, st));
     if (q) HIPCK(hipMemcpyAsync(c->in_msgs.p, msgs, n * q * 48, hipMemcpyHostToDevice, st));
     const uint8_t* d_msgs = c->in_msgs.as<uint8_t>();
+    if (rlc && !per_vk && !gt) {
+        // whole-batch check; on reject (a bad or identity credential somewhere) fall through to the
+        // per-credential path so every verdict equals the reference's
+        uint8_t accept = 0;
+        s = rlc_host(c, n, q, &accept);
+        if (s) return s;
+        if (accept) {
+            memset(verdicts, 1, n);
+            return CC_OK;
+        }
+    }
     if (per_vk) {
         int og = oth_group(c->mode);
         size_t fs = og == 1 ? 1 : 2;  // Fp slots per coordinate

@@ -246,14 +246,26 @@ DEV bool cc_opaque_false() {
     asm volatile("s_mov_b32 %0, 0" : "=s"(x));
     return x != 0;
 }
+// The operands pass through an empty volatile asm so their radix-2^29 conversions cannot be
+// common-subexpression-eliminated across multiplication sites (that keeps 14-limb copies of every
+// reused operand live and spills); the conversion is ~30 instructions against ~400 mads.
+DEV void fp_opaque(Fp& x) {
+#pragma unroll
+    for (int k = 0; k < NL; k++) asm volatile("" : "+v"(x.v[k]));
+}
 DEV void fp_mul(Fp& r, const Fp& a, const Fp& b) {
     do {
-        r = fp_mul_v(a, b);
+        Fp x = a, y = b;
+        fp_opaque(x);
+        fp_opaque(y);
+        r = fp_mul_v(x, y);
     } while (cc_opaque_false());
 }
 DEV void fp_sqr(Fp& r, const Fp& a) {
     do {
-        r = fp_sqr_v(a);
+        Fp x = a;
+        fp_opaque(x);
+        r = fp_sqr_v(x);
     } while (cc_opaque_false());
 }
 #else
@@ -501,30 +513,30 @@ DEV void f12_mul(Fp12& r, const Fp12& x, const Fp12& y) {
     r.c = rc;
 }
 
-// Chung-Hasan SQR2 over the cubic extension
+// Chung-Hasan SQR2 over the cubic extension:
+//   s0 = a^2, s1 = 2ab, s2 = (a - b + c)^2, s3 = 2bc, s4 = c^2
+//   r.a = s0 + s s3, r.b = s1 + s s4, r.c = s1 + s2 + s3 - s0 - s4
+// ordered so partial sums replace the s_k as soon as possible (r may alias x).
 DEV void f12_sqr(Fp12& r, const Fp12& x) {
-    Fp4 s0, s1, s2, s3, s4, t;
+    Fp4 t, s0, s1, acc, ra;
+    f4_sub(t, x.a, x.b);
+    f4_add(t, t, x.c);
+    f4_sqr(acc, t);       // s2
     f4_sqr(s0, x.a);
     f4_mul(s1, x.a, x.b);
     f4_dbl(s1, s1);
-    f4_sub(t, x.a, x.b);
-    f4_add(t, t, x.c);
-    f4_sqr(s2, t);
-    f4_mul(s3, x.b, x.c);
-    f4_dbl(s3, s3);
-    f4_sqr(s4, x.c);
-    Fp4 ra, rb, rc;
-    f4_mul_s(t, s3);
-    f4_add(ra, s0, t);
-    f4_mul_s(t, s4);
-    f4_add(rb, s1, t);
-    f4_add(rc, s1, s2);
-    f4_add(rc, rc, s3);
-    f4_sub(rc, rc, s0);
-    f4_sub(rc, rc, s4);
+    f4_add(acc, acc, s1);
+    f4_sub(acc, acc, s0); // s2 + s1 - s0
+    f4_mul(t, x.b, x.c);
+    f4_dbl(t, t);         // s3
+    f4_add(acc, acc, t);
+    f4_mul_s(ra, t);
+    f4_add(ra, ra, s0);   // r.a
+    f4_sqr(t, x.c);       // s4
+    f4_sub(r.c, acc, t);
+    f4_mul_s(t, t);
+    f4_add(r.b, s1, t);
     r.a = ra;
-    r.b = rb;
-    r.c = rc;
 }
 
 // Granger-Scott squaring for elements of the cyclotomic subgroup (AMCL FP12::usqr):

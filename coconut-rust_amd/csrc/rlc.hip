@@ -1,0 +1,259 @@
+// Random-linear-combination (RLC) batch verification for gfx950 (BASELINE config 3).
+//
+// Per credential i the reference checks e(sigma_1,i, pr_i) * e(-sigma_2,i, g~) == 1 (ps_sig
+// Signature::verify [EXT], reference src/signature.rs:473-478).  RLC checks the whole batch at once:
+//
+//     prod_i e(sigma_1,i, delta_i pr_i) * e(-sigma_2,i, delta_i g~) == 1        (SigG2)
+//     prod_i e(delta_i pr_i, sigma_1,i) * e(g~, -delta_i sigma_2,i) == 1        (SigG1)
+//
+// with independent 128-bit delta_i (ChaCha20 keyed by a fresh host seed): one Miller loop per
+// credential, the product of all Miller values, and ONE final exponentiation per batch (or, over
+// several GPUs, one per gathered set of per-GPU partial products).  A forged credential passes with
+// probability <= 2^-127.  If the batch fails, or any sigma is the identity (which the per-credential
+// semantics reject), the caller falls back to per-credential verification, so verdicts always equal
+// the reference's.
+//
+//   k_prep_rlc_sigg2 / k_prep_rlc_sigg1 : decode, delta, delta-scaled fixed-base MSM (delta X + sum
+//                                         (delta m_j) Y_j) and the delta-scaled second pair, written
+//                                         in the Miller kernels' SoA operand layout (soa.h)
+//   k_f12_reduce                        : one level of the pairwise product tree of Fp12 values
+//   k_rlc_partial_out / k_rlc_combine   : 145-word partial (Fp12 Montgomery words + identity flag),
+//                                         and the product of gathered partials ahead of k_fexp
+#include "codec.h"
+#include "fr.h"
+#include "pairing.h"
+#include "soa.h"
+
+using namespace cc;
+
+namespace {
+
+constexpr int NWIN = 32, WENT = 255;
+
+template <class F>
+DEV void ld_aff_words(Aff<F>& a, const uint32_t* p) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(&a);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(Aff<F>) / 4); k++) d[k] = p[k];
+}
+
+// acc += k * B_j through base j's 8-bit window table; k canonical (8 LE limbs), nwin windows
+template <class F>
+DEV void fixed_add(Jac<F>& acc, const uint32_t k[NR], const uint32_t* table, int j, int nwin) {
+    constexpr int EW = sizeof(Aff<F>) / 4;
+    const uint32_t* tj = table + (size_t)j * NWIN * WENT * EW;
+#pragma unroll 1
+    for (int w = 0; w < nwin; w++) {
+        const uint32_t d = (k[w >> 2] >> (8 * (w & 3))) & 0xffu;
+        if (d) {
+            Aff<F> e;
+            ld_aff_words<F>(e, tj + ((size_t)w * WENT + d - 1) * EW);
+            jac_add_aff(acc, acc, e);
+        }
+    }
+}
+
+// G1 Jacobian -> line-evaluation form (X Z, Y, Z^3) in three SoA slots
+DEV void st_eval(const Soa& S, int slot, size_t i, const Jac<Fp>& P) {
+    Fp t;
+    fp_mul(t, P.x, P.z);
+    st_fp(S, slot, i, t);
+    st_fp(S, slot + 1, i, P.y);
+    fp_sqr(t, P.z);
+    fp_mul(t, t, P.z);
+    st_fp(S, slot + 2, i, t);
+}
+
+}  // namespace
+
+// Tables: bases [Y~_0 .. Y~_{q-1}, g~, X~] (indices 0..q-1, q, q+1) of cc_set_verkey.
+// flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 delta pr = O, bit4 second pair degenerate.
+__global__ __launch_bounds__(256) void k_prep_rlc_sigg2(size_t n, int q, uint64_t base_index,
+                                                        const uint32_t* __restrict__ key,
+                                                        const uint8_t* __restrict__ s1b,
+                                                        const uint8_t* __restrict__ s2b,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint32_t* __restrict__ table,
+                                                        const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
+                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ any) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp2> a;
+        if (!g2_decode(a, s1b + i * 192)) fl |= 1u;
+        st_f2(S, S_Q1, i, a.x);
+        st_f2(S, S_Q1 + 2, i, a.y);
+        if (!g2_decode(a, s2b + i * 192)) fl |= 2u;
+        f2_neg(a.y, a.y);
+        st_f2(S, S_Q2, i, a.x);
+        st_f2(S, S_Q2 + 2, i, a.y);
+    }
+    uint32_t kk[NR];
+    for (int k = 0; k < 8; k++) kk[k] = key[k];
+    uint32_t d[NR];
+    rlc_delta(d, kk, base_index + i);
+    Jac<Fp> acc;
+    jac_set_inf(acc);
+    if (!binf[q + 1]) fixed_add<Fp>(acc, d, table, q + 1, 16);  // delta X~ (128-bit delta: 16 windows)
+    for (int j = 0; j < q; j++) {
+        if (binf[j]) continue;
+        Fr m;
+        fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
+        uint32_t dm[NR];
+        fr_mul_canon(dm, d, m.v);
+        fixed_add<Fp>(acc, dm, table, j, NWIN);
+    }
+    if (jac_is_inf(acc)) fl |= 4u;
+    st_eval(S, S_P1, i, acc);
+    jac_set_inf(acc);
+    if (!binf[q]) fixed_add<Fp>(acc, d, table, q, 16);  // delta g~
+    if (jac_is_inf(acc)) fl |= 16u;
+    st_eval(S, S_P2, i, acc);
+    flags[i] = fl;
+    if (fl & 3u) atomicOr(any, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_prep_rlc_sigg1(size_t n, int q, uint64_t base_index,
+                                                        const uint32_t* __restrict__ key,
+                                                        const uint8_t* __restrict__ s1b,
+                                                        const uint8_t* __restrict__ s2b,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint32_t* __restrict__ table,
+                                                        const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
+                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ any) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Soa S{prep, n};
+    uint32_t fl = 0;
+    uint32_t kk[NR];
+    for (int k = 0; k < 8; k++) kk[k] = key[k];
+    uint32_t d[NR];
+    rlc_delta(d, kk, base_index + i);
+    {
+        Aff<Fp> a;
+        if (!g1_decode(a, s1b + i * 97)) fl |= 1u;
+        st_fp(S, S_P1, i, a.x);
+        st_fp(S, S_P1 + 1, i, a.y);
+        // -delta sigma_2 (variable base, 128-bit double-and-add)
+        Jac<Fp> s;
+        jac_set_inf(s);
+        if (g1_decode(a, s2b + i * 97)) {
+            for (int b = 127; b >= 0; b--) {
+                jac_dbl(s, s);
+                if ((d[b >> 5] >> (b & 31)) & 1u) jac_add_aff(s, s, a);
+            }
+            fp_neg(s.y, s.y);
+        } else {
+            fl |= 2u;
+        }
+        if (jac_is_inf(s)) fl |= 16u;
+        st_eval(S, S_P2, i, s);
+    }
+    Jac<Fp2> acc;
+    jac_set_inf(acc);
+    if (!binf[q + 1]) fixed_add<Fp2>(acc, d, table, q + 1, 16);
+    for (int j = 0; j < q; j++) {
+        if (binf[j]) continue;
+        Fr m;
+        fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
+        uint32_t dm[NR];
+        fr_mul_canon(dm, d, m.v);
+        fixed_add<Fp2>(acc, dm, table, j, NWIN);
+    }
+    Aff<Fp2> a2;
+    if (!jac_to_aff(a2, acc)) fl |= 4u;
+    st_f2(S, S_Q1, i, a2.x);
+    st_f2(S, S_Q1 + 2, i, a2.y);
+    flags[i] = fl;
+    if (fl & 3u) atomicOr(any, 1u);
+}
+
+// out[t] = in[2t] * in[2t+1] (in[2t] alone for an odd tail); SoA strides n_in / n_out
+__global__ __launch_bounds__(256) void k_f12_reduce(size_t n_in, const uint32_t* __restrict__ in,
+                                                    uint32_t* __restrict__ out) {
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t n_out = (n_in + 1) / 2;
+    if (t >= n_out) return;
+    const Soa I{const_cast<uint32_t*>(in), n_in}, O{out, n_out};
+    Fp12 a;
+    ld_f12(a, I, 2 * t);
+    if (2 * t + 1 < n_in) {
+        Fp12 b;
+        ld_f12(b, I, 2 * t + 1);
+        f12_mul(a, a, b);
+    }
+    st_f12(O, t, a);
+}
+
+// 145-word partial: the batch's Miller product (one element, Montgomery words in slot order) and
+// the identity flag (any sigma = O in the batch)
+__global__ void k_rlc_partial_out(const uint32_t* __restrict__ f1, const uint32_t* __restrict__ any,
+                                  uint32_t* __restrict__ partial) {
+    const int t = threadIdx.x;
+    if (t < 144) partial[t] = f1[t];
+    if (t == 144) partial[t] = *any ? 1u : 0u;
+}
+
+// product of k gathered partials -> fbuf (n = 1) and flags[0] (bit0 set if any part is flagged)
+__global__ void k_rlc_combine(size_t k, const uint32_t* __restrict__ parts, uint32_t* __restrict__ f1,
+                              uint32_t* __restrict__ flag) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    Fp12 acc;
+    uint32_t* w = reinterpret_cast<uint32_t*>(&acc);
+    for (int j = 0; j < 144; j++) w[j] = parts[j];
+    uint32_t fl = parts[144];
+    for (size_t p = 1; p < k; p++) {
+        Fp12 x;
+        uint32_t* v = reinterpret_cast<uint32_t*>(&x);
+        for (int j = 0; j < 144; j++) v[j] = parts[p * 145 + j];
+        fl |= parts[p * 145 + 144];
+        f12_mul(acc, acc, x);
+    }
+    for (int j = 0; j < 144; j++) f1[j] = w[j];
+    *flag = fl ? 1u : 0u;
+}
+
+static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+extern "C" {
+
+int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
+                 const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, const uint32_t* d_binf,
+                 uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, hipStream_t st) {
+    if (!n) return 0;
+    dim3 g(nblocks(n, 256)), b(256);
+    if (mode == 0)
+        hipLaunchKernelGGL(k_prep_rlc_sigg2, g, b, 0, st, n, q, base_index, d_key, d_s1, d_s2, d_msgs, d_table,
+                           d_binf, d_prep, d_flags, d_any);
+    else
+        hipLaunchKernelGGL(k_prep_rlc_sigg1, g, b, 0, st, n, q, base_index, d_key, d_s1, d_s2, d_msgs, d_table,
+                           d_binf, d_prep, d_flags, d_any);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// reduce n SoA Fp12 values in `a` to one, ping-ponging with `b` (each >= n * 144 words);
+// writes the 145-word partial
+int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any, uint32_t* d_partial,
+                   hipStream_t st) {
+    if (!n) return -1;
+    uint32_t *src = d_a, *dst = d_b;
+    while (n > 1) {
+        const size_t n_out = (n + 1) / 2;
+        hipLaunchKernelGGL(k_f12_reduce, dim3(nblocks(n_out, 256)), dim3(256), 0, st, n, src, dst);
+        n = n_out;
+        uint32_t* t = src;
+        src = dst;
+        dst = t;
+    }
+    hipLaunchKernelGGL(k_rlc_partial_out, dim3(1), dim3(192), 0, st, src, d_any, d_partial);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t* d_flag, hipStream_t st) {
+    hipLaunchKernelGGL(k_rlc_combine, dim3(1), dim3(64), 0, st, k, d_parts, d_f1, d_flag);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // extern "C"

@@ -85,6 +85,25 @@ cc_status cc_verify_batch(cc_ctx* ctx, size_t n, size_t q, const uint8_t* sigma1
 cc_status cc_verify_batch_device(cc_ctx* ctx, size_t n, size_t q, const uint8_t* d_sigma1, const uint8_t* d_sigma2,
                                  const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt_or_null, void* stream);
 
+/* RLC batch mode, multi-GPU form.  Each GPU reduces its shard to one 145-word
+ * partial (Fp12 Miller product in the library's Montgomery words + an identity flag); the caller
+ * gathers the partials of all GPUs (RCCL all-gather over xGMI, or any transport) and every GPU
+ * finishes with ONE final exponentiation:
+ *   cc_rlc_partial_device: deltas = ChaCha20(seed32, base_index + i), i < n (shared verkey only);
+ *                          d_partial: 145 x u32 device buffer.
+ *   cc_rlc_finish_device : product of nparts partials (nparts x 145 u32, device), final
+ *                          exponentiation; *d_accept = 1 iff the whole batch verifies (then every
+ *                          per-credential verdict is 1); 0 means "fall back to per-credential
+ *                          verification" (a bad or identity credential somewhere).  d_gt optional
+ *                          (576 B, GT of the combined product).
+ * Both are asynchronous on `stream` (NULL: the context stream).  cc_verify_batch(..., rlc = 1)
+ * runs the single-GPU form with a fresh seed from /dev/urandom and falls back by itself. */
+cc_status cc_rlc_partial_device(cc_ctx* ctx, size_t n, size_t q, uint64_t base_index, const uint8_t* seed32,
+                                const uint8_t* d_sigma1, const uint8_t* d_sigma2, const uint8_t* d_msgs,
+                                uint32_t* d_partial, void* stream);
+cc_status cc_rlc_finish_device(cc_ctx* ctx, size_t nparts, const uint32_t* d_partials, uint8_t* d_accept,
+                               uint8_t* d_gt_or_null, void* stream);
+
 /* Batch Signature::aggregate: n independent aggregations of `len` (id, Signature) entries each;
  * only the first t entries are used, sigma_1 comes from entry 0, Lagrange over the de-duplicated
  * id set (signature.rs:448-470).  ids: n x len; sigma1/sigma2: n x len encodings;

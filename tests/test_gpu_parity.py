@@ -210,3 +210,79 @@ def test_full_size_batch_config2(ctxs):
     ctx.set_verkey(b["X"], b["Y"])
     v = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"])
     assert np.array_equal(v, b["expect"])
+
+
+# ---------------------------------------------------------------- RLC batch mode
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_rlc_batch_accepts_valid_and_falls_back_exactly(ctxs, mode):
+    """cc_verify_batch(rlc=1): an all-valid batch is accepted by one final exponentiation; a batch
+    with corrupted credentials falls back to per-credential verdicts, identical to the reference
+    semantics (verdicts known by construction)."""
+    from coconut import verify_batch
+    m = MODES[mode]
+    q, n = 6, 1024
+    b = _gen_batch(m, n, q, seed=31 + m, bad_every=n + 1)  # no corrupted credential
+    ctx = ctxs[mode]
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    v = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], rlc=True)
+    assert b["expect"].all() and np.array_equal(v, b["expect"])
+    b2 = _gen_batch(m, n, q, seed=41 + m, bad_every=97)
+    ctx.set_params(b2["g_tilde"])
+    ctx.set_verkey(b2["X"], b2["Y"])
+    v2 = verify_batch(ctx, n, q, b2["s1"], b2["s2"], b2["msgs"], rlc=True)
+    assert not b2["expect"].all() and np.array_equal(v2, b2["expect"])
+
+
+def test_rlc_golden_fixture_with_identity_and_offcurve(ctxs):
+    """The golden fixture mixes valid, corrupted, identity and off-curve credentials: RLC must reject
+    the batch as a whole and reproduce every per-credential verdict."""
+    from coconut import verify_batch
+    for name in ("verify_g2_q6.json", "verify_g1_q6.json"):
+        d = golden(name)
+        ctx = ctxs[d["mode"]]
+        cr = d["creds"]
+        ctx.set_params(bytes.fromhex(d["g_tilde"]))
+        ctx.set_verkey(bytes.fromhex(d["vk"]["X"]), [bytes.fromhex(y) for y in d["vk"]["Y"]])
+        v = verify_batch(ctx, len(cr), d["q"], _cat(c["sigma1"] for c in cr), _cat(c["sigma2"] for c in cr),
+                         _cat(m for c in cr for m in c["msgs"]), rlc=True)
+        assert list(v) == [c["verdict"] for c in cr], name
+        valid = [c for c in cr if c["verdict"] == 1]
+        v = verify_batch(ctx, len(valid), d["q"], _cat(c["sigma1"] for c in valid),
+                         _cat(c["sigma2"] for c in valid), _cat(m for c in valid for m in c["msgs"]), rlc=True)
+        assert v.all(), name
+
+
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_rlc_partials_gathered_across_shards(ctxs, mode):
+    """The multi-GPU form on one device: 4 shards -> 4 partials (independent seeds and base indices)
+    -> one finish.  Accepts the valid batch; one corrupted credential in one shard rejects it."""
+    import torch
+    from coconut.dist import DeviceEngine, shard_bounds
+    m = MODES[mode]
+    q, n, world = 6, 2048, 4
+    b = _gen_batch(m, n, q, seed=51 + m, bad_every=n + 1)
+    ctx = ctxs[mode]
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    sb = 192 if m == 0 else 97
+    dev = torch.device("cuda", 0)
+    s1 = torch.frombuffer(bytearray(b["s1"]), dtype=torch.uint8).to(dev)
+    s2 = torch.frombuffer(bytearray(b["s2"]), dtype=torch.uint8).to(dev)
+    ms = torch.frombuffer(bytearray(b["msgs"]), dtype=torch.uint8).to(dev)
+
+    def run(s2_dev):
+        parts = []
+        for r in range(world):
+            lo, hi = shard_bounds(n, world, r)
+            e = DeviceEngine(ctx, hi - lo, q, s1[lo * sb:hi * sb], s2_dev[lo * sb:hi * sb],
+                             ms[lo * q * 48:hi * q * 48], base_index=lo)
+            parts.append(e.partial().clone())
+        torch.cuda.synchronize()
+        return e.finish(torch.stack(parts), world)
+
+    assert run(s2)
+    bad = s2.clone()
+    i = 3 * n // 4 + 5  # inside shard 3: swap in another credential's sigma_2
+    bad[i * sb:(i + 1) * sb] = s2[(i + 1) * sb:(i + 2) * sb]
+    assert not run(bad)
