@@ -57,7 +57,7 @@ def fp_mults_per_credential(q=Q):
     return {"prep": prep, "miller": miller, "fexp": easy + hard}
 
 
-def make_batch(ctx, n, q, seed, bad_every=16):
+def make_batch(ctx, n, q, seed, bad_every=16):  # bad_every = 0: all valid
     """Synthetic credentials built on the GPU with the product's fixed-base multiplication."""
     import coconut
     rng = np.random.default_rng(seed)
@@ -76,7 +76,7 @@ def make_batch(ctx, n, q, seed, bad_every=16):
     for i in range(n):
         s = (x + sum(yj * mj for yj, mj in zip(y, m[i]))) % R_ORDER
         e = ks[i] * s % R_ORDER
-        if i % bad_every == bad_every - 1:
+        if bad_every and i % bad_every == bad_every - 1:
             e = (e + 1) % R_ORDER  # sigma_2 + G: must be rejected
             expect[i] = 0
         e1 += ks[i].to_bytes(48, "big")
@@ -116,15 +116,7 @@ def cpu_baseline(batch, q, threads, target_s=1.5):
             "cpu_seconds": dt * threads}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=N_PER_GPU, help="credentials per GPU per step")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
-
+def _dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -133,6 +125,93 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+    return world, rank, local, dist
+
+
+def bench_rlc(args):
+    """BASELINE config 3: batches of q = 16 credentials verified in RLC batch mode.  Each rank owns
+    131,072 credentials (2^20 over 8 GPUs); a step = per-rank partial (delta-weighted Miller product
+    of the slice) -> RCCL all-gather of the 580-byte partials -> one final exponentiation on every
+    rank -> accept.  All credentials are valid, so the accept path is what is timed; the reject
+    path (fallback) is checked once after the timed region."""
+    import coconut
+    from coconut.dist import DeviceEngine, gather_partials
+    world, rank, local, dist = _dist_setup()
+    n = args.n if args.n != N_PER_GPU else 131072
+    q = 16
+    ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
+    batch = make_batch(ctx, n, q, seed=3000 + rank, bad_every=0)
+    ctx.set_params(batch["g_tilde"])
+    ctx.set_verkey(batch["X"], batch["Y"])
+    dev = torch.device("cuda", local)
+    up = lambda x: torch.frombuffer(bytearray(x), dtype=torch.uint8).to(dev)  # noqa: E731
+    d_s1, d_s2, d_m = up(batch["s1"]), up(batch["s2"]), up(batch["msgs"])
+    eng = DeviceEngine(ctx, n, q, d_s1, d_s2, d_m, base_index=rank * n)
+
+    def step():
+        part = eng.partial()
+        allp, k = gather_partials(part)
+        return eng.finish(allp, k)
+
+    for _ in range(args.warmup):
+        assert step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ok = True
+    for _ in range(args.steps):
+        ok &= step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if not ok:
+        raise SystemExit("RLC rejected an all-valid batch — refusing to report a number")
+    # reject path: one credential of rank 0's slice corrupted -> every rank must reject
+    bad = d_s2.clone()
+    if rank == 0:
+        bad[:192] = d_s2[192:384]
+    eng_bad = DeviceEngine(ctx, n, q, d_s1, bad, d_m, base_index=rank * n)
+    pb, k = gather_partials(eng_bad.partial())
+    if eng_bad.finish(pb, k):
+        raise SystemExit("RLC accepted a corrupted batch — refusing to report a number")
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    value = n * world * args.steps / elapsed
+    if rank == 0:
+        print(json.dumps({
+            "metric": "verified credentials/sec, RLC batch mode (msg_count=16)",
+            "value": round(value, 1), "unit": "credentials/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 12x32-bit storage, integer-only)",
+            "data": "synthetic (seeded; all valid, reject path checked after timing)",
+            "config": {"workload": "config3: RLC batch verify, msg_count=16, shared verkey, SigG2",
+                       "credentials_per_gpu": n, "msg_count": q,
+                       "parallelism": f"shard-by-credential x{world} + RCCL all-gather of Fp12 partials"}}))
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=N_PER_GPU, help="credentials per GPU per step")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", choices=["verify", "rlc"], default="verify",
+                    help="verify: config 2 (per-credential verdicts, the headline metric); "
+                         "rlc: config 3 (RLC batch mode, q = 16, 131,072 per GPU, RCCL all-gather of partials)")
+    args = ap.parse_args()
+    if args.mode == "rlc":
+        return bench_rlc(args)
+
+    world, rank, local, dist = _dist_setup()
     device = local
     import coconut
 

@@ -4,7 +4,9 @@
 // CC_FP_INLINE: the multiplications are inlined inside each step function; the steps themselves are
 // out of line and exchange Fp12 values through a per-lane SoA scratch (one load/store per step,
 // against thousands of Fp multiplications per step), so each step's code exists once.
-// (CC_FP_INLINE: see field.h — off until the Fp12 code is register-lean enough to inline)
+#ifdef CC_HOT_INLINE  // build option (Makefile HOT_INLINE=1): inline every Fp multiplication
+#define CC_FP_INLINE 1
+#endif
 #include "codec.h"
 #include "pairing.h"
 #include "soa.h"

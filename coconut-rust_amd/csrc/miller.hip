@@ -18,7 +18,9 @@
 #ifndef CC_MILLER_SIG
 #define CC_MILLER_SIG 2
 #endif
-// (CC_FP_INLINE: see field.h — off until the Fp12 code is register-lean enough to inline)
+#ifdef CC_HOT_INLINE  // build option (Makefile HOT_INLINE=1): inline every Fp multiplication
+#define CC_FP_INLINE 1
+#endif
 #include "codec.h"
 #include "pairing.h"
 #include "soa.h"
