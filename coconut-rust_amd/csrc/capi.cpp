@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -24,7 +25,13 @@ int cck_miller_g2(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d
                   uint32_t* d_f, hipStream_t st);
 int cck_miller_g1(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                   uint32_t* d_f, hipStream_t st);
-int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
+int cck_miller_pl_g2(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
+                     uint32_t* d_f, hipStream_t st);
+int cck_miller_pl_g1(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
+                     uint32_t* d_f, hipStream_t st);
+int cck_fexp_pl(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
+                uint8_t* d_gt, hipStream_t st);
+int cck_fexp_lane(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
              uint8_t* d_gt, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
 int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
@@ -105,10 +112,27 @@ struct cc_ctx {
 
 // mode 0 (SigG2): d_const = g~ affine G1 (24 words); mode 1 (SigG1): g~ Miller lines (68 x 72 words).
 // lane2: pair 1's G1 point is per lane (prep slots S_P2.., Jacobian evaluation form; RLC mode).
+// Pairing kernels: pair-lane form (tower_pl.h, one credential per lane pair; default) or the
+// one-credential-per-lane form (CC_LANE_LAYOUT=lane, kept for A/B measurement).
+static bool pair_lanes() {
+    static const int v = [] {
+        const char* e = getenv("CC_LANE_LAYOUT");
+        return (e && !strcmp(e, "lane")) ? 0 : 1;
+    }();
+    return v != 0;
+}
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                       uint32_t* d_f, hipStream_t st, int lane2 = 0) {
+    if (pair_lanes())
+        return mode == 0 ? cck_miller_pl_g2(lane2, n, d_prep, d_flags, d_const, d_f, st)
+                         : cck_miller_pl_g1(lane2, n, d_prep, d_flags, d_const, d_f, st);
     return mode == 0 ? cck_miller_g2(lane2, n, d_prep, d_flags, d_const, d_f, st)
                      : cck_miller_g1(lane2, n, d_prep, d_flags, d_const, d_f, st);
+}
+static int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
+                    uint8_t* d_gt, hipStream_t st) {
+    return pair_lanes() ? cck_fexp_pl(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st)
+                        : cck_fexp_lane(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st);
 }
 
 static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }

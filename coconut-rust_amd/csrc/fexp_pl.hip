@@ -1,5 +1,6 @@
 // Final-exponentiation kernel for gfx950 (AMCL `pair::fexp` via amcl_wrapper `GT::ate_2_pairing`,
-// reference src/lib.rs:13) plus the RLC product reduction.
+// reference src/lib.rs:13), pair-lane form (tower_pl.h): one credential per
+// pair of adjacent lanes, each lane holding one half of every Fp2 value.
 //
 // CC_FP_INLINE: the multiplications are inlined inside each step function; the steps themselves are
 // out of line and exchange Fp12 values through a per-lane SoA scratch (one load/store per step,
@@ -8,10 +9,10 @@
 #define CC_FP_INLINE 1
 #endif
 #include "codec.h"
-#include "pairing.h"
-#include "soa.h"
+#include "tower_pl.h"
 
-using namespace cc;
+namespace cc {
+namespace pl {
 
 // ================================================================ final exponentiation
 // f^((p^6-1)(p^2+1)) then the hard part 3 + (x-1)^2 [p^3 + x p^2 + (x^2-1) p + x^3 - x]
@@ -68,11 +69,11 @@ static __device__ __noinline__ void fx_mul(Soa a, int opa, Soa b, int opb, Soa d
 }
 
 // fbuf: Miller output f (12 slots); scratch: 4 x 12 slots (T, A, S, R)
-__global__ __launch_bounds__(256) void k_fexp(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
+__global__ __launch_bounds__(256, 2) void k_fexp(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
                                               const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
                                               uint8_t* __restrict__ gt_out) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
+    if (i >= n) return;  // pair-uniform
     const Soa F{fbuf, n};
     const Soa T{scratch, n}, A{scratch + (size_t)12 * NL * n, n}, S{scratch + (size_t)24 * NL * n, n},
         R{scratch + (size_t)36 * NL * n, n};
@@ -97,24 +98,27 @@ __global__ __launch_bounds__(256) void k_fexp(size_t n, uint32_t* __restrict__ f
     ld_f12(res, R, i);
     const uint32_t fl = flags ? flags[i] : 0u;
     const bool ok = f12_is_one(res) && (fl & 11u) == 0;  // sigma_1/sigma_2 = O or PoK Schnorr failure
-    verdicts[i] = ok ? 1 : 0;
-    if (gt_out) {
-        const Fp* v = reinterpret_cast<const Fp*>(&res);
-        uint8_t* o = gt_out + i * 576;
-        for (int k = 0; k < 12; k++) {
+    if (!half_id()) verdicts[i] = ok ? 1 : 0;
+    if (gt_out) {  // each lane writes its halves: Fp slots 2k + h of the AMCL FP12 order
+        const Fp2* v = reinterpret_cast<const Fp2*>(&res);
+        uint8_t* o = gt_out + i * 576 + 48 * half_id();
+        for (int k = 0; k < 6; k++) {
             Fp c;
-            fp_from_mont(c, v[k]);
-            store_be48_aligned(o + 48 * k, c);
+            fp_from_mont(c, v[k].c);
+            store_be48_aligned(o + 96 * k, c);
         }
     }
 }
 
+}  // namespace pl
+}  // namespace cc
+
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
-extern "C" int cck_fexp_lane(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
+extern "C" int cck_fexp_pl(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                         uint8_t* d_gt, hipStream_t st) {
     if (!n) return 0;
-    hipLaunchKernelGGL(k_fexp, dim3(nblocks(n, 256)), dim3(256), 0, st, n, d_f, d_scratch, d_flags, d_verdicts,
+    hipLaunchKernelGGL(cc::pl::k_fexp, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, d_f, d_scratch, d_flags, d_verdicts,
                        d_gt);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -396,197 +396,12 @@ DEV void f2_inv(Fp2& r, const Fp2& x) {
     fp_neg(r.b, t);
 }
 
-// ============================== Fp4 = Fp2[s]/(s^2 - xi) ==============================
-struct Fp4 {
-    Fp2 a, b;  // a + b s
-};
-
-DEV void f4_zero(Fp4& r) { f2_zero(r.a); f2_zero(r.b); }
-DEV void f4_one(Fp4& r) { f2_one(r.a); f2_zero(r.b); }
-DEV void f4_add(Fp4& r, const Fp4& x, const Fp4& y) { f2_add(r.a, x.a, y.a); f2_add(r.b, x.b, y.b); }
-DEV void f4_sub(Fp4& r, const Fp4& x, const Fp4& y) { f2_sub(r.a, x.a, y.a); f2_sub(r.b, x.b, y.b); }
-DEV void f4_dbl(Fp4& r, const Fp4& x) { f2_dbl(r.a, x.a); f2_dbl(r.b, x.b); }
-DEV void f4_neg(Fp4& r, const Fp4& x) { f2_neg(r.a, x.a); f2_neg(r.b, x.b); }
-DEV void f4_conj(Fp4& r, const Fp4& x) { r.a = x.a; f2_neg(r.b, x.b); }  // a - b s
-
-DEV void f4_mul(Fp4& r, const Fp4& x, const Fp4& y) {
-    Fp2 t0, t1, s0, s1;
-    f2_mul(t0, x.a, y.a);
-    f2_mul(t1, x.b, y.b);
-    f2_add(s0, x.a, x.b);
-    f2_add(s1, y.a, y.b);
-    f2_mul(s0, s0, s1);
-    f2_sub(s0, s0, t0);
-    f2_sub(r.b, s0, t1);
-    f2_mul_xi(t1, t1);
-    f2_add(r.a, t0, t1);
-}
-
-// (a + b s)^2 = (a^2 + xi b^2) + 2ab s
-DEV void f4_sqr(Fp4& r, const Fp4& x) {
-    Fp2 ab, s0, s1;
-    f2_mul(ab, x.a, x.b);
-    f2_add(s0, x.a, x.b);
-    f2_mul_xi(s1, x.b);
-    f2_add(s1, s1, x.a);
-    f2_mul(s0, s0, s1);  // (a + b)(a + xi b) = a^2 + xi b^2 + ab (1 + xi)
-    f2_sub(s0, s0, ab);
-    f2_mul_xi(s1, ab);
-    f2_sub(r.a, s0, s1);
-    f2_dbl(r.b, ab);
-}
-
-// x * s = xi b + a s
-DEV void f4_mul_s(Fp4& r, const Fp4& x) {
-    Fp2 t;
-    f2_mul_xi(t, x.b);
-    r.b = x.a;
-    r.a = t;
-}
-
-// x * (c, 0) with c in Fp2
-DEV void f4_mul_f2(Fp4& r, const Fp4& x, const Fp2& c) {
-    f2_mul(r.a, x.a, c);
-    f2_mul(r.b, x.b, c);
-}
-
-DEV void f4_inv(Fp4& r, const Fp4& x) {
-    Fp2 n, t;
-    f2_sqr(n, x.a);
-    f2_sqr(t, x.b);
-    f2_mul_xi(t, t);
-    f2_sub(n, n, t);  // a^2 - xi b^2
-    f2_inv(n, n);
-    f2_mul(r.a, x.a, n);
-    f2_mul(t, x.b, n);
-    f2_neg(r.b, t);
-}
-
-// ============================== Fp12 = Fp4[w]/(w^3 - s) ==============================
-struct Fp12 {
-    Fp4 a, b, c;  // a + b w + c w^2
-};
-
-DEV void f12_one(Fp12& r) { f4_one(r.a); f4_zero(r.b); f4_zero(r.c); }
+#include "tower.inc"
 
 DEV bool f12_is_one(const Fp12& x) {
     return fp_is_one(x.a.a.a) && fp_is_zero(x.a.a.b) && f2_is_zero(x.a.b) && f2_is_zero(x.b.a) &&
            f2_is_zero(x.b.b) && f2_is_zero(x.c.a) && f2_is_zero(x.c.b);
 }
 
-// conj = x^(p^6): w -> -w, s -> -s
-DEV void f12_conj(Fp12& r, const Fp12& x) {
-    f4_conj(r.a, x.a);
-    Fp4 t;
-    f4_conj(t, x.b);
-    f4_neg(r.b, t);
-    f4_conj(r.c, x.c);
-}
-
-DEV void f12_mul(Fp12& r, const Fp12& x, const Fp12& y) {
-    Fp4 t0, t1, t2, s, u, ra, rb, rc;
-    f4_mul(t0, x.a, y.a);
-    f4_mul(t1, x.b, y.b);
-    f4_mul(t2, x.c, y.c);
-    f4_add(s, x.b, x.c);
-    f4_add(u, y.b, y.c);
-    f4_mul(s, s, u);
-    f4_sub(s, s, t1);
-    f4_sub(s, s, t2);
-    f4_mul_s(s, s);
-    f4_add(ra, s, t0);
-    f4_add(s, x.a, x.b);
-    f4_add(u, y.a, y.b);
-    f4_mul(s, s, u);
-    f4_sub(s, s, t0);
-    f4_sub(s, s, t1);
-    f4_mul_s(u, t2);
-    f4_add(rb, s, u);
-    f4_add(s, x.a, x.c);
-    f4_add(u, y.a, y.c);
-    f4_mul(s, s, u);
-    f4_sub(s, s, t0);
-    f4_sub(s, s, t2);
-    f4_add(rc, s, t1);
-    r.a = ra;
-    r.b = rb;
-    r.c = rc;
-}
-
-// Chung-Hasan SQR2 over the cubic extension:
-//   s0 = a^2, s1 = 2ab, s2 = (a - b + c)^2, s3 = 2bc, s4 = c^2
-//   r.a = s0 + s s3, r.b = s1 + s s4, r.c = s1 + s2 + s3 - s0 - s4
-// ordered so partial sums replace the s_k as soon as possible (r may alias x).
-DEV void f12_sqr(Fp12& r, const Fp12& x) {
-    Fp4 t, s0, s1, acc, ra;
-    f4_sub(t, x.a, x.b);
-    f4_add(t, t, x.c);
-    f4_sqr(acc, t);       // s2
-    f4_sqr(s0, x.a);
-    f4_mul(s1, x.a, x.b);
-    f4_dbl(s1, s1);
-    f4_add(acc, acc, s1);
-    f4_sub(acc, acc, s0); // s2 + s1 - s0
-    f4_mul(t, x.b, x.c);
-    f4_dbl(t, t);         // s3
-    f4_add(acc, acc, t);
-    f4_mul_s(ra, t);
-    f4_add(ra, ra, s0);   // r.a
-    f4_sqr(t, x.c);       // s4
-    f4_sub(r.c, acc, t);
-    f4_mul_s(t, t);
-    f4_add(r.b, s1, t);
-    r.a = ra;
-}
-
-// Granger-Scott squaring for elements of the cyclotomic subgroup (AMCL FP12::usqr):
-// a' = 3a^2 - 2 conj(a), b' = 3 s c^2 + 2 conj(b), c' = 3 b^2 - 2 conj(c)
-DEV void f12_cyc_sqr(Fp12& r, const Fp12& x) {
-    Fp4 A, B, C, t;
-    f4_sqr(A, x.a);
-    f4_sqr(B, x.c);
-    f4_mul_s(B, B);
-    f4_sqr(C, x.b);
-    // a'
-    f4_conj(t, x.a);
-    f4_sub(t, A, t);
-    f4_dbl(t, t);
-    f4_add(r.a, t, A);
-    // b'
-    f4_conj(t, x.b);
-    f4_add(t, B, t);
-    f4_dbl(t, t);
-    f4_add(r.b, t, B);
-    // c'
-    f4_conj(t, x.c);
-    f4_sub(t, C, t);
-    f4_dbl(t, t);
-    f4_add(r.c, t, C);
-}
-
-DEV void f12_inv(Fp12& r, const Fp12& x) {
-    Fp4 A, B, C, F, t;
-    f4_sqr(A, x.a);
-    f4_mul(t, x.b, x.c);
-    f4_mul_s(t, t);
-    f4_sub(A, A, t);  // a^2 - s bc
-    f4_sqr(B, x.c);
-    f4_mul_s(B, B);
-    f4_mul(t, x.a, x.b);
-    f4_sub(B, B, t);  // s c^2 - ab
-    f4_sqr(C, x.b);
-    f4_mul(t, x.a, x.c);
-    f4_sub(C, C, t);  // b^2 - ac
-    f4_mul(F, x.c, B);
-    f4_mul(t, x.b, C);
-    f4_add(F, F, t);
-    f4_mul_s(F, F);
-    f4_mul(t, x.a, A);
-    f4_add(F, F, t);
-    f4_inv(F, F);
-    f4_mul(r.a, A, F);
-    f4_mul(r.b, B, F);
-    f4_mul(r.c, C, F);
-}
 
 }  // namespace cc

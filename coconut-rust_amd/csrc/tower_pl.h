@@ -1,0 +1,199 @@
+// Pair-lane BLS12-381 tower for gfx950 — device code (the product path).
+//
+// Same field tower and pairing algorithms as field.h / pairing.h (AMCL's Fp2 -> Fp4 -> Fp12, which
+// the reference reaches through amcl_wrapper 0.1.7), with ONE credential
+// per PAIR of adjacent lanes: lane 2i holds the real half (a) of every Fp2 value, lane 2i+1 the
+// imaginary half (b).  Why: one credential per lane needs ~600 live words in the Miller loop, so a
+// 65,536-credential batch runs as 1,024 waves at one wave per SIMD with heavy scratch spills, and a
+// lone wave issues VALU at half rate on gfx950 (profiles/r01_ubench_int.jsonl).  Splitting every
+// Fp2 across a lane pair halves the per-lane state and doubles the wave count (2,048 waves, two per
+// SIMD), while the multiplication count per credential stays the same:
+//
+//   Fp2 mul  (a + b i)(c + d i):  lane a computes a c + b (p - d), lane b computes a d + b c — each
+//            a SUM of two 381-bit products with ONE Montgomery reduction (fp_mul2): 3 x 196 mads
+//            per lane vs 3 full multiplications (6 x 196) for Karatsuba on one lane.
+//   Fp2 sqr: lane a (a + b)(a - b), lane b a (2b): one multiplication per lane.
+//   Fp2 x Fp: one multiplication per lane.
+//
+// The partner's half is fetched with DPP quad_perm [1,0,3,2] (one v_mov_b32_dpp per word, no LDS).
+// Every control-flow decision in code using this file must be uniform across a lane pair.
+#pragma once
+#include "pairing.h"
+#include "soa.h"
+
+namespace cc {
+namespace pl {
+
+// partner lane's word (lane ^ 1) via DPP quad_perm [1, 0, 3, 2]
+DEV uint32_t swp(uint32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true); }
+DEV Fp swp(const Fp& x) {
+    Fp r;
+#pragma unroll
+    for (int k = 0; k < NL; k++) r.v[k] = swp(x.v[k]);
+    return r;
+}
+// 1 on the lane holding imaginary halves
+DEV uint32_t half_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 1u; }
+DEV Fp fp_sel(bool c, const Fp& x, const Fp& y) {
+    Fp r;
+#pragma unroll
+    for (int k = 0; k < NL; k++) r.v[k] = c ? x.v[k] : y.v[k];
+    return r;
+}
+
+// (u1 v1 + u2 v2) * 2^-406 mod p, canonical; u, v < 2^384 with u1 v1 + u2 v2 < 2p^2.
+// Column sums: 28 products + 14 reduction products of < 2^58, plus the carry, < 2^64.
+DEV Fp fp_mul2_v(const Fp& U1, const Fp& V1, const Fp& U2, const Fp& V2) {
+    uint32_t a[L29], b[L29], c[L29], d[L29], m[L29], r[L29];
+    to29(a, U1);
+    to29(b, V1);
+    to29(c, U2);
+    to29(d, V2);
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * L29 - 1; k++) {
+        uint64_t acc2 = 0;  // second product in its own chain (ILP)
+#pragma unroll
+        for (int i = 0; i < L29; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= L29) continue;
+            acc = mad64(a[i], b[j], acc);
+            acc2 = mad64(c[i], d[j], acc2);
+        }
+        acc += acc2;
+        redc_column(k, acc, m, r);
+    }
+    r[L29 - 1] = (uint32_t)acc;
+    Fp o;
+    from29(o, r);
+    return o;
+}
+
+// own half of x * y (x, y: own halves of two Fp2 values)
+DEV Fp f2_mul_half(const Fp& x, const Fp& y) {
+    const bool im = half_id() != 0;
+    const Fp xs = swp(x), ys = swp(y);
+    Fp nys;
+    fp_neg(nys, ys);
+    // re: a c + b (-d) = x y + xs (-ys);   im: b c + a d = x ys + xs y
+    return fp_mul2_v(x, im ? ys : y, xs, im ? y : nys);
+}
+// own half of x^2: re (a + b)(a - b), im a (2b)
+DEV Fp f2_sqr_half(const Fp& x) {
+    const bool im = half_id() != 0;
+    const Fp xs = swp(x);
+    Fp s, d;
+    fp_add(s, x, xs);
+    fp_sub(d, x, xs);
+    Fp u = fp_sel(im, xs, s), v;
+    fp_dbl(v, x);
+    v = fp_sel(im, v, d);
+    return fp_mul_v(u, v);
+}
+
+#ifdef CC_FP_INLINE
+DEV Fp f2_mul_call_(const Fp& x, const Fp& y) { return f2_mul_half(x, y); }
+DEV Fp f2_sqr_call_(const Fp& x) { return f2_sqr_half(x); }
+#else
+static __device__ __noinline__ Fp f2_mul_call(CC_L12(a), CC_L12(b)) {
+    const Fp A = {{CC_V12(a)}}, B = {{CC_V12(b)}};
+    return f2_mul_half(A, B);
+}
+static __device__ __noinline__ Fp f2_sqr_call(CC_L12(a)) {
+    const Fp A = {{CC_V12(a)}};
+    return f2_sqr_half(A);
+}
+DEV Fp f2_mul_call_(const Fp& x, const Fp& y) { return f2_mul_call(CC_E12(x), CC_E12(y)); }
+DEV Fp f2_sqr_call_(const Fp& x) { return f2_sqr_call(CC_E12(x)); }
+#endif
+
+// ============================== Fp2 (pair-lane) ==============================
+struct Fp2 {
+    Fp c;  // this lane's half: real part on even lanes, imaginary part on odd lanes
+};
+
+DEV void f2_zero(Fp2& r) { fp_zero(r.c); }
+DEV void f2_one(Fp2& r) {
+    Fp o, z;
+    fp_one(o);
+    fp_zero(z);
+    r.c = fp_sel(half_id() != 0, z, o);
+}
+// pair-uniform predicates: both halves agree
+DEV bool pair_all(bool own) { return (swp((uint32_t)own) & (uint32_t)own) != 0; }
+DEV bool f2_is_zero(const Fp2& x) { return pair_all(fp_is_zero(x.c)); }
+DEV bool f2_eq(const Fp2& x, const Fp2& y) { return pair_all(fp_eq(x.c, y.c)); }
+DEV void f2_add(Fp2& r, const Fp2& x, const Fp2& y) { fp_add(r.c, x.c, y.c); }
+DEV void f2_sub(Fp2& r, const Fp2& x, const Fp2& y) { fp_sub(r.c, x.c, y.c); }
+DEV void f2_dbl(Fp2& r, const Fp2& x) { fp_dbl(r.c, x.c); }
+DEV void f2_neg(Fp2& r, const Fp2& x) { fp_neg(r.c, x.c); }
+DEV void f2_conj(Fp2& r, const Fp2& x) {
+    Fp n;
+    fp_neg(n, x.c);
+    r.c = fp_sel(half_id() != 0, n, x.c);
+}
+DEV void f2_mul(Fp2& r, const Fp2& x, const Fp2& y) { r.c = f2_mul_call_(x.c, y.c); }
+DEV void f2_sqr(Fp2& r, const Fp2& x) { r.c = f2_sqr_call_(x.c); }
+DEV void f2_mul_fp(Fp2& r, const Fp2& x, const Fp& k) { fp_mul(r.c, x.c, k); }
+// x * (1 + i) = (a - b) + (a + b) i
+DEV void f2_mul_xi(Fp2& r, const Fp2& x) {
+    const Fp xs = swp(x.c);
+    Fp s, d;
+    fp_add(s, x.c, xs);
+    fp_sub(d, x.c, xs);
+    r.c = fp_sel(half_id() != 0, s, d);
+}
+// (a + b i)^-1 = (a - b i) / (a^2 + b^2); the norm and its inverse are computed on both lanes
+DEV void f2_inv(Fp2& r, const Fp2& x) {
+    const Fp xs = swp(x.c);
+    Fp n = fp_mul2_v(x.c, x.c, xs, xs);
+    fp_inv(n, n);
+    Fp2 t;
+    fp_mul(t.c, x.c, n);
+    f2_conj(r, t);
+}
+DEV void f2_half(Fp2& r, const Fp2& a) { fp_half(r.c, a.c); }
+DEV void load_f2c(Fp2& r, const F2c& c) {
+    const bool im = half_id() != 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.c.v[j] = im ? c.b[j] : c.a[j];
+}
+
+#include "tower.inc"
+
+DEV bool f12_is_one(const Fp12& x) {
+    Fp one;
+    fp_one(one);
+    const bool im = half_id() != 0;
+    // real halves: (1, 0, 0, 0, 0, 0); imaginary halves: all 0
+    bool ok = im ? fp_is_zero(x.a.a.c) : fp_eq(x.a.a.c, one);
+    ok = ok && fp_is_zero(x.a.b.c) && fp_is_zero(x.b.a.c) && fp_is_zero(x.b.b.c) && fp_is_zero(x.c.a.c) &&
+         fp_is_zero(x.c.b.c);
+    return pair_all(ok);
+}
+
+#include "pairing.inc"
+
+// ---------------------------------------------------------------- SoA access (soa.h layout):
+// an Fp2 occupies slots (slot, slot + 1) = (a, b); each lane moves its own half.
+DEV void ld_f2(Fp2& x, const Soa& s, int slot, size_t i) { ld_fp(x.c, s, slot + (int)half_id(), i); }
+DEV void st_f2(const Soa& s, int slot, size_t i, const Fp2& x) { st_fp(s, slot + (int)half_id(), i, x.c); }
+DEV void ld_f12(Fp12& x, const Soa& s, size_t i) {
+    Fp2* v = reinterpret_cast<Fp2*>(&x);
+#pragma unroll
+    for (int k = 0; k < 6; k++) ld_f2(v[k], s, 2 * k, i);
+}
+DEV void st_f12(const Soa& s, size_t i, const Fp12& x) {
+    const Fp2* v = reinterpret_cast<const Fp2*>(&x);
+#pragma unroll
+    for (int k = 0; k < 6; k++) st_f2(s, 2 * k, i, v[k]);
+}
+// AoS Fp2 (a then b, 12 words each)
+DEV void ld_f2_aos(Fp2& x, const uint32_t* p) {
+    const uint32_t* q = p + NL * half_id();
+#pragma unroll
+    for (int k = 0; k < NL; k++) x.c.v[k] = q[k];
+}
+
+}  // namespace pl
+}  // namespace cc
