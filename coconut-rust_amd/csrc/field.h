@@ -131,19 +131,12 @@ DEV uint32_t p29(int j) {
     return Q[j];
 }
 
-// c + a*b as one v_mad_u64_u32 (carry-out into VCC, unused).  Inline asm keeps the long mad
-// chains opaque to the IR combiners, which otherwise take minutes per kernel on them.
-DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
-    uint64_t r;
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c) : "vcc");
-    return r;
-}
-// same with a wave-uniform multiplier (a limb of p) in an SGPR
-DEV uint64_t mad64s(uint32_t a, uint32_t b, uint64_t c) {
-    uint64_t r;
-    asm("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c) : "vcc");
-    return r;
-}
+// c + a*b: one v_mad_u64_u32.  Written in plain C, not inline asm: the hazard recognizer cannot see
+// into an asm block and pads every asm mad with an s_nop (measured: ~1 nop per mad); the compiler's
+// own v_mad_u64_u32 (dead SGPR carry-out) chains back to back.
+DEV uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) { return c + (uint64_t)a * b; }
+// same with a wave-uniform multiplier (a limb of p, an SGPR operand)
+DEV uint64_t mad64s(uint32_t a, uint32_t b, uint64_t c) { return c + (uint64_t)a * b; }
 
 // 12 x 32 -> 14 x 29 (value < 2^384)
 DEV void to29(uint32_t o[L29], const Fp& x) {
