@@ -98,25 +98,35 @@ DEV void fp_reduce_once(Fp& r, const uint32_t t[NL]) {
     for (int j = 0; j < NL; j++) r.v[j] = br ? t[j] : s[j];
 }
 
+// Carry chains: gfx950 needs wait states between a VALU carry-out and the next carry-in of the same
+// chain (the compiler pads them with s_nop), so each add/sub below runs two or three independent
+// chains interleaved limb by limb.
 DEV void fp_add(Fp& r, const Fp& a, const Fp& b) {
-    uint32_t t[NL];
-    uint32_t c = 0;
+    uint32_t t[NL], s[NL];
+    uint32_t c = 0, br = 0;
 #pragma unroll
-    for (int j = 0; j < NL; j++) t[j] = __builtin_addc(a.v[j], b.v[j], c, &c);
-    fp_reduce_once(r, t);  // a + b < 2p < 2^384: no carry out
+    for (int j = 0; j < NL; j++) {
+        t[j] = __builtin_addc(a.v[j], b.v[j], c, &c);  // a + b < 2p < 2^384: no carry out
+        s[j] = __builtin_subc(t[j], p_limb(j), br, &br);
+    }
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.v[j] = br ? t[j] : s[j];
 }
 
 DEV void fp_dbl(Fp& r, const Fp& a) { fp_add(r, a, a); }
 
+// a - b, or a + (p - b) when a < b
 DEV void fp_sub(Fp& r, const Fp& a, const Fp& b) {
-    uint32_t t[NL];
-    uint32_t br = 0;
+    uint32_t t[NL], u[NL];
+    uint32_t b1 = 0, b2 = 0, c3 = 0;
 #pragma unroll
-    for (int j = 0; j < NL; j++) t[j] = __builtin_subc(a.v[j], b.v[j], br, &br);
-    uint32_t mask = 0u - br;
-    uint32_t c = 0;
+    for (int j = 0; j < NL; j++) {
+        t[j] = __builtin_subc(a.v[j], b.v[j], b1, &b1);
+        const uint32_t w = __builtin_subc(p_limb(j), b.v[j], b2, &b2);
+        u[j] = __builtin_addc(a.v[j], w, c3, &c3);
+    }
 #pragma unroll
-    for (int j = 0; j < NL; j++) r.v[j] = __builtin_addc(t[j], p_limb(j) & mask, c, &c);
+    for (int j = 0; j < NL; j++) r.v[j] = b1 ? u[j] : t[j];
 }
 
 DEV void fp_neg(Fp& r, const Fp& a) {
