@@ -49,12 +49,22 @@ static __device__ __noinline__ void fx_cube(Soa src, Soa dst, size_t i) {
     st_f12(dst, i, r);
 }
 
-// dst <- src^x, x = -|x| (cyclotomic square-and-multiply, then conj)
+// dst <- src^x, x = -|x| (cyclotomic square-and-multiply, then conj).  The base is re-read from src at
+// each of the 5 multiplications instead of being held in registers across the 63 squarings.
 static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, size_t i) {
-    Fp12 y, r;
-    ld_f12(y, src, i);
-    cyc_pow_x(r, y);
-    st_f12(dst, i, r);
+    Fp12 acc;
+    ld_f12(acc, src, i);
+    for (int b = 62; b >= 0; b--) {
+        f12_cyc_sqr(acc, acc);
+        if ((X_ABS >> b) & 1ull) {
+            asm volatile("" ::: "memory");  // keep the reload inside the loop
+            Fp12 y;
+            ld_f12(y, src, i);
+            f12_mul(acc, acc, y);
+        }
+    }
+    f12_conj(acc, acc);
+    st_f12(dst, i, acc);
 }
 
 // dst <- op_a(a) * op_b(b)

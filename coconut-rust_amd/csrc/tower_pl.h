@@ -9,7 +9,7 @@
 // Fp2 across a lane pair halves the per-lane state and doubles the wave count (2,048 waves, two per
 // SIMD), while the multiplication count per credential stays the same:
 //
-//   Fp2 mul  (a + b i)(c + d i):  lane a computes a c + b (p - d), lane b computes a d + b c — each
+//   Fp2 mul  (a + b i)(c + d i):  lane a computes a c + b (2p - d), lane b computes a d + b c — each
 //            a SUM of two 381-bit products with ONE Montgomery reduction (fp_mul2): 3 x 196 mads
 //            per lane vs 3 full multiplications (6 x 196) for Karatsuba on one lane.
 //   Fp2 sqr: lane a (a + b)(a - b), lane b a (2b): one multiplication per lane.
@@ -41,18 +41,15 @@ DEV Fp fp_sel(bool c, const Fp& x, const Fp& y) {
     return r;
 }
 
-// (u1 v1 + u2 v2) * 2^-406 mod p, canonical; u, v < 2^384 with u1 v1 + u2 v2 < 2p^2.
-// Column sums: 28 products + 14 reduction products of < 2^58, plus the carry, < 2^64.
-DEV Fp fp_mul2_v(const Fp& U1, const Fp& V1, const Fp& U2, const Fp& V2) {
-    uint32_t a[L29], b[L29], c[L29], d[L29], m[L29], r[L29];
-    to29(a, U1);
-    to29(b, V1);
-    to29(c, U2);
-    to29(d, V2);
+// (a b + c d) * 2^-406 mod p, canonical, on radix-2^29 limbs: a, c < 2^29 per limb, b, d < 2^30 per
+// limb, a b + c d < 3p^2.  Column sums: 14 products < 2^58 + 14 < 2^59 + 14 reduction products < 2^58
+// + the carry < 56 * 2^58 < 2^64.  The second product runs in its own accumulator chain (ILP).
+DEV Fp mul2_29(const uint32_t a[L29], const uint32_t b[L29], const uint32_t c[L29], const uint32_t d[L29]) {
+    uint32_t m[L29], r[L29];
     uint64_t acc = 0;
 #pragma unroll
     for (int k = 0; k < 2 * L29 - 1; k++) {
-        uint64_t acc2 = 0;  // second product in its own chain (ILP)
+        uint64_t acc2 = 0;
 #pragma unroll
         for (int i = 0; i < L29; i++) {
             const int j = k - i;
@@ -69,14 +66,38 @@ DEV Fp fp_mul2_v(const Fp& U1, const Fp& V1, const Fp& U2, const Fp& V2) {
     return o;
 }
 
-// own half of x * y (x, y: own halves of two Fp2 values)
+DEV Fp fp_mul2_v(const Fp& U1, const Fp& V1, const Fp& U2, const Fp& V2) {
+    uint32_t a[L29], b[L29], c[L29], d[L29];
+    to29(a, U1);
+    to29(b, V1);
+    to29(c, U2);
+    to29(d, V2);
+    return mul2_29(a, b, c, d);
+}
+
+// 2p in radix 2^29 with every limb in [2^29 - 1, 2^30): 2p - y limb by limb needs no borrows
+DEV uint32_t two_p29(int k) {
+    constexpr uint32_t D[L29] = {0x3fff5556u, 0x3feffffeu, 0x29ffffdbu, 0x2ffffac4u, 0x3ec483d4u, 0x32a0f6afu, 0x35fb3985u,
+                                 0x213ce143u, 0x2ec8ee96u, 0x2434baccu, 0x258dd3dau, 0x25ff9a68u, 0x20223d46u, 0x00000019u};
+    return D[k];
+}
+
+// own half of x * y (x, y: own halves of two Fp2 values).  The operands are converted to radix 2^29
+// once and the partner's converted limbs fetched by DPP.
+//   re: a c + b (2p - d) = x y + xs (2p - ys);   im: b c + a d = x ys + xs y
 DEV Fp f2_mul_half(const Fp& x, const Fp& y) {
     const bool im = half_id() != 0;
-    const Fp xs = swp(x), ys = swp(y);
-    Fp nys;
-    fp_neg(nys, ys);
-    // re: a c + b (-d) = x y + xs (-ys);   im: b c + a d = x ys + xs y
-    return fp_mul2_v(x, im ? ys : y, xs, im ? y : nys);
+    uint32_t a[L29], y29[L29], b[L29], c[L29], d[L29];
+    to29(a, x);
+    to29(y29, y);
+#pragma unroll
+    for (int k = 0; k < L29; k++) {
+        c[k] = swp(a[k]);
+        const uint32_t ys = swp(y29[k]);
+        b[k] = im ? ys : y29[k];
+        d[k] = im ? y29[k] : two_p29(k) - ys;
+    }
+    return mul2_29(a, b, c, d);
 }
 // own half of x^2: re (a + b)(a - b), im a (2b)
 DEV Fp f2_sqr_half(const Fp& x) {
