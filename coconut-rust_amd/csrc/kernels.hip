@@ -15,6 +15,7 @@
 #include "codec.h"
 #include "pairing.h"
 #include "soa.h"
+#include "tower_pl.h"  // pl::swp (lane-pair exchange)
 
 using namespace cc;
 
@@ -158,6 +159,36 @@ DEV void msm_fixed(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t* __re
     }
 }
 
+// fixed-base over windows [w0, w1) only, X~ included on request (the lane-pair split of msm_fixed)
+template <class F>
+DEV void msm_fixed_part(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                        bool with_x, const uint32_t* __restrict__ table, const uint32_t* __restrict__ binf, int w0,
+                        int w1) {
+    constexpr int EW = sizeof(Aff<F>) / 4;
+    if (!with_x || Xinf) {
+        jac_set_inf(acc);
+    } else {
+        Aff<F> x;
+        ld_aff_aos<F>(x, Xaff);
+        jac_from_aff(acc, x);
+    }
+    for (int j = 0; j < q; j++) {
+        if (binf[j]) continue;  // uniform across the batch (shared verkey)
+        Fr m;
+        fr_from_be48(m, msgs + (size_t)j * 48);
+        const uint32_t* tj = table + (size_t)j * NWIN * WENT * EW;
+#pragma unroll 1
+        for (int w = w0; w < w1; w++) {
+            uint32_t dgt = (m.v[w >> 2] >> (8 * (w & 3))) & 0xffu;
+            if (dgt) {
+                Aff<F> e;
+                ld_aff_aos<F>(e, tj + ((size_t)w * WENT + dgt - 1) * EW);
+                jac_add_aff(acc, acc, e);
+            }
+        }
+    }
+}
+
 // variable-base (per-credential verkey): interleaved double-and-add over the q+1 bases.
 // bases: SoA scratch of decoded affine points, slots [j][coord] ; binf per (j, i)
 template <class F>
@@ -264,6 +295,58 @@ __global__ __launch_bounds__(256) void k_prep_sigg2(size_t n, int q, const uint8
     fp_mul(t, t, pr.z);
     st_fp(S, S_P1 + 2, i, t);
     flags[i] = fl;
+}
+
+// SigG2 + shared verkey, one credential per lane PAIR (the layout of the pairing kernels): the even
+// lane decodes sigma_1, the odd lane sigma_2; each lane sums half of the fixed-base windows, the two
+// partial sums are exchanged by DPP and added (same operand order on both lanes, so both hold the
+// same Jacobian representation); the even lane writes (X Z, Y), the odd lane Z^3.
+__global__ __launch_bounds__(256) void k_prep_sigg2_pair(size_t n, int q, const uint8_t* __restrict__ s1b,
+                                                         const uint8_t* __restrict__ s2b,
+                                                         const uint8_t* __restrict__ msgs,
+                                                         const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                         const uint32_t* __restrict__ table,
+                                                         const uint32_t* __restrict__ binf_fixed,
+                                                         uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t i = g >> 1;
+    const int h = (int)(g & 1);
+    if (i >= n) return;  // pair-uniform
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp2> a;
+        if (!g2_decode(a, (h ? s2b : s1b) + i * 192)) fl |= h ? 2u : 1u;
+        if (h) f2_neg(a.y, a.y);  // -sigma_2
+        const int slot = h ? S_Q2 : S_Q1;
+        st_f2(S, slot, i, a.x);
+        st_f2(S, slot + 2, i, a.y);
+    }
+    Jac<Fp> pr, o;
+    msm_fixed_part<Fp>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, h == 0, table, binf_fixed, h ? NWIN / 2 : 0,
+                       h ? NWIN : NWIN / 2);
+    o.x = pl::swp(pr.x);
+    o.y = pl::swp(pr.y);
+    o.z = pl::swp(pr.z);
+    fl |= pl::swp(fl);
+    if (h) {
+        Jac<Fp> t = pr;
+        pr = o;
+        o = t;
+    }
+    jac_add(pr, pr, o);  // (even half) + (odd half) on both lanes
+    if (jac_is_inf(pr)) fl |= 4u;
+    Fp t;
+    if (!h) {
+        fp_mul(t, pr.x, pr.z);
+        st_fp(S, S_P1, i, t);
+        st_fp(S, S_P1 + 1, i, pr.y);
+        flags[i] = fl;
+    } else {
+        fp_sqr(t, pr.z);
+        fp_mul(t, t, pr.z);
+        st_fp(S, S_P1 + 2, i, t);
+    }
 }
 
 // SigG1: sigma in G1 (97 B), verkey in G2; pr converted to affine (it is the Miller-loop T)
@@ -403,8 +486,8 @@ int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const ui
     dim3 g(nblocks(n, 256)), b(256);
     if (mode == 0) {
         if (fixed)
-            hipLaunchKernelGGL(k_prep_sigg2<true>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
-                               d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
+            hipLaunchKernelGGL(k_prep_sigg2_pair, dim3(nblocks(2 * n, 256)), b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff,
+                               Xinf, d_table, d_binf_fixed, d_prep, d_flags);
         else
             hipLaunchKernelGGL(k_prep_sigg2<false>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
                                d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
