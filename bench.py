@@ -36,6 +36,23 @@ Q = 6
 MADS_PER_FPMUL = 288  # 12 x 12 limb products for a*b plus 12 x 12 for m*p (32x32->64 v_mad_u64_u32)
 PEAK_MAD_PER_S = 2.74e13  # measured gfx950 v_mad_u64_u32 issue rate, tools/ubench_int.hip (profiles/)
 HBM_PEAK_GBS = 8000.0
+# PMC counters of the same build, collected by tools/pmc_round.sh (separate rocprofv3 --pmc passes)
+# and summarised by tools/pmc_summary.py; bench.py cannot read counters in a plain run.
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_final", "pmc_summary.json")
+
+
+def pmc_traffic(kernel_key):
+    """HBM-side bytes per launch of the kernel whose name contains kernel_key: 2 x FETCH_SIZE (gfx950
+    counts half of wide reads, MI355X_MICROARCH.md HBM section) + WRITE_SIZE, both KiB; None if absent."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for name, c in d.items():
+        if kernel_key in name and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            return round((2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024)
+    return None
 
 
 def fp_mults_per_credential(q=Q):
@@ -305,7 +322,9 @@ def main():
             "phase_ms": {k: round(float(v), 3) for k, v in zip(names, phase_ms)},
             "roofline": {"bound": "valu-int", "kernel": names[dom], "achieved": round(achieved / 1e12, 3),
                          "peak": PEAK_MAD_PER_S / 1e12, "unit": "Tmad/s (v_mad_u64_u32)",
-                         "frac": round(achieved / PEAK_MAD_PER_S, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_MAD_PER_S, 4),
+                         "traffic": pmc_traffic("k_" + names[dom]), "traffic_unit": "bytes per launch (PMC, "
+                         "profiles/r01_final/pmc_summary.json: register-spill/call-frame scratch, not algorithmic)",
                          "algorithmic_mads_per_credential": round(fm[names[dom]] * MADS_PER_FPMUL),
                          "whole_step_frac": round(total_mads / (ms_per_step * 1e-3) / PEAK_MAD_PER_S, 4),
                          "hbm_view_GBs": round(n * (2 * 192 + q * 48 + 1) / (ms_per_step * 1e-3) / 1e9, 3),

@@ -21,18 +21,12 @@ int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* 
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
-int cck_miller_g2(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-                  uint32_t* d_f, hipStream_t st);
-int cck_miller_g1(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-                  uint32_t* d_f, hipStream_t st);
 int cck_miller_pl_g2(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                      uint32_t* d_f, hipStream_t st);
 int cck_miller_pl_g1(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                      uint32_t* d_f, hipStream_t st);
 int cck_fexp_pl(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                 uint8_t* d_gt, hipStream_t st);
-int cck_fexp_lane(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
-             uint8_t* d_gt, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
 int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
                   size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
@@ -112,27 +106,15 @@ struct cc_ctx {
 
 // mode 0 (SigG2): d_const = g~ affine G1 (24 words); mode 1 (SigG1): g~ Miller lines (68 x 72 words).
 // lane2: pair 1's G1 point is per lane (prep slots S_P2.., Jacobian evaluation form; RLC mode).
-// Pairing kernels: pair-lane form (tower_pl.h, one credential per lane pair; default) or the
-// one-credential-per-lane form (CC_LANE_LAYOUT=lane, kept for A/B measurement).
-static bool pair_lanes() {
-    static const int v = [] {
-        const char* e = getenv("CC_LANE_LAYOUT");
-        return (e && !strcmp(e, "lane")) ? 0 : 1;
-    }();
-    return v != 0;
-}
+// Pairing kernels run one credential per lane pair (tower_pl.h).
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                       uint32_t* d_f, hipStream_t st, int lane2 = 0) {
-    if (pair_lanes())
-        return mode == 0 ? cck_miller_pl_g2(lane2, n, d_prep, d_flags, d_const, d_f, st)
-                         : cck_miller_pl_g1(lane2, n, d_prep, d_flags, d_const, d_f, st);
-    return mode == 0 ? cck_miller_g2(lane2, n, d_prep, d_flags, d_const, d_f, st)
-                     : cck_miller_g1(lane2, n, d_prep, d_flags, d_const, d_f, st);
+    return mode == 0 ? cck_miller_pl_g2(lane2, n, d_prep, d_flags, d_const, d_f, st)
+                     : cck_miller_pl_g1(lane2, n, d_prep, d_flags, d_const, d_f, st);
 }
 static int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                     uint8_t* d_gt, hipStream_t st) {
-    return pair_lanes() ? cck_fexp_pl(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st)
-                        : cck_fexp_lane(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st);
+    return cck_fexp_pl(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st);
 }
 
 static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }

@@ -199,6 +199,27 @@ def test_generated_batch_against_c_oracle(ctxs, mode):
     assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v[:k])
 
 
+@pytest.mark.parametrize("n", [1, 3, 129, 257])
+def test_ragged_batch_sizes_pair_lanes(ctxs, n):
+    """Batch sizes that leave lane pairs / blocks partly filled (one credential per lane pair, 128
+    per block): every verdict and GT byte against the C oracle."""
+    from coconut import verify_batch
+    q = 6
+    b = _gen_batch(0, n, q, seed=100 + n)
+    ctx = ctxs["G2"]
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    v, gts = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], want_gt=True)
+    assert np.array_equal(v, b["expect"])
+    oc = oracle_lib()
+    ver = ctypes.create_string_buffer(n)
+    ref = ctypes.create_string_buffer(576 * n)
+    oc.oc_verify_batch(0, ctypes.c_size_t(n), ctypes.c_size_t(q), b["s1"], b["s2"], b["msgs"], b["X"], b["Y"], 0,
+                       b["g_tilde"], ver, ref, host_threads())
+    assert ref.raw == gts
+    assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v)
+
+
 def test_full_size_batch_config2(ctxs):
     """BASELINE config 2 size (65,536 credentials, q = 6, shared vk): every verdict equals the one
     known by construction (size-independent property; 1/16 corrupted)."""

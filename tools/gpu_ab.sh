@@ -7,6 +7,4 @@ echo "[ab] pytest -m gpu (pair-lane)"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout=300 -p no:cacheprovider > "$OUT/pytest_gpu_pl.log" 2>&1
 echo "[ab] bench pair-lane"
 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_pl.log" 2>&1
-echo "[ab] bench lane"
-CC_LANE_LAYOUT=lane timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_lane.log" 2>&1
 echo "[ab] done"

@@ -1,0 +1,34 @@
+#!/usr/bin/env python3
+"""Summarise the rocprofv3 PMC passes of tools/pmc_round.sh (one bench step) into per-kernel,
+per-launch counter values: profiles/<round>/pmc_summary.json.  bench.py reads the Miller kernel's
+FETCH_SIZE / WRITE_SIZE from it for roofline.traffic (MI355X_MICROARCH.md, HBM section: FETCH_SIZE
+counts half the bytes of wide coalesced reads on gfx950, so traffic = 2 * FETCH_SIZE + WRITE_SIZE;
+both are in KiB)."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main(src, dst):
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    launches = collections.defaultdict(set)
+    for f in sorted(glob.glob(os.path.join(src, "p*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"]
+            per[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            launches[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
+    out = {}
+    for k, cs in per.items():
+        if not any(s in k for s in ("k_miller", "k_fexp", "k_prep")):
+            continue
+        out[k] = {c: v / max(1, len(launches[(k, c)])) for c, v in cs.items()}
+    json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
+    print(json.dumps({k[:40]: {c: round(v, 1) for c, v in d.items() if c in ("FETCH_SIZE", "WRITE_SIZE")}
+                      for k, d in out.items()}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
