@@ -129,10 +129,17 @@ DEV void fp_sub(Fp& r, const Fp& a, const Fp& b) {
     for (int j = 0; j < NL; j++) r.v[j] = b1 ? u[j] : t[j];
 }
 
+// p - a for a != 0, 0 for a == 0 (one borrow chain and a mask)
 DEV void fp_neg(Fp& r, const Fp& a) {
-    Fp z;
-    fp_zero(z);
-    fp_sub(r, z, a);
+    uint32_t t[NL], o = 0, br = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        t[j] = __builtin_subc(p_limb(j), a.v[j], br, &br);
+        o |= a.v[j];
+    }
+    const uint32_t mask = o ? ~0u : 0u;
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.v[j] = t[j] & mask;
 }
 
 // ---------------------------------------------------------------- Montgomery multiplication

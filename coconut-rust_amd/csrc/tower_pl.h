@@ -148,21 +148,33 @@ DEV void f2_add(Fp2& r, const Fp2& x, const Fp2& y) { fp_add(r.c, x.c, y.c); }
 DEV void f2_sub(Fp2& r, const Fp2& x, const Fp2& y) { fp_sub(r.c, x.c, y.c); }
 DEV void f2_dbl(Fp2& r, const Fp2& x) { fp_dbl(r.c, x.c); }
 DEV void f2_neg(Fp2& r, const Fp2& x) { fp_neg(r.c, x.c); }
+// conj: negate the imaginary half only
 DEV void f2_conj(Fp2& r, const Fp2& x) {
-    Fp n;
-    fp_neg(n, x.c);
-    r.c = fp_sel(half_id() != 0, n, x.c);
+    uint32_t t[NL], o = 0, br = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        t[j] = __builtin_subc(p_limb(j), x.c.v[j], br, &br);
+        o |= x.c.v[j];
+    }
+    const bool neg = half_id() != 0 && o != 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.c.v[j] = neg ? t[j] : x.c.v[j];
 }
 DEV void f2_mul(Fp2& r, const Fp2& x, const Fp2& y) { r.c = f2_mul_call_(x.c, y.c); }
 DEV void f2_sqr(Fp2& r, const Fp2& x) { r.c = f2_sqr_call_(x.c); }
 DEV void f2_mul_fp(Fp2& r, const Fp2& x, const Fp& k) { fp_mul(r.c, x.c, k); }
-// x * (1 + i) = (a - b) + (a + b) i
+// x * (1 + i) = (a - b) + (a + b) i: own + (im ? partner : p - partner), one reduced addition
 DEV void f2_mul_xi(Fp2& r, const Fp2& x) {
     const Fp xs = swp(x.c);
-    Fp s, d;
-    fp_add(s, x.c, xs);
-    fp_sub(d, x.c, xs);
-    r.c = fp_sel(half_id() != 0, s, d);
+    const bool im = half_id() != 0;
+    Fp w;
+    uint32_t br = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        const uint32_t d = __builtin_subc(p_limb(j), xs.v[j], br, &br);  // p - xs in [1, p]
+        w.v[j] = im ? xs.v[j] : d;
+    }
+    fp_add(r.c, x.c, w);  // x + w < 2p
 }
 // (a + b i)^-1 = (a - b i) / (a^2 + b^2); the norm and its inverse are computed on both lanes
 DEV void f2_inv(Fp2& r, const Fp2& x) {
