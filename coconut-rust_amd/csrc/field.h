@@ -360,6 +360,8 @@ DEV bool f2_is_zero(const Fp2& x) { return fp_is_zero(x.a) && fp_is_zero(x.b); }
 DEV bool f2_eq(const Fp2& x, const Fp2& y) { return fp_eq(x.a, y.a) && fp_eq(x.b, y.b); }
 DEV void f2_add(Fp2& r, const Fp2& x, const Fp2& y) { fp_add(r.a, x.a, y.a); fp_add(r.b, x.b, y.b); }
 DEV void f2_sub(Fp2& r, const Fp2& x, const Fp2& y) { fp_sub(r.a, x.a, y.a); fp_sub(r.b, x.b, y.b); }
+// sum feeding only a multiplication (the pair-lane tower skips the reduction there; canonical here)
+DEV void f2_add_lz(Fp2& r, const Fp2& x, const Fp2& y) { f2_add(r, x, y); }
 DEV void f2_dbl(Fp2& r, const Fp2& x) { fp_dbl(r.a, x.a); fp_dbl(r.b, x.b); }
 DEV void f2_neg(Fp2& r, const Fp2& x) { fp_neg(r.a, x.a); fp_neg(r.b, x.b); }
 DEV void f2_conj(Fp2& r, const Fp2& x) { r.a = x.a; fp_neg(r.b, x.b); }

@@ -9,7 +9,7 @@
 // Fp2 across a lane pair halves the per-lane state and doubles the wave count (2,048 waves, two per
 // SIMD), while the multiplication count per credential stays the same:
 //
-//   Fp2 mul  (a + b i)(c + d i):  lane a computes a c + b (2p - d), lane b computes a d + b c — each
+//   Fp2 mul  (a + b i)(c + d i):  lane a computes a c + b (4p - d), lane b computes a d + b c — each
 //            a SUM of two 381-bit products with ONE Montgomery reduction (fp_mul2): 3 x 196 mads
 //            per lane vs 3 full multiplications (6 x 196) for Karatsuba on one lane.
 //   Fp2 sqr: lane a (a + b)(a - b), lane b a (2b): one multiplication per lane.
@@ -75,16 +75,18 @@ DEV Fp fp_mul2_v(const Fp& U1, const Fp& V1, const Fp& U2, const Fp& V2) {
     return mul2_29(a, b, c, d);
 }
 
-// 2p in radix 2^29 with every limb in [2^29 - 1, 2^30): 2p - y limb by limb needs no borrows
-DEV uint32_t two_p29(int k) {
-    constexpr uint32_t D[L29] = {0x3fff5556u, 0x3feffffeu, 0x29ffffdbu, 0x2ffffac4u, 0x3ec483d4u, 0x32a0f6afu, 0x35fb3985u,
-                                 0x213ce143u, 0x2ec8ee96u, 0x2434baccu, 0x258dd3dau, 0x25ff9a68u, 0x20223d46u, 0x00000019u};
+// 4p in radix 2^29 with limbs 0..12 in [2^29 - 1, 2^30) and limb 13 = 51: 4p - y limb by limb needs
+// no borrows for any y < 2p (y's limb 13 is then <= 26)
+DEV uint32_t four_p29(int k) {
+    constexpr uint32_t D[L29] = {0x3ffeaaacu, 0x3fdffffeu, 0x33ffffb8u, 0x3ffff589u, 0x3d8907a9u, 0x2541ed60u, 0x2bf6730cu,
+                                 0x2279c288u, 0x3d91dd2du, 0x28697599u, 0x2b1ba7b5u, 0x2bff34d1u, 0x20447a8du, 0x00000033u};
     return D[k];
 }
 
-// own half of x * y (x, y: own halves of two Fp2 values).  The operands are converted to radix 2^29
-// once and the partner's converted limbs fetched by DPP.
-//   re: a c + b (2p - d) = x y + xs (2p - ys);   im: b c + a d = x ys + xs y
+// own half of x * y (x, y: own halves of two Fp2 values, each < 2p: canonical or a lazy sum).  The
+// operands are converted to radix 2^29 once and the partner's converted limbs fetched by DPP.
+//   re: a c + b (4p - d) = x y + xs (4p - ys);   im: b c + a d = x ys + xs y
+// a c + b (4p - d) < 12 p^2 < p R, so the Montgomery result is < 2p and one subtraction makes it canonical.
 DEV Fp f2_mul_half(const Fp& x, const Fp& y) {
     const bool im = half_id() != 0;
     uint32_t a[L29], y29[L29], b[L29], c[L29], d[L29];
@@ -95,20 +97,29 @@ DEV Fp f2_mul_half(const Fp& x, const Fp& y) {
         c[k] = swp(a[k]);
         const uint32_t ys = swp(y29[k]);
         b[k] = im ? ys : y29[k];
-        d[k] = im ? y29[k] : two_p29(k) - ys;
+        d[k] = im ? y29[k] : four_p29(k) - ys;
     }
     return mul2_29(a, b, c, d);
 }
-// own half of x^2: re (a + b)(a - b), im a (2b)
+// 2p, 32-bit limbs
+DEV uint32_t two_p_limb(int j) {
+    constexpr uint32_t T[NL] = {0xffff5556u, 0x73fdffffu, 0x62a7ffffu, 0x3d57fffdu, 0xed61ec48u, 0xce61a541u,
+                                0xe70a257eu, 0xc8ee9709u, 0x869759aeu, 0x96374f6cu, 0x72ffcd34u, 0x340223d4u};
+    return T[j];
+}
+// own half of x^2 (x < 2p): re (a + b)(a - b) = (x + xs)(x + 2p - xs), im a (2b) = xs (x + x).  The
+// factors are left unreduced (< 4p each): Montgomery takes them (16 p^2 < p R), the result is canonical.
 DEV Fp f2_sqr_half(const Fp& x) {
     const bool im = half_id() != 0;
     const Fp xs = swp(x);
-    Fp s, d;
-    fp_add(s, x, xs);
-    fp_sub(d, x, xs);
-    Fp u = fp_sel(im, xs, s), v;
-    fp_dbl(v, x);
-    v = fp_sel(im, v, d);
+    Fp u, v;
+    uint32_t c1 = 0, c2 = 0, b3 = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        u.v[j] = __builtin_addc(im ? 0u : x.v[j], xs.v[j], c1, &c1);           // im: xs, re: x + xs
+        const uint32_t w = __builtin_subc(two_p_limb(j), xs.v[j], b3, &b3);   // 2p - xs > 0
+        v.v[j] = __builtin_addc(x.v[j], im ? x.v[j] : w, c2, &c2);            // im: 2x, re: x + 2p - xs
+    }
     return fp_mul_v(u, v);
 }
 
@@ -145,6 +156,12 @@ DEV bool pair_all(bool own) { return (swp((uint32_t)own) & (uint32_t)own) != 0; 
 DEV bool f2_is_zero(const Fp2& x) { return pair_all(fp_is_zero(x.c)); }
 DEV bool f2_eq(const Fp2& x, const Fp2& y) { return pair_all(fp_eq(x.c, y.c)); }
 DEV void f2_add(Fp2& r, const Fp2& x, const Fp2& y) { fp_add(r.c, x.c, y.c); }
+// x + y without reduction (< 2p for canonical x, y): only for values consumed by f2_mul / f2_sqr
+DEV void f2_add_lz(Fp2& r, const Fp2& x, const Fp2& y) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < NL; j++) r.c.v[j] = __builtin_addc(x.c.v[j], y.c.v[j], c, &c);
+}
 DEV void f2_sub(Fp2& r, const Fp2& x, const Fp2& y) { fp_sub(r.c, x.c, y.c); }
 DEV void f2_dbl(Fp2& r, const Fp2& x) { fp_dbl(r.c, x.c); }
 DEV void f2_neg(Fp2& r, const Fp2& x) { fp_neg(r.c, x.c); }
