@@ -55,13 +55,26 @@ DEV void ld_P(G1Eval& P, const PSrc& s, size_t i) {
     }
 }
 
-// f *= line(P); a skipped pair (identity argument) contributes the constant 1
-DEV void eval_mul(Fp12& f, const Fp2& l0, const Fp2& l2, const Fp2& l3, const G1Eval& P, bool skip) {
+// f *= line(P); a skipped pair (identity argument) contributes the constant 1.  P's coordinates are
+// loaded one at a time, right before their multiplication (fewer live registers across the calls).
+DEV void ld_Pc(Fp& x, const PSrc& s, int slot, size_t i) {
+#pragma unroll
+    for (int k = 0; k < NL; k++) x.v[k] = s.p[(size_t)(slot * NL + k) * s.n + i * s.is];
+}
+DEV void eval_mul(Fp12& f, const Fp2& l0, const Fp2& l2, const Fp2& l3, const PSrc& ps, size_t i, bool skip) {
     if (skip) return;  // e(O, Q) = e(P, O) = 1
     Fp2 a0, a2, a3;
-    f2_mul_fp(a0, l0, P.pz);
-    f2_mul_fp(a2, l2, P.px);
-    f2_mul_fp(a3, l3, P.py);
+    Fp c;
+    if (ps.jac) {
+        ld_Pc(c, ps, 2, i);
+        f2_mul_fp(a0, l0, c);
+    } else {
+        a0 = l0;
+    }
+    ld_Pc(c, ps, 0, i);
+    f2_mul_fp(a2, l2, c);
+    ld_Pc(c, ps, 1, i);
+    f2_mul_fp(a3, l3, c);
     f12_mul_line(f, a0, a2, a3);
 }
 
@@ -103,9 +116,7 @@ static __device__ __noinline__ void miller_add(StepState* st, const uint32_t* qs
         line_add(T, Q, l0, l2, l3);
         st->T = T;
     }
-    G1Eval P;
-    ld_P(P, ps, i);
-    eval_mul(f, l0, l2, l3, P, skip);
+    eval_mul(f, l0, l2, l3, ps, i, skip);
     st->f = f;
 }
 
@@ -162,9 +173,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
             } else {
                 line_dbl(T, l0, l2, l3);
             }
-            G1Eval P;
-            ld_P(P, k ? ps1 : ps0, i);
-            eval_mul(f, l0, l2, l3, P, k ? skip1 : skip0);
+            eval_mul(f, l0, l2, l3, k ? ps1 : ps0, i, k ? skip1 : skip0);
             if (kSigG2) {  // swap T with the parked one
                 G2Proj U;
                 unpark(U, lds);
