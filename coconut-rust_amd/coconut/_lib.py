@@ -23,6 +23,8 @@ _SIGS = {
     "cc_status_str": (ctypes.c_char_p, [c_int]),
     "cc_version": (ctypes.c_char_p, []),
     "cc_ctx_create": (c_int, [c_int, c_int, ctypes.POINTER(c_p)]),
+    "cc_ctx_create_multi": (c_int, [ctypes.c_uint64, c_int, ctypes.POINTER(c_p)]),
+    "cc_ctx_num_devices": (c_int, [c_p, ctypes.POINTER(c_int)]),
     "cc_ctx_destroy": (c_int, [c_p]),
     "cc_ctx_mode": (c_int, [c_p, ctypes.POINTER(c_int)]),
     "cc_set_params": (c_int, [c_p, c_p]),

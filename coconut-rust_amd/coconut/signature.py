@@ -124,11 +124,19 @@ class Context:
 
     _default = {}
 
-    def __init__(self, device: int = 0, mode: GroupMode = GroupMode.SIG_G2):
+    def __init__(self, device: int = 0, mode: GroupMode = GroupMode.SIG_G2, devices: Sequence[int] = None):
+        """devices=[...] makes a device-set context (cc_ctx_create_multi): cc_verify_batch shards the
+        batch over those GPUs, RLC mode gathers the per-GPU partials with RCCL inside the library."""
         self.mode = GroupMode(mode)
-        self.device = device
+        self.device = device if devices is None else devices[0]
         h = ctypes.c_void_p()
-        check(lib.cc_ctx_create(device, int(self.mode), ctypes.byref(h)), "cc_ctx_create")
+        if devices is None:
+            check(lib.cc_ctx_create(device, int(self.mode), ctypes.byref(h)), "cc_ctx_create")
+        else:
+            mask = 0
+            for d in devices:
+                mask |= 1 << int(d)
+            check(lib.cc_ctx_create_multi(mask, int(self.mode), ctypes.byref(h)), "cc_ctx_create_multi")
         self.h = h
         self._gtilde = None
         self._vk = None
@@ -168,6 +176,11 @@ class Context:
         py, k2 = buf(Yb)
         check(lib.cc_set_verkey(self.h, px, py, q), "cc_set_verkey")
         self._vk = key
+
+    def num_devices(self) -> int:
+        n = ctypes.c_int()
+        check(lib.cc_ctx_num_devices(self.h, ctypes.byref(n)), "cc_ctx_num_devices")
+        return n.value
 
     def timing(self, enabled: bool = True):
         check(lib.cc_set_timing(self.h, int(enabled)))

@@ -7,6 +7,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <rccl/rccl.h>
+
+#include <thread>
 #include <vector>
 
 #include "../../include/coconut_hip.h"
@@ -55,7 +58,7 @@ struct DevBuf {
     size_t bytes = 0;
     int ensure(size_t want) {
         if (want <= bytes) return 0;
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
         if (hipMalloc(&p, want) != hipSuccess) return -1;
@@ -63,7 +66,7 @@ struct DevBuf {
         return 0;
     }
     void release() {
-        if (p) hipFree(p);
+        if (p) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
     }
@@ -102,6 +105,35 @@ struct cc_ctx {
     bool timing = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_ms[3] = {0, 0, 0};
+    // orders a caller-supplied stream against the context stream (StreamOrder below)
+    hipEvent_t ev_order = nullptr;
+    // device set (cc_ctx_create_multi): one single-device context per GPU and one RCCL communicator
+    // per GPU (ncclCommInitAll, this process drives every device); empty for a single-device context
+    std::vector<cc_ctx*> peers;
+    std::vector<ncclComm_t> comms;
+    DevBuf rlc_gath;  // per peer: gathered partials (ndev x 145 words)
+};
+
+// Every *_device entry point may run on a caller stream while the context's workspaces (prep, flags,
+// fbuf, scratch, RLC buffers, verkey tables) are shared with the host entry points, which run on
+// c->stream.  StreamOrder makes the caller's stream wait for everything already queued on c->stream
+// at entry, and c->stream wait for the call's work at exit, so calls on any mix of streams touch the
+// workspaces in program order (two device calls on different streams are chained through c->stream).
+struct StreamOrder {
+    cc_ctx* c;
+    hipStream_t st;
+    StreamOrder(cc_ctx* c_, hipStream_t s) : c(c_), st(s) {
+        if (st != c->stream) {
+            (void)hipEventRecord(c->ev_order, c->stream);
+            (void)hipStreamWaitEvent(st, c->ev_order, 0);
+        }
+    }
+    ~StreamOrder() {
+        if (st != c->stream) {
+            (void)hipEventRecord(c->ev_order, st);
+            (void)hipStreamWaitEvent(c->stream, c->ev_order, 0);
+        }
+    }
 };
 
 // mode 0 (SigG2): d_const = g~ affine G1 (24 words); mode 1 (SigG1): g~ Miller lines (68 x 72 words).
@@ -122,6 +154,9 @@ static inline int oth_bytes(int mode) { return mode == 0 ? 97 : 192; }
 static inline int oth_group(int mode) { return mode == 0 ? 1 : 2; }
 static inline int sig_group(int mode) { return mode == 0 ? 2 : 1; }
 static inline size_t aff_words(int group) { return group == 1 ? 24 : 48; }
+
+static inline cc_ctx* primary(cc_ctx* c) { return c && !c->peers.empty() ? c->peers[0] : c; }
+static inline const cc_ctx* primary(const cc_ctx* c) { return c && !c->peers.empty() ? c->peers[0] : c; }
 
 #define HIPCK(x)                                  \
     do {                                          \
@@ -162,23 +197,34 @@ cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
         delete c;
         return CC_ERR_HIP;
     }
-    for (auto& e : c->ev) hipEventCreate(&e);
+    for (auto& e : c->ev) (void)hipEventCreate(&e);
+    (void)hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming);
     *out = c;
     return CC_OK;
 }
 
 cc_status cc_ctx_destroy(cc_ctx* c) {
     if (!c) return CC_OK;
-    hipSetDevice(c->device);
-    hipStreamSynchronize(c->stream);
+    if (!c->peers.empty()) {
+        for (size_t k = 0; k < c->comms.size(); k++) {
+            (void)hipSetDevice(c->peers[k]->device);
+            ncclCommDestroy(c->comms[k]);
+        }
+        for (cc_ctx* p : c->peers) cc_ctx_destroy(p);
+        delete c;
+        return CC_OK;
+    }
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag,
                       &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept};
     for (auto* b : bufs) b->release();
     for (auto& b : c->in_aux) b.release();
-    for (auto& e : c->ev) if (e) hipEventDestroy(e);
-    hipStreamDestroy(c->stream);
+    for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
+    if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+    (void)hipStreamDestroy(c->stream);
     delete c;
     return CC_OK;
 }
@@ -190,12 +236,14 @@ cc_status cc_ctx_mode(const cc_ctx* c, int* m) {
 }
 
 cc_status cc_set_timing(cc_ctx* c, int enabled) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c) return CC_ERR_DECODE;
     c->timing = enabled != 0;
     return CC_OK;
 }
 
 cc_status cc_last_timing(const cc_ctx* c, float* a, float* b, float* d) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c) return CC_ERR_DECODE;
     if (a) *a = c->last_ms[0];
     if (b) *b = c->last_ms[1];
@@ -236,6 +284,14 @@ static cc_status rebuild_tables(cc_ctx* c) {
 
 cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
     if (!c || !g_tilde) return CC_ERR_DECODE;
+    if (!c->peers.empty()) {
+        for (cc_ctx* p : c->peers) {
+            cc_status s = cc_set_params(p, g_tilde);
+            if (s) return s;
+        }
+        c->have_params = true;
+        return CC_OK;
+    }
     HIPCK(hipSetDevice(c->device));
     int og = oth_group(c->mode);
     size_t aw = aff_words(og);
@@ -264,6 +320,15 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
 cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q) {
     if (!c || !X || (q && !Y) || q > 4096) return CC_ERR_DECODE;
     if (!c->have_params) return CC_ERR_STATE;
+    if (!c->peers.empty()) {
+        for (cc_ctx* p : c->peers) {
+            cc_status s = cc_set_verkey(p, X, Y, q);
+            if (s) return s;
+        }
+        c->q = q;
+        c->have_vk = true;
+        return CC_OK;
+    }
     HIPCK(hipSetDevice(c->device));
     int og = oth_group(c->mode);
     size_t eb = (size_t)oth_bytes(c->mode), aw = aff_words(og);
@@ -294,27 +359,28 @@ static cc_status ensure_work(cc_ctx* c, size_t n) {
 // the three verify launches on device buffers; timing per phase when enabled
 static cc_status launch_verify(cc_ctx* c, size_t n, size_t q, int fixed, const uint8_t* d_s1, const uint8_t* d_s2,
                                const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
-    if (c->timing) hipEventRecord(c->ev[0], st);
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_prep(c->mode, fixed, n, (int)q, d_s1, d_s2, d_msgs, c->vk_aff.as<uint32_t>(), c->X_inf,
                  c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(), c->vkb.as<uint32_t>(),
                  c->vkbinf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
-    if (c->timing) hipEventRecord(c->ev[1], st);
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
-    if (c->timing) hipEventRecord(c->ev[2], st);
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(), d_verdicts, d_gt, st));
-    if (c->timing) hipEventRecord(c->ev[3], st);
+    if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }
 
 static void collect_timing(cc_ctx* c) {
     if (!c->timing) return;
-    hipEventSynchronize(c->ev[3]);
-    for (int k = 0; k < 3; k++) hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
+    (void)hipEventSynchronize(c->ev[3]);
+    for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
 }
 
 cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s1, const uint8_t* d_s2,
                                  const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt, void* stream) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!d_s1 || !d_s2 || !d_verdicts))) return CC_ERR_DECODE;
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
     if (q != c->q) return CC_ERR_LEN;
@@ -323,7 +389,10 @@ cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d
     cc_status s = ensure_work(c, n);
     if (s) return s;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    s = launch_verify(c, n, q, 1, d_s1, d_s2, d_msgs, d_verdicts, d_gt, st);
+    {
+        StreamOrder order(c, st);
+        s = launch_verify(c, n, q, 1, d_s1, d_s2, d_msgs, d_verdicts, d_gt, st);
+    }
     if (s) return s;
     if (c->timing) collect_timing(c);
     return CC_OK;
@@ -342,40 +411,53 @@ static int fresh_seed(uint8_t seed[32]) {
 cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_index, const uint8_t* seed32,
                                 const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs, uint32_t* d_partial,
                                 void* stream) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c || !seed32 || !d_partial || (n && (!d_s1 || !d_s2 || (q && !d_msgs)))) return CC_ERR_DECODE;
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
     if (q != c->q) return CC_ERR_LEN;
-    if (!n) return CC_ERR_DECODE;
     HIPCK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    StreamOrder order(c, st);
+    if (!n) {
+        // empty shard (a batch smaller than the rank count): the neutral partial — Fp12 one (Montgomery
+        // one in slot 0, zeros elsewhere) and a clear identity flag — so every rank still joins the
+        // all-gather and the product over ranks is unchanged
+        static const uint32_t kOne[12] = {0x03a9fb84u, 0xc57400d2u, 0x629c4a23u, 0x6147acdeu, 0x7e6d26cbu, 0x6b0f4b0bu,
+                                          0xc2b7d6e1u, 0x91ecbde7u, 0x4fdd80b8u, 0xd56a23c3u, 0xf3a0d636u, 0x13317c30u};
+        HIPCK(hipMemsetAsync(d_partial, 0, 145 * 4, st));
+        HIPCK(hipMemcpyAsync(d_partial, kOne, sizeof(kOne), hipMemcpyHostToDevice, st));
+        return CC_OK;
+    }
     cc_status s = ensure_work(c, n);
     if (s) return s;
     if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4)) return CC_ERR_HIP;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     memcpy(c->rlc_key_host, seed32, 32);
     HIPCK(hipMemcpyAsync(c->rlc_key.p, c->rlc_key_host, 32, hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
-    if (c->timing) hipEventRecord(c->ev[0], st);
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_prep_rlc(c->mode, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
                      c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
                      c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), st));
-    if (c->timing) hipEventRecord(c->ev[1], st);
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st, 1));
-    if (c->timing) hipEventRecord(c->ev[2], st);
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_rlc_reduce(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,
                        st));
-    if (c->timing) hipEventRecord(c->ev[3], st);
+    if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }
 
 cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_partials, uint8_t* d_accept,
                                uint8_t* d_gt, void* stream) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c || !nparts || !d_partials || !d_accept) return CC_ERR_DECODE;
     HIPCK(hipSetDevice(c->device));
     cc_status s = ensure_work(c, 1);
     if (s) return s;
     if (c->rlc_flag.ensure(4)) return CC_ERR_HIP;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    StreamOrder order(c, st);
     KCK(cck_rlc_combine(nparts, d_partials, c->fbuf.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), st));
     // one final exponentiation; flags[0] bit0 (a sigma was the identity somewhere) forces a reject
     KCK(cck_fexp(1, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), d_accept, d_gt, st));
@@ -397,6 +479,10 @@ static cc_status rlc_host(cc_ctx* c, size_t n, size_t q, uint8_t* accept) {
     return CC_OK;
 }
 
+static cc_status multi_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, const uint8_t* s2,
+                              const uint8_t* msgs, const uint8_t* vkX, const uint8_t* vkY, uint8_t* verdicts,
+                              uint8_t* gt, int rlc);
+
 cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, const uint8_t* s2, const uint8_t* msgs,
                           const uint8_t* vkX, const uint8_t* vkY, uint8_t* verdicts, uint8_t* gt, int rlc) {
     if (!c || (n && (!s1 || !s2 || !verdicts || (q && !msgs)))) return CC_ERR_DECODE;
@@ -408,6 +494,7 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
         if (q != c->q) return CC_ERR_LEN;
     }
     if (!n) return CC_OK;
+    if (!c->peers.empty()) return multi_verify(c, n, q, s1, s2, msgs, vkX, vkY, verdicts, gt, rlc);
     HIPCK(hipSetDevice(c->device));
     size_t sb = (size_t)sig_bytes(c->mode), ob = (size_t)oth_bytes(c->mode);
     if (c->in_s1.ensure(n * sb) || c->in_s2.ensure(n * sb) || c->in_msgs.ensure(n * q * 48 + 16) ||
@@ -456,6 +543,7 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
 
 cc_status cc_fixed_base_mul(cc_ctx* c, int group, const uint8_t* base, size_t n, const uint8_t* scalars,
                             uint8_t* out) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c || !base || (n && (!scalars || !out)) || (group != 1 && group != 2)) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
@@ -479,6 +567,7 @@ cc_status cc_fixed_base_mul(cc_ctx* c, int group, const uint8_t* base, size_t n,
 
 cc_status cc_signature_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* ids,
                                        const uint8_t* s1, const uint8_t* s2, uint8_t* out_s1, uint8_t* out_s2) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!ids || !s1 || !s2 || !out_s1 || !out_s2))) return CC_ERR_DECODE;
     if (len < t || len == 0) return CC_ERR_THRESHOLD;  // reference: assert!(sigs.len() >= threshold) + sigs[0]
     if (!n) return CC_OK;
@@ -506,6 +595,7 @@ cc_status cc_signature_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t
 
 cc_status cc_verkey_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, size_t q, const uint64_t* ids,
                                     const uint8_t* X, const uint8_t* Y, uint8_t* outX, uint8_t* outY) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!ids || !X || !outX || (q && (!Y || !outY))))) return CC_ERR_DECODE;
     if (len < t || len == 0) return CC_ERR_THRESHOLD;
     if (!n) return CC_OK;
@@ -544,6 +634,7 @@ cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nr
                               const uint8_t* s2, const uint8_t* J, const uint8_t* T, const uint8_t* resp,
                               const uint8_t* chal, const uint64_t* rev_idx, const uint8_t* rev_msgs,
                               uint8_t* verdicts, uint8_t* gt) {
+    c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!s1 || !s2 || !J || !T || !chal || !verdicts || (nresp && !resp) || (r && (!rev_idx || !rev_msgs)))))
         return CC_ERR_DECODE;
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
@@ -594,6 +685,133 @@ cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nr
     if (gt) HIPCK(hipMemcpyAsync(gt, c->gt.p, n * 576, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     return CC_OK;
+}
+
+
+// ---------------------------------------------------------------- device sets + RCCL
+cc_status cc_ctx_create_multi(uint64_t device_mask, cc_group_mode mode, cc_ctx** out) {
+    if (!out || !device_mask || (mode != CC_SIG_G2 && mode != CC_SIG_G1)) return CC_ERR_DECODE;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) return CC_ERR_HIP;
+    std::vector<int> devs;
+    for (int d = 0; d < 64; d++)
+        if ((device_mask >> d) & 1ull) {
+            if (d >= ndev) return CC_ERR_HIP;
+            devs.push_back(d);
+        }
+    cc_ctx* c = new cc_ctx();
+    c->device = devs[0];
+    c->mode = (int)mode;
+    for (int d : devs) {
+        cc_ctx* p = nullptr;
+        cc_status s = cc_ctx_create(d, mode, &p);
+        if (s) {
+            for (cc_ctx* q : c->peers) cc_ctx_destroy(q);
+            delete c;
+            return s;
+        }
+        c->peers.push_back(p);
+    }
+    c->comms.resize(devs.size());
+    if (ncclCommInitAll(c->comms.data(), (int)devs.size(), devs.data()) != ncclSuccess) {
+        c->comms.clear();
+        for (cc_ctx* q : c->peers) cc_ctx_destroy(q);
+        delete c;
+        return CC_ERR_RCCL;
+    }
+    *out = c;
+    return CC_OK;
+}
+
+cc_status cc_ctx_num_devices(const cc_ctx* c, int* n) {
+    if (!c || !n) return CC_ERR_DECODE;
+    *n = c->peers.empty() ? 1 : (int)c->peers.size();
+    return CC_OK;
+}
+
+}  // extern "C"
+
+// run f(k, lo, hi) for every peer k on its own host thread over the contiguous shard [lo, hi)
+template <class F>
+static cc_status for_shards(cc_ctx* c, size_t n, F f) {
+    const size_t k = c->peers.size();
+    std::vector<cc_status> st(k, CC_OK);
+    std::vector<std::thread> th;
+    for (size_t d = 0; d < k; d++)
+        th.emplace_back([&, d] { st[d] = f(d, n * d / k, n * (d + 1) / k); });
+    for (auto& t : th) t.join();
+    for (cc_status s : st)
+        if (s) return s;
+    return CC_OK;
+}
+
+extern "C" {
+
+// Shard by credential over the device set.  Per-credential mode: every device verifies its slice, no
+// collective.  RLC mode (shared verkey): every device reduces its slice to one 145-word partial, ONE
+// ncclAllGather over xGMI exchanges them, every device multiplies the gathered partials and runs the
+// single final exponentiation; on reject every device falls back to per-credential verification.
+static cc_status multi_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, const uint8_t* s2,
+                              const uint8_t* msgs, const uint8_t* vkX, const uint8_t* vkY, uint8_t* verdicts,
+                              uint8_t* gt, int rlc) {
+    const size_t sb = (size_t)sig_bytes(c->mode), ob = (size_t)oth_bytes(c->mode);
+    const size_t k = c->peers.size();
+    if (rlc && !vkX && !gt) {
+        uint8_t seed[32];
+        if (fresh_seed(seed)) return CC_ERR_HIP;
+        // stage each slice and compute its partial
+        cc_status s = for_shards(c, n, [&](size_t d, size_t lo, size_t hi) -> cc_status {
+            cc_ctx* p = c->peers[d];
+            const size_t m = hi - lo;
+            HIPCK(hipSetDevice(p->device));
+            if (p->in_s1.ensure(m * sb + 16) || p->in_s2.ensure(m * sb + 16) || p->in_msgs.ensure(m * q * 48 + 16) ||
+                p->rlc_part.ensure(145 * 4) || p->rlc_gath.ensure(k * 145 * 4) || p->rlc_accept.ensure(1))
+                return CC_ERR_HIP;
+            if (m) {
+                HIPCK(hipMemcpyAsync(p->in_s1.p, s1 + lo * sb, m * sb, hipMemcpyHostToDevice, p->stream));
+                HIPCK(hipMemcpyAsync(p->in_s2.p, s2 + lo * sb, m * sb, hipMemcpyHostToDevice, p->stream));
+                if (q) HIPCK(hipMemcpyAsync(p->in_msgs.p, msgs + lo * q * 48, m * q * 48, hipMemcpyHostToDevice, p->stream));
+            }
+            return cc_rlc_partial_device(p, m, q, lo, seed, p->in_s1.as<uint8_t>(), p->in_s2.as<uint8_t>(),
+                                         p->in_msgs.as<uint8_t>(), p->rlc_part.as<uint32_t>(), p->stream);
+        });
+        if (s) return s;
+        // the one exchange step: all-gather of the 580-byte partials
+        if (ncclGroupStart() != ncclSuccess) return CC_ERR_RCCL;
+        for (size_t d = 0; d < k; d++) {
+            cc_ctx* p = c->peers[d];
+            if (ncclAllGather(p->rlc_part.p, p->rlc_gath.p, 145, ncclUint32, c->comms[d], p->stream) != ncclSuccess) {
+                ncclGroupEnd();
+                return CC_ERR_RCCL;
+            }
+        }
+        if (ncclGroupEnd() != ncclSuccess) return CC_ERR_RCCL;
+        std::vector<uint8_t> acc(k, 0);
+        s = for_shards(c, n, [&](size_t d, size_t, size_t) -> cc_status {
+            cc_ctx* p = c->peers[d];
+            HIPCK(hipSetDevice(p->device));
+            cc_status r = cc_rlc_finish_device(p, k, p->rlc_gath.as<uint32_t>(), p->rlc_accept.as<uint8_t>(), nullptr,
+                                               p->stream);
+            if (r) return r;
+            HIPCK(hipMemcpyAsync(&acc[d], p->rlc_accept.p, 1, hipMemcpyDeviceToHost, p->stream));
+            HIPCK(hipStreamSynchronize(p->stream));
+            return CC_OK;
+        });
+        if (s) return s;
+        for (size_t d = 1; d < k; d++)
+            if (acc[d] != acc[0]) return CC_ERR_RCCL;  // every device multiplies the same gathered partials
+        if (acc[0]) {
+            memset(verdicts, 1, n);
+            return CC_OK;
+        }
+    }
+    // per-credential verification of every slice (also the RLC fallback)
+    return for_shards(c, n, [&](size_t d, size_t lo, size_t hi) -> cc_status {
+        if (hi == lo) return CC_OK;
+        return cc_verify_batch(c->peers[d], hi - lo, q, s1 + lo * sb, s2 + lo * sb, msgs + lo * q * 48,
+                               vkX ? vkX + lo * ob : nullptr, vkX ? vkY + lo * q * ob : nullptr, verdicts + lo,
+                               gt ? gt + lo * 576 : nullptr, 0);
+    });
 }
 
 }  // extern "C"

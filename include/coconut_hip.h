@@ -24,6 +24,14 @@
  *
  * All host pointers are caller-owned, read during the call and never retained.  A context owns
  * one HIP device, one stream and the device tables; use one context per calling thread.
+ * A context made by cc_ctx_create_multi spans a device set (one single-device context and one RCCL
+ * communicator per GPU, one host thread per GPU during a call): cc_set_params / cc_set_verkey apply
+ * to every device and cc_verify_batch shards the batch by credential over the set (RLC mode: one
+ * ncclAllGather of 580-byte partials over xGMI); the other entry points run on the
+ * set's first device.
+ * Streams: the *_device entry points take a caller stream; the library orders it against the
+ * context's own stream (which the host entry points use) with events at entry and exit, so calls on
+ * any mix of streams see the context's workspaces in program order.
  * Errors mirror the reference's failure modes (src/errors.rs:6-24): where the reference panics
  * (assert!/unwrap) the C ABI returns a code instead.
  */
@@ -56,6 +64,10 @@ const char* cc_status_str(int status);
 const char* cc_version(void);
 
 cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out);
+/* Device set: bit d of device_mask selects GPU d (SURVEY.md §8b `cc_ctx_create(device_mask, ...)`);
+ * CC_ERR_RCCL if the communicators cannot be created. */
+cc_status cc_ctx_create_multi(uint64_t device_mask, cc_group_mode mode, cc_ctx** out);
+cc_status cc_ctx_num_devices(const cc_ctx* ctx, int* ndev);
 cc_status cc_ctx_destroy(cc_ctx* ctx);
 cc_status cc_ctx_mode(const cc_ctx* ctx, int* mode_out);
 
@@ -90,7 +102,8 @@ cc_status cc_verify_batch_device(cc_ctx* ctx, size_t n, size_t q, const uint8_t*
  * gathers the partials of all GPUs (RCCL all-gather over xGMI, or any transport) and every GPU
  * finishes with ONE final exponentiation:
  *   cc_rlc_partial_device: deltas = ChaCha20(seed32, base_index + i), i < n (shared verkey only);
- *                          d_partial: 145 x u32 device buffer.
+ *                          d_partial: 145 x u32 device buffer; n = 0 (an empty shard) writes the
+ *                          neutral partial (Fp12 one, flag clear) so the rank still joins the gather.
  *   cc_rlc_finish_device : product of nparts partials (nparts x 145 u32, device), final
  *                          exponentiation; *d_accept = 1 iff the whole batch verifies (then every
  *                          per-credential verdict is 1); 0 means "fall back to per-credential

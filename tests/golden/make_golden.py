@@ -158,6 +158,49 @@ def make_aggregate(mode, seed, q=6, t=3, n=6, big=False):
             "cases": cases}
 
 
+def make_aggregate_subsets(mode, seed, q=6, t=67, n=100, ncase=3):
+    """BASELINE config 4 shape: t = 67 of n = 100 issuers, each case a seeded random 67-subset of ids
+    1..100 (gaps, shuffled order); case 1 also carries entries beyond t (ignored by the reference) and
+    case 2 a duplicated id inside the first t (HashSet de-duplication, signature.rs:454-458)."""
+    import random
+    grp, rng, params, sx, sy, signers, _ = setup(mode, q, t, n, seed)
+    msgs = [rng.fr() for _ in range(q)]
+    h = grp.sig.mul(grp.sig.gen, rng.fr())
+    partial = {s["id"]: C.sign(grp, s["sk"], msgs, h) for s in signers}
+    pick = random.Random(seed)
+    cases = []
+    for c in range(ncase):
+        ids = pick.sample(range(1, n + 1), t + (3 if c == 1 else 0))
+        if c == 2:
+            ids[5] = ids[40]
+        sigs = [(i, partial[i]) for i in ids]
+        keys = [(i, signers[i - 1]["vk"]) for i in ids]
+        asig = C.signature_aggregate(grp, t, sigs)
+        avk = C.verkey_aggregate(grp, t, keys)
+        if len(set(ids[:t])) == t:
+            assert avk[0] == grp.other.mul(params["g_tilde"], sx)
+            assert C.verify(grp, asig, msgs, avk, params["g_tilde"])
+        cases.append({
+            "ids": ids,
+            "sigma1": [hx(grp.sig_to_bytes(partial[i][0])) for i in ids],
+            "sigma2": [hx(grp.sig_to_bytes(partial[i][1])) for i in ids],
+            "X": [hx(grp.oth_to_bytes(signers[i - 1]["vk"][0])) for i in ids],
+            "Y": [[hx(grp.oth_to_bytes(y)) for y in signers[i - 1]["vk"][1]] for i in ids],
+            "out_sigma1": hx(grp.sig_to_bytes(asig[0])),
+            "out_sigma2": hx(grp.sig_to_bytes(asig[1])),
+            "out_X": hx(grp.oth_to_bytes(avk[0])),
+            "out_Y": [hx(grp.oth_to_bytes(y)) for y in avk[1]],
+            "verifies": int(C.verify(grp, asig, msgs, avk, params["g_tilde"])),
+        })
+        print(f"  aggregate-subsets {mode} case {c} ids={ids[:6]}...", flush=True)
+    return {"mode": mode, "q": q, "threshold": t, "total": n, "seed": seed,
+            "g_tilde": hx(grp.oth_to_bytes(params["g_tilde"])),
+            "msgs": [fr_hex(m) for m in msgs],
+            "secret_X": hx(grp.oth_to_bytes(grp.other.mul(params["g_tilde"], sx))),
+            "secret_Y": [hx(grp.oth_to_bytes(grp.other.mul(params["g_tilde"], y))) for y in sy],
+            "cases": cases}
+
+
 POK_KINDS = ["valid", "valid", "bad_chal", "bad_revealed", "bad_response", "sigma1_inf",
              "bad_J", "valid"]
 
@@ -247,7 +290,11 @@ def main():
             write(f"aggregate_{mode.lower()}.json", make_aggregate(mode, 4))
         if want("pok"):
             write(f"pok_{mode.lower()}_q6.json", make_pok(mode, 6, [3, 5], 8, 5))
-            write(f"pok_{mode.lower()}_q32.json", make_pok(mode, 32, [3, 5, 7, 11, 13, 17, 19, 23], 4, 6))
+            write(f"pok_{mode.lower()}_q32.json", make_pok(mode, 32, [3, 5, 7, 11, 13, 17, 19, 23], 8, 6))
+        if want("rlc16"):
+            write(f"verify_{mode.lower()}_q16.json", make_verify(mode, 16, 12, 8))
+        if want("agg67"):
+            write(f"aggregate_{mode.lower()}_t67_subsets.json", make_aggregate_subsets(mode, 9))
     if want("aggbig"):
         write("aggregate_g2_t67.json", make_aggregate("G2", 7, q=6, t=67, n=100, big=True))
 

@@ -83,7 +83,8 @@ def test_verify_length_mismatch_is_an_error(ctxs):
     assert e.value.code == -1
 
 
-@pytest.mark.parametrize("name", ["aggregate_g2.json", "aggregate_g1.json", "aggregate_g2_t67.json"])
+@pytest.mark.parametrize("name", ["aggregate_g2.json", "aggregate_g1.json", "aggregate_g2_t67.json",
+                                  "aggregate_g2_t67_subsets.json", "aggregate_g1_t67_subsets.json"])
 def test_aggregate_golden(ctxs, name):
     from coconut import signature_aggregate_batch, verkey_aggregate_batch
     d = golden(name)

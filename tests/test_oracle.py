@@ -119,7 +119,7 @@ def _verify_fixture_c(oc, name):
 
 
 @pytest.mark.parametrize("name", ["verify_g2_q6.json", "verify_g1_q6.json", "verify_g2_q16_pervk.json",
-                                  "verify_g1_q16_pervk.json"])
+                                  "verify_g1_q16_pervk.json", "verify_g2_q16.json", "verify_g1_q16.json"])
 def test_c_oracle_matches_golden_verify(oc, name):
     d, ver, gts = _verify_fixture_c(oc, name)
     for i, c in enumerate(d["creds"]):
@@ -136,7 +136,8 @@ def test_c_oracle_pairing_kat(oc):
         assert out.raw.hex() == k["gt"]
 
 
-@pytest.mark.parametrize("name", ["aggregate_g2.json", "aggregate_g1.json", "aggregate_g2_t67.json"])
+@pytest.mark.parametrize("name", ["aggregate_g2.json", "aggregate_g1.json", "aggregate_g2_t67.json",
+                                  "aggregate_g2_t67_subsets.json", "aggregate_g1_t67_subsets.json"])
 def test_c_oracle_matches_golden_aggregate(oc, name):
     d = golden(name)
     mode = 0 if d["mode"] == "G2" else 1

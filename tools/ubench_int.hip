@@ -96,6 +96,23 @@ __global__ void k_add(uint64_t* out, uint32_t seed) {
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// plain-C multiply-add chains, as the field code writes them (c + (u64)a * b): the compiler's own
+// v_mad_u64_u32 with a dead carry-out, no asm hazard padding.  NC independent chains per lane.
+template <int NC>
+__global__ void k_mad64_c(uint64_t* out, uint32_t seed) {
+    uint32_t a = threadIdx.x * 2654435761u + seed;
+    uint64_t acc[NC];
+    uint32_t b[NC];
+    for (int c = 0; c < NC; c++) { acc[c] = a + c; b[c] = a ^ (c * 0x9e3779b9u); }
+    for (int it = 0; it < ITERS * CHAINS / NC; it++) {
+#pragma unroll
+        for (int c = 0; c < NC; c++) acc[c] = acc[c] + (uint64_t)b[c] * (uint32_t)acc[c];
+    }
+    uint64_t s = 0;
+    for (int c = 0; c < NC; c++) s ^= acc[c];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 // dependent chain latency: one chain only
 __global__ void k_mad64_lat(uint64_t* out, uint32_t seed) {
     uint32_t b = threadIdx.x * 2654435761u + seed;
@@ -136,7 +153,9 @@ int main() {
     hipMalloc(&d, sizeof(uint64_t) * 4096 * 1024);
     struct { const char* name; kfn k; int ipc; } ks[] = {
         {"v_mad_u64_u32", k_mad64, 1}, {"v_mul_lo_u32", k_mullo, 1}, {"v_mul_hi_u32", k_mulhi, 1},
-        {"v_add_co+v_addc_co", k_addco, 2}, {"v_add_u32", k_add, 1}, {"v_fma_f64", k_fma64, 1}, {"v_mad_u64_u32_latency_1chain", k_mad64_lat, 1}};
+        {"v_add_co+v_addc_co", k_addco, 2}, {"v_add_u32", k_add, 1}, {"v_fma_f64", k_fma64, 1}, {"v_mad_u64_u32_latency_1chain", k_mad64_lat, 1},
+        {"v_mad_u64_u32_plainC_2chains", k_mad64_c<2>, 1}, {"v_mad_u64_u32_plainC_4chains", k_mad64_c<4>, 1},
+        {"v_mad_u64_u32_plainC_8chains", k_mad64_c<8>, 1}, {"v_mad_u64_u32_plainC_16chains", k_mad64_c<16>, 1}};
     for (auto& e : ks) {
         for (int wps = 1; wps <= 8; wps *= 2) {
             int threads = 256;  // 4 waves per block -> one per SIMD
