@@ -1,0 +1,329 @@
+"""bench.py modes for BASELINE configs 4 and 5 (imported by bench.py; also the synthetic-data
+generators of the GPU property tests).
+
+config 4 (--mode aggregate): Threshold aggregation at scale — per credential one
+  Signature::aggregate (signature.rs:448-470) over the partial signatures of a seeded random
+  67-subset of n = 100 issuers, and one Verkey::aggregate (signature.rs:483-526) of the same
+  subset's verkeys from the resident issuer table (cc_set_issuers).  10,000 credentials per GPU.
+config 5 (--mode pok): PoKOfSignatureProof::verify (ps_sig [EXT], reference pok_sig.rs:103-105),
+  q = 32, revealed {3,5,7,11,13,17,19,23}, 65,536 proofs per GPU; 1/16 with a corrupted response.
+
+All group elements are k*G for known scalars k, produced by the product's GPU fixed-base
+multiplication; expected outputs are known by construction and checked after the timed region.
+"""
+import ctypes
+import json
+import os
+import time
+
+import numpy as np
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+REVEALED = [3, 5, 7, 11, 13, 17, 19, 23]
+
+
+def _fr(rng):
+    return int.from_bytes(rng.bytes(32), "big") % R
+
+
+def _be(v):
+    return int(v % R).to_bytes(48, "big")
+
+
+def _poly(c, x):
+    acc = 0
+    for a in reversed(c):
+        acc = (acc * x + a) % R
+    return acc
+
+
+def make_aggregate_batch(ctx, mode, n, t=67, n_iss=100, q=6, seed=4):
+    """Shamir-shared issuer keys (degree t-1) so any t-subset aggregates to the master key:
+    X~ = x g~, Y~_j = y_j g~ exactly (the reference's check_key_aggregation, signature.rs:554-559)."""
+    import coconut
+    rng = np.random.default_rng(seed)
+    og, sg = (1, 2) if mode == 0 else (2, 1)
+    gen = {1: coconut.G1_GENERATOR, 2: coconut.G2_GENERATOR}
+    ob, sb = (97, 192) if mode == 0 else (192, 97)
+    fx = [_fr(rng) for _ in range(t)]
+    fy = [[_fr(rng) for _ in range(t)] for _ in range(q)]
+    gk = _fr(rng) or 1
+    iss = np.arange(1, n_iss + 1, dtype=np.uint64)
+    xk = [_poly(fx, int(i)) for i in iss]
+    yk = [[_poly(fy[j], int(i)) for j in range(q)] for i in iss]
+    sc = b"".join(_be(xk[k] * gk) + b"".join(_be(yk[k][j] * gk) for j in range(q)) for k in range(n_iss))
+    keys = coconut.fixed_base_mul(ctx, og, gen[og], sc)
+    X = b"".join(keys[(k * (q + 1)) * ob:(k * (q + 1) + 1) * ob] for k in range(n_iss))
+    Y = b"".join(keys[(k * (q + 1) + 1) * ob:(k * (q + 1) + 1 + q) * ob] for k in range(n_iss))
+    master = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(_be(v * gk) for v in [fx[0]] + [fy[j][0] for j in range(q)]))
+    ids = np.empty((n, t), dtype=np.uint64)
+    hk, e2, exp2 = [], [], []
+    for i in range(n):
+        sub = rng.choice(n_iss, size=t, replace=False)
+        ids[i] = iss[sub]
+        m = [_fr(rng) for _ in range(q)]
+        k = _fr(rng) or 1
+        hk.append(k)
+        for s_ in sub:
+            e2.append(_be(k * (xk[s_] + sum(yk[s_][j] * m[j] for j in range(q)))))
+        exp2.append(_be(k * (fx[0] + sum(fy[j][0] * m[j] for j in range(q)))))
+    s1one = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(_be(k) for k in hk))
+    s1 = b"".join(s1one[i * sb:(i + 1) * sb] * t for i in range(n))  # every entry carries sigma_1 = h
+    s2 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e2))
+    want_s2 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(exp2))
+    return dict(mode=mode, n=n, t=t, q=q, iss=iss, X=X, Y=Y, ids=ids, s1=s1, s2=s2, want_s1=s1one,
+                want_s2=want_s2, want_X=master[:ob], want_Y=master[ob:], ob=ob, sb=sb)
+
+
+def make_pok_batch(ctx, mode, n, q=32, revealed=REVEALED, seed=5, bad_every=16):
+    """ps_sig PoK proofs with known discrete logs (oracle/coconut_ref.py pok_init / gen_proof):
+    sigma' = (r1 h, r1 (sigma_2 + r2 h)), J = (r2 + sum_hidden y_i m_i) g~, T = (b_0 + sum y_i b_i) g~,
+    responses b_i - chal * secret_i."""
+    import coconut
+    rng = np.random.default_rng(seed)
+    og, sg = (1, 2) if mode == 0 else (2, 1)
+    gen = {1: coconut.G1_GENERATOR, 2: coconut.G2_GENERATOR}
+    x = _fr(rng)
+    y = [_fr(rng) for _ in range(q)]
+    gk = _fr(rng) or 1
+    ob = 97 if og == 1 else 192
+    vk = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(_be(v * gk) for v in [x] + y + [1]))
+    X, Y, g_tilde = vk[:ob], vk[ob:ob * (q + 1)], vk[ob * (q + 1):]
+    hidden = [i for i in range(q) if i not in revealed]
+    s1s, s2s, js, ts, resp, chal, rev = [], [], [], [], [], [], []
+    expect = np.ones(n, dtype=np.uint8)
+    for p in range(n):
+        m = [_fr(rng) for _ in range(q)]
+        k, r1, r2, c = _fr(rng) or 1, _fr(rng) or 1, _fr(rng), _fr(rng)
+        s = (x + sum(y[i] * m[i] for i in range(q))) % R
+        s1s.append(_be(k * r1))
+        s2s.append(_be(r1 * k * (s + r2)))
+        secrets = [r2] + [m[i] for i in hidden]
+        ylog = [1] + [y[i] for i in hidden]
+        bl = [_fr(rng) for _ in secrets]
+        js.append(_be(gk * sum(a * b for a, b in zip(ylog, secrets))))
+        ts.append(_be(gk * sum(a * b for a, b in zip(ylog, bl))))
+        rs = [(b - c * sc) % R for b, sc in zip(bl, secrets)]
+        if bad_every and p % bad_every == bad_every - 1:
+            rs[-1] = (rs[-1] + 5) % R
+            expect[p] = 0
+        resp.append(b"".join(_be(v) for v in rs))
+        chal.append(_be(c))
+        rev.append(b"".join(_be(m[i]) for i in revealed))
+    S1 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(s1s))
+    S2 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(s2s))
+    J = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(js))
+    T = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(ts))
+    return dict(mode=mode, n=n, q=q, revealed=list(revealed), X=X, Y=Y, g_tilde=g_tilde, s1=S1, s2=S2, J=J, T=T,
+                resp=b"".join(resp), chal=b"".join(chal), rev=b"".join(rev), nresp=len(hidden) + 1, expect=expect)
+
+
+def _timed(args, step, dev, dist, ctx):
+    import torch
+    from bench import _max_over_ranks
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ctx.timing(True)
+    phase = np.zeros(3)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        phase += np.array(ctx.last_timing())
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ctx.timing(False)
+    return _max_over_ranks(el, dist, dev), phase / max(args.steps, 1)
+
+
+def bench_aggregate(args):
+    import torch
+    import coconut
+    from bench import _dist_setup, to_dev, MADS_PER_M, peak_mad_per_s, opcounts
+    world, rank, local, dist = _dist_setup()
+    dev = torch.device("cuda", local)
+    n = args.n or 10000
+    ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
+    t_set = time.perf_counter()
+    b = make_aggregate_batch(ctx, 0, n, seed=4000 + rank)
+    gen_s = time.perf_counter() - t_set
+    t_iss = time.perf_counter()
+    ctx.set_issuers(b["iss"], b["X"], b["Y"], b["q"])
+    iss_ms = (time.perf_counter() - t_iss) * 1e3
+    t, q, sb, ob = b["t"], b["q"], b["sb"], b["ob"]
+    d_ids = torch.from_numpy(b["ids"].view(np.int64).copy()).to(dev)
+    d_s1, d_s2 = to_dev(b["s1"], dev), to_dev(b["s2"], dev)
+    o1 = torch.zeros(n * sb, dtype=torch.uint8, device=dev)
+    o2 = torch.zeros(n * sb, dtype=torch.uint8, device=dev)
+    oX = torch.zeros(n * ob, dtype=torch.uint8, device=dev)
+    oY = torch.zeros(n * q * ob, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(dev)
+    stream.wait_stream(torch.cuda.current_stream(dev))
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    lib = coconut._lib.lib
+    P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    phases = {"sig": np.zeros(3), "vk": np.zeros(3)}
+
+    def step():
+        st = lib.cc_signature_aggregate_batch_device(ctx.h, n, t, t, P(d_ids), P(d_s1), P(d_s2), P(o1), P(o2), sh)
+        if ctx._timing:
+            phases["sig"] += np.array(ctx.last_timing())
+        st |= lib.cc_verkey_aggregate_ids_device(ctx.h, n, t, t, P(d_ids), P(oX), P(oY), sh)
+        if ctx._timing:
+            phases["vk"] += np.array(ctx.last_timing())
+        if st:
+            raise RuntimeError(f"aggregate: {lib.cc_status_str(st).decode()}")
+
+    el, _ = _timed(args, step, dev, dist, ctx)
+    torch.cuda.synchronize(dev)
+    ok = (bytes(o2.cpu().numpy()) == b["want_s2"] and bytes(o1.cpu().numpy()) == b["want_s1"]
+          and bytes(oX.cpu().numpy()) == b["want_X"] * n and bytes(oY.cpu().numpy()) == b["want_Y"] * n)
+    if not ok:
+        raise SystemExit("aggregation outputs disagree with construction — refusing to report a number")
+    value = n * world * args.steps / el
+    if rank == 0:
+        peak = peak_mad_per_s()
+        sig_ms = phases["sig"][1] / args.steps
+        vk_ms = phases["vk"][1] / args.steps
+        counts = opcounts("aggregate_sigg2_t67")
+        k_sig = counts["straus_sigma2"] * MADS_PER_M * n / (sig_ms * 1e-3)
+        k_vk = counts["fixed_verkey"] * MADS_PER_M * n / (vk_ms * 1e-3)
+        dom, ach = ("signature_msm", k_sig) if sig_ms >= vk_ms else ("verkey_msm", k_vk)
+        out = {
+            "metric": "aggregated credentials/sec (Signature::aggregate + Verkey::aggregate, t=67 of n=100)",
+            "value": round(value, 1), "unit": "credentials/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 12x32-bit Montgomery limbs, integer-only)",
+            "data": "synthetic (seeded Shamir-shared issuer keys; random 67-subsets; outputs checked = x g~, y_j g~, "
+                    "(x + sum y m) h)",
+            "config": {"workload": f"config4: {n:,} credentials per GPU, t=67 of n=100 issuers, msg_count={q}, SigG2",
+                       "credentials_per_gpu": n, "threshold": t, "issuers": 100,
+                       "parallelism": f"shard-by-credential x{world}"},
+            "roofline": {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 3),
+                         "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
+                         "frac": round(ach / peak, 4), "traffic": None},
+            "kernels": {"lagrange_ms": round((phases["sig"][0]) / args.steps, 3),
+                        "signature_msm_ms": round(sig_ms, 3), "verkey_msm_ms": round(vk_ms, 3),
+                        "signature_msm_frac": round(k_sig / peak, 4), "verkey_msm_frac": round(k_vk / peak, 4)},
+            "setup": {"issuer_tables_ms": round(iss_ms, 1), "synthetic_data_s": round(gen_s, 2)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_aggregate(b)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def cpu_aggregate(b, k=6):
+    """oracle/c oc_signature_aggregate + oc_verkey_aggregate on one thread over k credentials."""
+    from bench import _oracle, cpu_info
+    oc = _oracle()
+    t, q, sb, ob = b["t"], b["q"], b["sb"], b["ob"]
+    o1 = ctypes.create_string_buffer(sb)
+    o2 = ctypes.create_string_buffer(sb)
+    oX = ctypes.create_string_buffer(ob)
+    oY = ctypes.create_string_buffer(ob * q)
+    t0 = time.perf_counter()
+    for i in range(k):
+        ids = np.ascontiguousarray(b["ids"][i])
+        oc.oc_signature_aggregate(b["mode"], ctypes.c_size_t(t), ctypes.c_size_t(t), ids.ctypes.data_as(ctypes.c_void_p),
+                                  b["s1"][i * t * sb:(i + 1) * t * sb], b["s2"][i * t * sb:(i + 1) * t * sb], o1, o2)
+        rows = [int(v) - 1 for v in ids]
+        Xs = b"".join(b["X"][r * ob:(r + 1) * ob] for r in rows)
+        Ys = b"".join(b["Y"][r * q * ob:(r + 1) * q * ob] for r in rows)
+        oc.oc_verkey_aggregate(b["mode"], ctypes.c_size_t(t), ctypes.c_size_t(t), ctypes.c_size_t(q),
+                               ids.ctypes.data_as(ctypes.c_void_p), Xs, Ys, oX, oY)
+    dt = time.perf_counter() - t0
+    model, nproc, _ = cpu_info()
+    return {"value": round(k / dt, 2), "unit": "credentials/s", "cores": 1, "kind": "port",
+            "sample": f"{k} credentials of the timed batch on 1 thread in {dt:.2f} s (oracle/c "
+                      f"oc_signature_aggregate + oc_verkey_aggregate, test infrastructure); last outputs equal the "
+                      f"construction: {o2.raw == b['want_s2'][(k - 1) * sb:k * sb] and oX.raw == b['want_X']}",
+            "nproc": nproc, "cpu_model": model}
+
+
+def bench_pok(args):
+    import torch
+    import coconut
+    from bench import _dist_setup, to_dev, MADS_PER_M, peak_mad_per_s, opcounts
+    world, rank, local, dist = _dist_setup()
+    dev = torch.device("cuda", local)
+    n = args.n or 65536
+    ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
+    t0 = time.perf_counter()
+    b = make_pok_batch(ctx, 0, n, seed=5000 + rank)
+    gen_s = time.perf_counter() - t0
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    q, r, nresp = b["q"], len(b["revealed"]), b["nresp"]
+    D = {k: to_dev(b[k], dev) for k in ("s1", "s2", "J", "T", "resp", "chal", "rev")}
+    d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    ridx = (ctypes.c_uint64 * r)(*b["revealed"])
+    stream = torch.cuda.Stream(dev)
+    stream.wait_stream(torch.cuda.current_stream(dev))
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    lib = coconut._lib.lib
+    P = lambda k: ctypes.c_void_p(D[k].data_ptr())  # noqa: E731
+
+    def step():
+        st = lib.cc_pok_verify_batch_device(ctx.h, n, q, r, nresp, P("s1"), P("s2"), P("J"), P("T"), P("resp"),
+                                            P("chal"), ridx, P("rev"), ctypes.c_void_p(d_v.data_ptr()), None, sh)
+        if st:
+            raise RuntimeError(f"cc_pok_verify_batch_device: {lib.cc_status_str(st).decode()}")
+
+    el, phase_ms = _timed(args, step, dev, dist, ctx)
+    if not np.array_equal(d_v.cpu().numpy(), b["expect"]):
+        raise SystemExit("PoK verdicts disagree with construction — refusing to report a number")
+    value = n * world * args.steps / el
+    if rank == 0:
+        from bench import kernel_table, cpu_info
+        peak = peak_mad_per_s()
+        counts = opcounts("pok_sigg2_q32_r8")
+        kt = kernel_table(phase_ms, n, counts, 2 * 192 + 2 * 97 + (nresp + 1 + r) * 48, peak)
+        dom = max(kt, key=lambda k: kt[k]["ms"])
+        out = {
+            "metric": "verified PoK-of-signature proofs/sec (msg_count=32, 8 revealed)",
+            "value": round(value, 1), "unit": "proofs/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 12x32-bit Montgomery limbs, integer-only)",
+            "data": "synthetic (seeded; proofs with known discrete logs built on the GPU; 1/16 bad response)",
+            "config": {"workload": f"config5: {n:,} PoKOfSignatureProof::verify per GPU, q=32, revealed "
+                                   f"{b['revealed']}, SigG2", "proofs_per_gpu": n,
+                       "parallelism": f"shard-by-proof x{world}"},
+            "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
+                         "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
+                         "frac": kt[dom]["frac"], "traffic": None},
+            "kernels": kt,
+            "setup": {"synthetic_data_s": round(gen_s, 2)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            oc = __import__("bench")._oracle()
+            k = 24
+            ver = []
+            tt = time.perf_counter()
+            gtb = ctypes.create_string_buffer(576)
+            for p in range(k):
+                v = oc.oc_pok_verify(0, ctypes.c_size_t(q), ctypes.c_size_t(r), b["s1"][p * 192:(p + 1) * 192],
+                                     b["s2"][p * 192:(p + 1) * 192], b["J"][p * 97:(p + 1) * 97],
+                                     b["T"][p * 97:(p + 1) * 97], b["resp"][p * nresp * 48:(p + 1) * nresp * 48],
+                                     ctypes.c_size_t(nresp), b["chal"][p * 48:(p + 1) * 48],
+                                     (ctypes.c_uint64 * r)(*b["revealed"]), b["rev"][p * r * 48:(p + 1) * r * 48],
+                                     b["X"], b["Y"], b["g_tilde"], gtb)
+                ver.append(v)
+            dt = time.perf_counter() - tt
+            model, nproc, _ = cpu_info()
+            out["cpu_baseline"] = {"value": round(k / dt, 2), "unit": "proofs/s", "cores": 1, "kind": "port",
+                                   "sample": f"{k} proofs of the timed batch on 1 thread in {dt:.2f} s (oracle/c "
+                                             f"oc_pok_verify); verdicts agree with construction: "
+                                             f"{list(ver) == list(b['expect'][:k])}",
+                                   "nproc": nproc, "cpu_model": model}
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()

@@ -140,6 +140,8 @@ class Context:
         self.h = h
         self._gtilde = None
         self._vk = None
+        self._timing = False
+        self._iss_q = 0
 
     @classmethod
     def default(cls, device: int = 0, mode: GroupMode = GroupMode.SIG_G2) -> "Context":
@@ -177,6 +179,15 @@ class Context:
         check(lib.cc_set_verkey(self.h, px, py, q), "cc_set_verkey")
         self._vk = key
 
+    def set_issuers(self, ids, X: bytes, Y: bytes, q: int):
+        """Issuer verkey table (cc_set_issuers): ids[k] is issuer k's signer id, X n x OtherGroup,
+        Y n x q x OtherGroup; then verkey_aggregate_ids takes id lists only."""
+        ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64))
+        px, k1 = buf(X)
+        py, k2 = buf(Y)
+        check(lib.cc_set_issuers(self.h, len(ids), q, ctypes.c_void_p(ids.ctypes.data), px, py), "cc_set_issuers")
+        self._iss_q = q
+
     def num_devices(self) -> int:
         n = ctypes.c_int()
         check(lib.cc_ctx_num_devices(self.h, ctypes.byref(n)), "cc_ctx_num_devices")
@@ -184,6 +195,7 @@ class Context:
 
     def timing(self, enabled: bool = True):
         check(lib.cc_set_timing(self.h, int(enabled)))
+        self._timing = bool(enabled)
 
     def last_timing(self):
         a, b, c = ctypes.c_float(), ctypes.c_float(), ctypes.c_float()
@@ -239,6 +251,18 @@ def verkey_aggregate_batch(ctx: Context, n: int, length: int, t: int, q: int, id
     check(lib.cc_verkey_aggregate_batch(ctx.h, n, length, t, q, ctypes.c_void_p(ids.ctypes.data), px, py,
                                         ctypes.c_void_p(oX.ctypes.data), ctypes.c_void_p(oY.ctypes.data)),
           "cc_verkey_aggregate_batch")
+    return oX[:n * ob].tobytes(), oY[:n * q * ob].tobytes()
+
+
+def verkey_aggregate_ids(ctx: Context, n: int, length: int, t: int, ids):
+    """Verkey::aggregate for n credentials from the issuer table (cc_verkey_aggregate_ids)."""
+    ob, q = ctx.mode.other_bytes, ctx._iss_q
+    ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64).reshape(n, length))
+    oX = np.zeros(max(n, 1) * ob, dtype=np.uint8)
+    oY = np.zeros(max(n * q, 1) * ob, dtype=np.uint8)
+    check(lib.cc_verkey_aggregate_ids(ctx.h, n, length, t, ctypes.c_void_p(ids.ctypes.data),
+                                      ctypes.c_void_p(oX.ctypes.data), ctypes.c_void_p(oY.ctypes.data)),
+          "cc_verkey_aggregate_ids")
     return oX[:n * ob].tobytes(), oY[:n * q * ob].tobytes()
 
 

@@ -147,6 +147,188 @@ __global__ __launch_bounds__(256) void k_msm_tasks(size_t ntask, size_t t, const
     encode_pt<F>(out + task * ebytes<F>(), r, fin);
 }
 
+// ================================================================ windowed Straus MSM (variable bases)
+// One Lagrange-weighted MSM per lane with signed 4-bit windows: per base the multiples 1P..8P are
+// built in Jacobian form, batch-normalised to affine with ONE inversion per task (Montgomery's
+// trick over all 8t entries), then 65 windows x (4 doublings + t mixed additions).  For t = 67 in G2
+// that is ~147k Fp multiplications per task against ~253k for the bitwise double-and-add it
+// replaces.  Identity bases (AMCL decodes an off-curve point to infinity) and identity multiples of
+// small-order points are flagged and skipped, so every input gives the reference's group element.
+// Scratch per task (AoS, contiguous): 8t Jacobian entries (3*FS*12 words, affine x,y written back in
+// place, word 2*FS*12 = infinity flag), 8t prefix products (FS*12 words), 65t digit bytes.
+template <class F>
+__host__ __device__ inline size_t straus_words(size_t t) {
+    constexpr int FS = sizeof(F) / sizeof(Fp);
+    return t * 8 * (3 * FS * NL) + t * 8 * (FS * NL) + (t * 65 + 3) / 4;
+}
+
+// signed radix-16 digits of a canonical 255-bit scalar: 65 digits in [-8, 8], least significant first
+DEV void recode_w4(int8_t* d, const uint32_t k[8]) {
+    int carry = 0;
+#pragma unroll 1
+    for (int w = 0; w < 64; w++) {
+        int v = (int)((k[w >> 3] >> (4 * (w & 7))) & 0xfu) + carry;
+        carry = v > 8;
+        d[w] = (int8_t)(v - 16 * carry);
+    }
+    d[64] = (int8_t)carry;
+}
+
+template <class F>
+__global__ __launch_bounds__(64) void k_msm_straus(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
+                                                   size_t pt_stride, size_t pt_jstride, size_t pt_step,
+                                                   const uint32_t* __restrict__ l, size_t l_div,
+                                                   uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
+    const size_t task = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (task >= ntask) return;
+    using T = FT<F>;
+    constexpr int FS = sizeof(F) / sizeof(Fp);
+    constexpr int JW = 3 * FS * NL, PW = FS * NL;
+    const size_t cred = task / l_div;
+    const uint8_t* base = pts + cred * pt_stride + (task % l_div) * pt_jstride;
+    const uint32_t* lk = l + cred * t * 8;
+    uint32_t* ent = scratch + task * straus_words<F>(t);
+    uint32_t* pre = ent + t * 8 * JW;
+    int8_t* dig = reinterpret_cast<int8_t*>(pre + t * 8 * PW);
+    const size_t m = t * 8;
+    // multiples 1P..8P (Jacobian) and the running product of their Z coordinates
+    F acc_z;
+    T::one(acc_z);
+#pragma unroll 1
+    for (size_t k = 0; k < t; k++) {
+        Aff<F> P;
+        const bool ok = decode_pt<F>(P, base + k * pt_step);
+        recode_w4(dig + k * 65, lk + k * 8);
+        Jac<F> J;
+        if (ok) {
+            jac_from_aff(J, P);
+        } else {
+            jac_set_inf(J);
+        }
+#pragma unroll 1
+        for (int d = 0; d < 8; d++) {
+            if (d == 1) {
+                jac_dbl(J, J);
+            } else if (d > 1) {
+                if (ok) jac_add_aff(J, J, P);
+            }
+            const size_t e = k * 8 + d;
+            uint32_t* w = ent + e * JW;
+            const uint32_t* jw = reinterpret_cast<const uint32_t*>(&J);
+            for (int c = 0; c < JW; c++) w[c] = jw[c];
+            const uint32_t* zw = reinterpret_cast<const uint32_t*>(&acc_z);
+            for (int c = 0; c < PW; c++) pre[e * PW + c] = zw[c];
+            if (!jac_is_inf(J)) T::mul(acc_z, acc_z, J.z);
+        }
+    }
+    // one inversion, then walk back: z_e^-1 = inv * prefix_e; inv *= z_e
+    F inv;
+    T::inv(inv, acc_z);
+#pragma unroll 1
+    for (size_t e = m; e-- > 0;) {
+        Jac<F> J;
+        uint32_t* w = ent + e * JW;
+        uint32_t* jw = reinterpret_cast<uint32_t*>(&J);
+        for (int c = 0; c < JW; c++) jw[c] = w[c];
+        const bool inf = jac_is_inf(J);
+        if (!inf) {
+            F pz, zi, zi2;
+            uint32_t* pw = reinterpret_cast<uint32_t*>(&pz);
+            for (int c = 0; c < PW; c++) pw[c] = pre[e * PW + c];
+            T::mul(zi, inv, pz);
+            T::mul(inv, inv, J.z);
+            T::sqr(zi2, zi);
+            T::mul(J.x, J.x, zi2);
+            T::mul(zi2, zi2, zi);
+            T::mul(J.y, J.y, zi2);
+        }
+        for (int c = 0; c < 2 * PW; c++) w[c] = jw[c];  // affine x, y
+        w[2 * PW] = inf ? 1u : 0u;
+    }
+    // 65 signed windows, most significant first
+    Jac<F> acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (int win = 64; win >= 0; win--) {
+        if (win != 64 && !jac_is_inf(acc))
+            for (int z = 0; z < 4; z++) jac_dbl(acc, acc);
+#pragma unroll 1
+        for (size_t k = 0; k < t; k++) {
+            const int d = dig[k * 65 + win];
+            if (!d) continue;
+            const uint32_t* w = ent + (k * 8 + (d < 0 ? -d : d) - 1) * JW;
+            if (w[2 * PW]) continue;  // identity multiple
+            Aff<F> e;
+            uint32_t* ew = reinterpret_cast<uint32_t*>(&e);
+            for (int c = 0; c < 2 * PW; c++) ew[c] = w[c];
+            if (d < 0) T::neg(e.y, e.y);
+            jac_add_aff(acc, acc, e);
+        }
+    }
+    Aff<F> r;
+    bool fin = jac_to_aff(r, acc);
+    encode_pt<F>(out + task * ebytes<F>(), r, fin);
+}
+
+// ================================================================ issuer-table Verkey::aggregate
+// Verkey::aggregate (signature.rs:483-526) over a resident issuer table: the bases X~_k, Y~_k,j of
+// the n_iss issuers are FIXED, so cc_set_issuers gives each one an 8-bit window table (32 x 255
+// affine multiples, the layout of the shared-verkey tables) and every Lagrange-weighted MSM is a
+// fixed-base sum: t x 32 mixed additions, no doublings.  Task = (credential, j): j = 0 -> X~,
+// j = 1..q -> Y~_{j-1}.  Issuer ids are sorted; each entry's id is found by binary search (the
+// host entry point has checked they all exist).  Table entries that are the identity (possible only
+// for small-order bases) are stored as (0, 0), which is on neither curve, and skipped.
+template <class F>
+DEV bool aff_is_zero_pair(const Aff<F>& a) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
+    uint32_t o = 0;
+    for (int c = 0; c < (int)(sizeof(Aff<F>) / 4); c++) o |= w[c];
+    return o == 0;
+}
+
+template <class F>
+__global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size_t t, int q,
+                                                      const uint64_t* __restrict__ ids,
+                                                      const uint32_t* __restrict__ l,
+                                                      const uint64_t* __restrict__ iss_ids, int n_iss,
+                                                      const uint32_t* __restrict__ table,
+                                                      const uint32_t* __restrict__ binf,
+                                                      uint8_t* __restrict__ outX, uint8_t* __restrict__ outY) {
+    const size_t task = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (task >= n * (size_t)(q + 1)) return;
+    const size_t cred = task / (q + 1);
+    const int j = (int)(task % (q + 1));
+    constexpr int EW = sizeof(Aff<F>) / 4;
+    Jac<F> acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (size_t k = 0; k < t; k++) {
+        const uint64_t id = ids[cred * len + k];
+        int lo = 0, hi = n_iss;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (iss_ids[mid] < id) lo = mid + 1; else hi = mid;
+        }
+        const int b = lo * (q + 1) + j;
+        if (binf[b]) continue;
+        const uint32_t* kv = l + (cred * t + k) * 8;
+        const uint32_t* tb = table + (size_t)b * NWIN * WENT * EW;
+#pragma unroll 1
+        for (int w = 0; w < NWIN; w++) {
+            const uint32_t d = (kv[w >> 2] >> (8 * (w & 3))) & 0xffu;
+            if (!d) continue;
+            Aff<F> e;
+            ld_aff_aos<F>(e, tb + ((size_t)w * WENT + d - 1) * EW);
+            if (aff_is_zero_pair(e)) continue;
+            jac_add_aff(acc, acc, e);
+        }
+    }
+    Aff<F> r;
+    const bool fin = jac_to_aff(r, acc);
+    uint8_t* o = j == 0 ? outX + cred * ebytes<F>() : outY + (cred * q + (j - 1)) * ebytes<F>();
+    encode_pt<F>(o, r, fin);
+}
+
 // ================================================================ PoK verify prep
 // Prep layout and flag bits as kernels.hip (Q1 0..3 | Q2 4..7 | P1 8..10 | P2 11..12),
 // plus flag bit3 = Schnorr check failed.
@@ -303,6 +485,37 @@ int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_
     else
         hipLaunchKernelGGL(k_msm_tasks<Fp2>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
                            d_scratch, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+size_t cck_straus_words(int group, size_t t) { return group == 1 ? straus_words<Fp>(t) : straus_words<Fp2>(t); }
+
+int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
+                   size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
+                   hipStream_t st) {
+    if (!ntask) return 0;
+    dim3 g(nblocks(ntask, 64)), b(64);
+    if (group == 1)
+        hipLaunchKernelGGL(k_msm_straus<Fp>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
+                           d_scratch, d_out);
+    else
+        hipLaunchKernelGGL(k_msm_straus<Fp2>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
+                           d_scratch, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uint64_t* d_ids, const uint32_t* d_l,
+                     const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, const uint32_t* d_binf,
+                     uint8_t* d_outX, uint8_t* d_outY, hipStream_t st) {
+    if (!n) return 0;
+    const size_t ntask = n * (size_t)(q + 1);
+    dim3 g(nblocks(ntask, 256)), b(256);
+    if (group == 1)
+        hipLaunchKernelGGL(k_vk_agg_fixed<Fp>, g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table, d_binf,
+                           d_outX, d_outY);
+    else
+        hipLaunchKernelGGL(k_vk_agg_fixed<Fp2>, g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
+                           d_binf, d_outX, d_outY);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -9,6 +9,7 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <thread>
 #include <vector>
 
@@ -34,6 +35,13 @@ int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t
 int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
                   size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
                   hipStream_t st);
+size_t cck_straus_words(int group, size_t t);
+int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
+                   size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
+                   hipStream_t st);
+int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uint64_t* d_ids, const uint32_t* d_l,
+                     const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, const uint32_t* d_binf,
+                     uint8_t* d_outX, uint8_t* d_outY, hipStream_t st);
 int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
                   uint8_t* d_out, hipStream_t st);
 int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
@@ -100,6 +108,12 @@ struct cc_ctx {
     DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, vkbinf, msgs_canon, lag;
     // RLC batch mode: ChaCha20 key, identity flag word, partial / gathered partials, verdict
     DevBuf rlc_key, rlc_any, rlc_part, rlc_flag, rlc_accept;
+    DevBuf pok_idx;  // revealed indices of the last PoK batch
+    // issuer table (cc_set_issuers): sorted ids, decoded verkeys, per-base 8-bit window tables
+    size_t iss_n = 0, iss_q = 0;
+    std::vector<uint64_t> iss_ids_host;
+    DevBuf iss_ids, iss_aff, iss_inf, iss_table;
+    DevBuf agg_scratch;
     uint32_t rlc_key_host[8] = {0};
     // timing
     bool timing = false;
@@ -219,7 +233,8 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag,
-                      &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept};
+                      &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->pok_idx, &c->rlc_gath,
+                      &c->iss_ids, &c->iss_aff, &c->iss_inf, &c->iss_table, &c->agg_scratch};
     for (auto* b : bufs) b->release();
     for (auto& b : c->in_aux) b.release();
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -565,6 +580,46 @@ cc_status cc_fixed_base_mul(cc_ctx* c, int group, const uint8_t* base, size_t n,
     return CC_OK;
 }
 
+// Lagrange-weighted MSMs: windowed Straus over variable bases (aggregate.hip k_msm_straus)
+static cc_status agg_scratch(cc_ctx* c, int group, size_t ntask, size_t t) {
+    return c->agg_scratch.ensure(ntask * cck_straus_words(group, t) * 4 + 64) ? CC_ERR_HIP : CC_OK;
+}
+
+static cc_status launch_sig_aggregate(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* d_ids,
+                                      const uint8_t* d_s1, const uint8_t* d_s2, uint8_t* d_o1, uint8_t* d_o2,
+                                      hipStream_t st) {
+    const size_t sb = (size_t)sig_bytes(c->mode);
+    const int sg = sig_group(c->mode);
+    if (c->lag.ensure(n * t * 32 + 32)) return CC_ERR_HIP;
+    cc_status s = agg_scratch(c, sg, n, t);
+    if (s) return s;
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
+    KCK(cck_lagrange(n, len, t, d_ids, c->lag.as<uint32_t>(), st));
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    KCK(cck_msm_straus(sg, n, t, d_s2, len * sb, 0, sb, c->lag.as<uint32_t>(), 1, c->agg_scratch.as<uint32_t>(), d_o2, st));
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
+    // sigma_1 = sigs[0].sigma_1 (signature.rs:452): strided device copy of entry 0
+    HIPCK(hipMemcpy2DAsync(d_o1, sb, d_s1, len * sb, sb, n, hipMemcpyDeviceToDevice, st));
+    if (c->timing) (void)hipEventRecord(c->ev[3], st);
+    return CC_OK;
+}
+
+cc_status cc_signature_aggregate_batch_device(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* d_ids,
+                                              const uint8_t* d_s1, const uint8_t* d_s2, uint8_t* d_out_s1,
+                                              uint8_t* d_out_s2, void* stream) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || (n && (!d_ids || !d_s1 || !d_s2 || !d_out_s1 || !d_out_s2))) return CC_ERR_DECODE;
+    if (len < t || len == 0) return CC_ERR_THRESHOLD;  // reference: assert!(sigs.len() >= threshold)
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    StreamOrder order(c, st);
+    cc_status s = launch_sig_aggregate(c, n, len, t, d_ids, d_s1, d_s2, d_out_s1, d_out_s2, st);
+    if (s) return s;
+    if (c->timing) collect_timing(c);
+    return CC_OK;
+}
+
 cc_status cc_signature_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* ids,
                                        const uint8_t* s1, const uint8_t* s2, uint8_t* out_s1, uint8_t* out_s2) {
     c = primary(c);  // a device set forwards to its first device
@@ -573,23 +628,24 @@ cc_status cc_signature_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     size_t sb = (size_t)sig_bytes(c->mode);
-    int sg = sig_group(c->mode);
-    size_t fs = sg == 1 ? 1 : 2;
     hipStream_t st = c->stream;
     DevBuf& d_ids = c->in_aux[0];
     DevBuf& d_pts = c->in_aux[1];
     DevBuf& d_out = c->in_aux[2];
-    if (d_ids.ensure(n * len * 8) || d_pts.ensure(n * len * sb) || d_out.ensure(n * sb) ||
-        c->lag.ensure(n * (t ? t : 1) * 32) || c->scratch.ensure(n * (t * 2 * fs * 12 + t + 1) * 4))
+    DevBuf& d_p1 = c->in_aux[3];
+    DevBuf& d_o1 = c->in_aux[4];
+    if (d_ids.ensure(n * len * 8) || d_pts.ensure(n * len * sb) || d_out.ensure(n * sb) || d_p1.ensure(n * len * sb) ||
+        d_o1.ensure(n * sb))
         return CC_ERR_HIP;
     HIPCK(hipMemcpyAsync(d_ids.p, ids, n * len * 8, hipMemcpyHostToDevice, st));
     HIPCK(hipMemcpyAsync(d_pts.p, s2, n * len * sb, hipMemcpyHostToDevice, st));
-    KCK(cck_lagrange(n, len, t, d_ids.as<uint64_t>(), c->lag.as<uint32_t>(), st));
-    KCK(cck_msm_tasks(sg, n, t, d_pts.as<uint8_t>(), len * sb, 0, sb, c->lag.as<uint32_t>(), 1,
-                      c->scratch.as<uint32_t>(), d_out.as<uint8_t>(), st));
+    HIPCK(hipMemcpyAsync(d_p1.p, s1, n * len * sb, hipMemcpyHostToDevice, st));
+    cc_status s = launch_sig_aggregate(c, n, len, t, d_ids.as<uint64_t>(), d_p1.as<uint8_t>(), d_pts.as<uint8_t>(),
+                                       d_o1.as<uint8_t>(), d_out.as<uint8_t>(), st);
+    if (s) return s;
     HIPCK(hipMemcpyAsync(out_s2, d_out.p, n * sb, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(out_s1, d_o1.p, n * sb, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    for (size_t i = 0; i < n; i++) memcpy(out_s1 + i * sb, s1 + i * len * sb, sb);  // sigma_1 = sigs[0].sigma_1
     return CC_OK;
 }
 
@@ -602,7 +658,6 @@ cc_status cc_verkey_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, s
     HIPCK(hipSetDevice(c->device));
     size_t ob = (size_t)oth_bytes(c->mode);
     int og = oth_group(c->mode);
-    size_t fs = og == 1 ? 1 : 2;
     hipStream_t st = c->stream;
     DevBuf& d_ids = c->in_aux[0];
     DevBuf& d_X = c->in_aux[1];
@@ -612,21 +667,185 @@ cc_status cc_verkey_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, s
     size_t ntask_y = n * q;
     size_t maxtask = ntask_y > n ? ntask_y : n;
     if (d_ids.ensure(n * len * 8) || d_X.ensure(n * len * ob) || d_Y.ensure(n * len * q * ob + 16) ||
-        d_oX.ensure(n * ob) || d_oY.ensure(ntask_y * ob + 16) || c->lag.ensure(n * (t ? t : 1) * 32) ||
-        c->scratch.ensure(maxtask * (t * 2 * fs * 12 + t + 1) * 4))
+        d_oX.ensure(n * ob) || d_oY.ensure(ntask_y * ob + 16) || c->lag.ensure(n * t * 32 + 32))
         return CC_ERR_HIP;
+    cc_status s = agg_scratch(c, og, maxtask, t);
+    if (s) return s;
     HIPCK(hipMemcpyAsync(d_ids.p, ids, n * len * 8, hipMemcpyHostToDevice, st));
     HIPCK(hipMemcpyAsync(d_X.p, X, n * len * ob, hipMemcpyHostToDevice, st));
     if (q) HIPCK(hipMemcpyAsync(d_Y.p, Y, n * len * q * ob, hipMemcpyHostToDevice, st));
     KCK(cck_lagrange(n, len, t, d_ids.as<uint64_t>(), c->lag.as<uint32_t>(), st));
-    KCK(cck_msm_tasks(og, n, t, d_X.as<uint8_t>(), len * ob, 0, ob, c->lag.as<uint32_t>(), 1,
-                      c->scratch.as<uint32_t>(), d_oX.as<uint8_t>(), st));
+    KCK(cck_msm_straus(og, n, t, d_X.as<uint8_t>(), len * ob, 0, ob, c->lag.as<uint32_t>(), 1,
+                       c->agg_scratch.as<uint32_t>(), d_oX.as<uint8_t>(), st));
     if (q)
-        KCK(cck_msm_tasks(og, ntask_y, t, d_Y.as<uint8_t>(), len * q * ob, ob, q * ob, c->lag.as<uint32_t>(), q,
-                          c->scratch.as<uint32_t>(), d_oY.as<uint8_t>(), st));
+        KCK(cck_msm_straus(og, ntask_y, t, d_Y.as<uint8_t>(), len * q * ob, ob, q * ob, c->lag.as<uint32_t>(), q,
+                           c->agg_scratch.as<uint32_t>(), d_oY.as<uint8_t>(), st));
     HIPCK(hipMemcpyAsync(outX, d_oX.p, n * ob, hipMemcpyDeviceToHost, st));
     if (q) HIPCK(hipMemcpyAsync(outY, d_oY.p, ntask_y * ob, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    return CC_OK;
+}
+
+// ---------------------------------------------------------------- issuer table (config 4)
+cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids, const uint8_t* X, const uint8_t* Y) {
+    if (!c || !n_iss || !ids || !X || (q && !Y) || n_iss > (1u << 20) || q > 4096) return CC_ERR_DECODE;
+    if (!c->peers.empty()) {
+        for (cc_ctx* p : c->peers) {
+            cc_status s = cc_set_issuers(p, n_iss, q, ids, X, Y);
+            if (s) return s;
+        }
+        return CC_OK;
+    }
+    HIPCK(hipSetDevice(c->device));
+    const int og = oth_group(c->mode);
+    const size_t ob = (size_t)oth_bytes(c->mode), aw = aff_words(og);
+    // rows sorted by id; ids must be unique (they are the signers' Shamir x-coordinates)
+    std::vector<size_t> ord(n_iss);
+    for (size_t k = 0; k < n_iss; k++) ord[k] = k;
+    std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return ids[a] < ids[b]; });
+    for (size_t k = 1; k < n_iss; k++)
+        if (ids[ord[k]] == ids[ord[k - 1]]) return CC_ERR_DECODE;
+    const size_t nb = n_iss * (q + 1);
+    std::vector<uint8_t> enc(nb * ob);
+    std::vector<uint64_t> sid(n_iss);
+    for (size_t r = 0; r < n_iss; r++) {
+        const size_t k = ord[r];
+        sid[r] = ids[k];
+        memcpy(&enc[(r * (q + 1)) * ob], X + k * ob, ob);
+        for (size_t j = 0; j < q; j++) memcpy(&enc[(r * (q + 1) + 1 + j) * ob], Y + (k * q + j) * ob, ob);
+    }
+    if (c->iss_ids.ensure(n_iss * 8) || c->iss_aff.ensure(nb * aw * 4) || c->iss_inf.ensure(nb * 4) ||
+        c->iss_table.ensure(nb * NWIN * WENT * aw * 4))
+        return CC_ERR_HIP;
+    cc_status s = decode_points_host(c, og, nb, enc.data(), c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>());
+    if (s) return s;
+    HIPCK(hipMemcpy(c->iss_ids.p, sid.data(), n_iss * 8, hipMemcpyHostToDevice));
+    DevBuf pw;
+    if (pw.ensure(nb * NWIN * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
+    KCK(cck_build_table(og, (int)nb, c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>(), pw.as<uint32_t>(),
+                        c->iss_table.as<uint32_t>(), c->stream));
+    HIPCK(hipStreamSynchronize(c->stream));
+    pw.release();
+    c->iss_n = n_iss;
+    c->iss_q = q;
+    c->iss_ids_host = sid;
+    return CC_OK;
+}
+
+static cc_status launch_vk_aggregate_ids(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* d_ids,
+                                         uint8_t* d_oX, uint8_t* d_oY, hipStream_t st) {
+    if (c->lag.ensure(n * t * 32 + 32)) return CC_ERR_HIP;
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
+    KCK(cck_lagrange(n, len, t, d_ids, c->lag.as<uint32_t>(), st));
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    KCK(cck_vk_agg_fixed(oth_group(c->mode), n, len, t, (int)c->iss_q, d_ids, c->lag.as<uint32_t>(),
+                         c->iss_ids.as<uint64_t>(), (int)c->iss_n, c->iss_table.as<uint32_t>(), c->iss_inf.as<uint32_t>(),
+                         d_oX, d_oY, st));
+    if (c->timing) {
+        (void)hipEventRecord(c->ev[2], st);
+        (void)hipEventRecord(c->ev[3], st);
+    }
+    return CC_OK;
+}
+
+cc_status cc_verkey_aggregate_ids_device(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* d_ids,
+                                         uint8_t* d_outX, uint8_t* d_outY, void* stream) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || (n && (!d_ids || !d_outX || (c->iss_q && !d_outY)))) return CC_ERR_DECODE;
+    if (!c->iss_n) return CC_ERR_STATE;
+    if (len < t || len == 0) return CC_ERR_THRESHOLD;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    StreamOrder order(c, st);
+    cc_status s = launch_vk_aggregate_ids(c, n, len, t, d_ids, d_outX, d_outY, st);
+    if (s) return s;
+    if (c->timing) collect_timing(c);
+    return CC_OK;
+}
+
+cc_status cc_verkey_aggregate_ids(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* ids, uint8_t* outX,
+                                  uint8_t* outY) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || (n && (!ids || !outX || (c->iss_q && !outY)))) return CC_ERR_DECODE;
+    if (!c->iss_n) return CC_ERR_STATE;
+    if (len < t || len == 0) return CC_ERR_THRESHOLD;
+    if (!n) return CC_OK;
+    for (size_t i = 0; i < n; i++)
+        for (size_t k = 0; k < t; k++)
+            if (!std::binary_search(c->iss_ids_host.begin(), c->iss_ids_host.end(), ids[i * len + k]))
+                return CC_ERR_DECODE;  // id without an issuer verkey (the reference indexes a missing key)
+    HIPCK(hipSetDevice(c->device));
+    const size_t ob = (size_t)oth_bytes(c->mode), q = c->iss_q;
+    hipStream_t st = c->stream;
+    DevBuf& d_ids = c->in_aux[0];
+    DevBuf& d_oX = c->in_aux[2];
+    DevBuf& d_oY = c->in_aux[4];
+    if (d_ids.ensure(n * len * 8) || d_oX.ensure(n * ob) || d_oY.ensure(n * q * ob + 16)) return CC_ERR_HIP;
+    HIPCK(hipMemcpyAsync(d_ids.p, ids, n * len * 8, hipMemcpyHostToDevice, st));
+    cc_status s = launch_vk_aggregate_ids(c, n, len, t, d_ids.as<uint64_t>(), d_oX.as<uint8_t>(), d_oY.as<uint8_t>(), st);
+    if (s) return s;
+    HIPCK(hipMemcpyAsync(outX, d_oX.p, n * ob, hipMemcpyDeviceToHost, st));
+    if (q) HIPCK(hipMemcpyAsync(outY, d_oY.p, n * q * ob, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    return CC_OK;
+}
+
+// revealed indices (shared by the batch): < q and unique (ps_sig's HashMap keys); reference would panic
+static cc_status check_revealed(size_t q, size_t r, const uint64_t* rev_idx, std::vector<uint32_t>& idx) {
+    idx.assign(r ? r : 1, 0);
+    for (size_t z = 0; z < r; z++) {
+        if (rev_idx[z] >= q) return CC_ERR_LEN;  // reference would index out of bounds (panic)
+        for (size_t y = 0; y < z; y++)
+            if (rev_idx[y] == rev_idx[z]) return CC_ERR_DECODE;  // HashMap keys are unique
+        idx[z] = (uint32_t)rev_idx[z];
+    }
+    return CC_OK;
+}
+
+static cc_status launch_pok(cc_ctx* c, size_t n, size_t q, size_t r, const uint8_t* d_s1, const uint8_t* d_s2,
+                            const uint8_t* d_J, const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal,
+                            const uint32_t* d_idx, const uint8_t* d_rev_msgs, uint8_t* d_verdicts, uint8_t* d_gt,
+                            hipStream_t st) {
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
+    KCK(cck_prep_pok(c->mode, n, (int)q, (int)r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_idx,
+                     c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(),
+                     c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
+    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
+    KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(), d_verdicts, d_gt, st));
+    if (c->timing) (void)hipEventRecord(c->ev[3], st);
+    return CC_OK;
+}
+
+cc_status cc_pok_verify_batch_device(cc_ctx* c, size_t n, size_t q, size_t r, size_t nresp, const uint8_t* d_s1,
+                                     const uint8_t* d_s2, const uint8_t* d_J, const uint8_t* d_T,
+                                     const uint8_t* d_resp, const uint8_t* d_chal, const uint64_t* rev_idx,
+                                     const uint8_t* d_rev_msgs, uint8_t* d_verdicts, uint8_t* d_gt, void* stream) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || (n && (!d_s1 || !d_s2 || !d_J || !d_T || !d_chal || !d_verdicts || (nresp && !d_resp) ||
+                     (r && (!rev_idx || !d_rev_msgs)))))
+        return CC_ERR_DECODE;
+    if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
+    if (q != c->q) return CC_ERR_LEN;
+    std::vector<uint32_t> idx;
+    cc_status s = check_revealed(q, r, rev_idx, idx);
+    if (s) return s;
+    if (nresp != q - r + 1) return CC_ERR_BASES_EXPS;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    s = ensure_work(c, n);
+    if (s) return s;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    StreamOrder order(c, st);
+    if (c->pok_idx.ensure(idx.size() * 4)) return CC_ERR_HIP;
+    HIPCK(hipMemcpyAsync(c->pok_idx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, st));
+    s = launch_pok(c, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, c->pok_idx.as<uint32_t>(), d_rev_msgs, d_verdicts,
+                   d_gt, st);
+    if (s) return s;
+    if (c->timing) collect_timing(c);
     return CC_OK;
 }
 
@@ -639,13 +858,9 @@ cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nr
         return CC_ERR_DECODE;
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
     if (q != c->q) return CC_ERR_LEN;
-    std::vector<uint32_t> idx(r ? r : 1);
-    for (size_t z = 0; z < r; z++) {
-        if (rev_idx[z] >= q) return CC_ERR_LEN;  // reference would index out of bounds (panic)
-        for (size_t y = 0; y < z; y++)
-            if (rev_idx[y] == rev_idx[z]) return CC_ERR_DECODE;  // HashMap keys are unique
-        idx[z] = (uint32_t)rev_idx[z];
-    }
+    std::vector<uint32_t> idx;
+    cc_status s = check_revealed(q, r, rev_idx, idx);
+    if (s) return s;
     if (nresp != q - r + 1) return CC_ERR_BASES_EXPS;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
@@ -661,7 +876,7 @@ cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nr
         dR.ensure(n * nresp * 48 + 16) || dC.ensure(n * 48) || dM.ensure(n * r * 48 + 16) || dI.ensure(r * 4 + 4) ||
         c->verdicts.ensure(n) || (gt && c->gt.ensure(n * 576)))
         return CC_ERR_HIP;
-    cc_status s = ensure_work(c, n);
+    s = ensure_work(c, n);
     if (s) return s;
     HIPCK(hipMemcpyAsync(c->in_s1.p, s1, n * sb, hipMemcpyHostToDevice, st));
     HIPCK(hipMemcpyAsync(c->in_s2.p, s2, n * sb, hipMemcpyHostToDevice, st));
@@ -673,17 +888,14 @@ cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nr
         HIPCK(hipMemcpyAsync(dM.p, rev_msgs, n * r * 48, hipMemcpyHostToDevice, st));
         HIPCK(hipMemcpyAsync(dI.p, idx.data(), r * 4, hipMemcpyHostToDevice, st));
     }
-    KCK(cck_prep_pok(c->mode, n, (int)q, (int)r, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), dJ.as<uint8_t>(),
-                     dT.as<uint8_t>(), dR.as<uint8_t>(), dC.as<uint8_t>(), dM.as<uint8_t>(), dI.as<uint32_t>(),
-                     c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(),
-                     c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
-    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
-    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
-    KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(),
-                 c->verdicts.as<uint8_t>(), gt ? c->gt.as<uint8_t>() : nullptr, st));
+    s = launch_pok(c, n, q, r, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), dJ.as<uint8_t>(), dT.as<uint8_t>(),
+                   dR.as<uint8_t>(), dC.as<uint8_t>(), dI.as<uint32_t>(), dM.as<uint8_t>(), c->verdicts.as<uint8_t>(),
+                   gt ? c->gt.as<uint8_t>() : nullptr, st);
+    if (s) return s;
     HIPCK(hipMemcpyAsync(verdicts, c->verdicts.p, n, hipMemcpyDeviceToHost, st));
     if (gt) HIPCK(hipMemcpyAsync(gt, c->gt.p, n * 576, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    collect_timing(c);
     return CC_OK;
 }
 

@@ -129,6 +129,26 @@ cc_status cc_signature_aggregate_batch(cc_ctx* ctx, size_t n, size_t len, size_t
 cc_status cc_verkey_aggregate_batch(cc_ctx* ctx, size_t n, size_t len, size_t t, size_t q, const uint64_t* ids,
                                     const uint8_t* X, const uint8_t* Y, uint8_t* outX, uint8_t* outY);
 
+/* Device-buffer form of cc_signature_aggregate_batch (inputs resident in HBM; the timed path of
+ * BASELINE config 4).  Asynchronous on `stream` (NULL: the context stream). */
+cc_status cc_signature_aggregate_batch_device(cc_ctx* ctx, size_t n, size_t len, size_t t, const uint64_t* d_ids,
+                                              const uint8_t* d_sigma1, const uint8_t* d_sigma2,
+                                              uint8_t* d_out_sigma1, uint8_t* d_out_sigma2, void* stream);
+
+/* Issuer table for Verkey::aggregate at scale (BASELINE config 4: t = 67 of n = 100 issuers).  The
+ * n_issuers verkeys (X: n_issuers x OtherGroup, Y: n_issuers x q x OtherGroup) and their signer ids
+ * (unique) are decoded once and given fixed-base window tables in HBM (one-time cost); a batch then
+ * passes only id lists.  cc_verkey_aggregate_ids(_device) computes, per credential, exactly
+ * Verkey::aggregate(t, [(id_k, &issuer[id_k])]) (signature.rs:483-526): first t entries, Lagrange
+ * over the de-duplicated id set.  ids: n x len.  CC_ERR_DECODE if an id has no issuer verkey (host
+ * form; the device form requires every id to be in the table). */
+cc_status cc_set_issuers(cc_ctx* ctx, size_t n_issuers, size_t q, const uint64_t* ids, const uint8_t* X,
+                         const uint8_t* Y);
+cc_status cc_verkey_aggregate_ids(cc_ctx* ctx, size_t n, size_t len, size_t t, const uint64_t* ids, uint8_t* outX,
+                                  uint8_t* outY);
+cc_status cc_verkey_aggregate_ids_device(cc_ctx* ctx, size_t n, size_t len, size_t t, const uint64_t* d_ids,
+                                         uint8_t* d_outX, uint8_t* d_outY, void* stream);
+
 /* Batch PoKOfSignatureProof::verify against the shared verkey and params.
  *   sigma1, sigma2  : n x SignatureGroup (sigma'_1, sigma'_2)
  *   J, T            : n x OtherGroup (J and the Schnorr commitment)
@@ -141,6 +161,14 @@ cc_status cc_pok_verify_batch(cc_ctx* ctx, size_t n, size_t q, size_t r, size_t 
                               const uint8_t* sigma2, const uint8_t* J, const uint8_t* T, const uint8_t* responses,
                               const uint8_t* chal, const uint64_t* revealed_idx, const uint8_t* revealed_msgs,
                               uint8_t* verdicts, uint8_t* gt_or_null);
+
+/* Same, with the per-proof buffers already in device memory (the timed bench path, config 5);
+ * revealed_idx stays a host array of r indices.  Asynchronous on `stream` (NULL: context stream). */
+cc_status cc_pok_verify_batch_device(cc_ctx* ctx, size_t n, size_t q, size_t r, size_t nresp, const uint8_t* d_sigma1,
+                                     const uint8_t* d_sigma2, const uint8_t* d_J, const uint8_t* d_T,
+                                     const uint8_t* d_responses, const uint8_t* d_chal, const uint64_t* revealed_idx,
+                                     const uint8_t* d_revealed_msgs, uint8_t* d_verdicts, uint8_t* d_gt_or_null,
+                                     void* stream);
 
 /* Batch fixed-base scalar multiplication out_i = k_i * base (group 1 = G1, 2 = G2); scalars n x 48 B
  * big-endian Fr, out n encodings.  The keygen derivation g~ * x_i (reference src/keygen.rs:27-32)

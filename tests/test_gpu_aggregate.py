@@ -1,0 +1,133 @@
+"""GPU tests of BASELINE configs 4 and 5 at their full sizes and of the new entry points:
+the issuer-table Verkey::aggregate (cc_set_issuers + cc_verkey_aggregate_ids), the device-buffer
+Signature::aggregate and PoK verify, and the windowed Straus MSM (also covered by every
+tests/golden/aggregate_*.json case in test_gpu_parity.py)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden
+from test_gpu_parity import MODES, _cat
+
+sys.path.insert(0, ROOT)
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    import coconut
+    c = {m: coconut.Context(0, coconut.GroupMode(v)) for m, v in MODES.items()}
+    yield c
+    for x in c.values():
+        x.close()
+
+
+@pytest.mark.parametrize("name", ["aggregate_g2_t67_subsets.json", "aggregate_g1_t67_subsets.json",
+                                  "aggregate_g2.json", "aggregate_g1.json"])
+def test_issuer_table_verkey_aggregate_golden(ctxs, name):
+    """Verkey::aggregate from the resident issuer table equals the oracle on every golden case
+    (random 67-subsets with gaps, extra entries beyond t, duplicated ids)."""
+    from coconut import verkey_aggregate_ids
+    d = golden(name)
+    ctx = ctxs[d["mode"]]
+    q, t = d["q"], d["threshold"]
+    table = {}
+    for case in d["cases"]:
+        for i, x, ys in zip(case["ids"], case["X"], case["Y"]):
+            table[i] = (x, ys)
+    ids = sorted(table)
+    ctx.set_issuers(ids, _cat(table[i][0] for i in ids), _cat(y for i in ids for y in table[i][1]), q)
+    ob = ctx.mode.other_bytes
+    for case in d["cases"]:
+        oX, oY = verkey_aggregate_ids(ctx, 1, len(case["ids"]), t, [case["ids"]])
+        assert oX.hex() == case["out_X"], case["ids"][:5]
+        assert [oY[j * ob:(j + 1) * ob].hex() for j in range(q)] == case["out_Y"]
+    # all cases in ONE batch (ragged lengths padded with valid ids beyond t, which are ignored)
+    L = max(len(c["ids"]) for c in d["cases"])
+    rows = [c["ids"] + [c["ids"][0]] * (L - len(c["ids"])) for c in d["cases"]]
+    oX, oY = verkey_aggregate_ids(ctx, len(rows), L, t, rows)
+    assert [oX[i * ob:(i + 1) * ob].hex() for i in range(len(rows))] == [c["out_X"] for c in d["cases"]]
+
+
+def test_issuer_table_unknown_id_is_an_error(ctxs):
+    from coconut import CoconutError, verkey_aggregate_ids
+    d = golden("aggregate_g2.json")
+    ctx = ctxs["G2"]
+    case = d["cases"][0]
+    ctx.set_issuers(case["ids"], _cat(case["X"]), _cat(y for row in case["Y"] for y in row), d["q"])
+    with pytest.raises(CoconutError):
+        verkey_aggregate_ids(ctx, 1, 3, 3, [[1, 2, 99]])
+
+
+def test_config4_full_size_property(ctxs):
+    """10,000 credentials, t = 67 of n = 100 Shamir-shared issuers, random subsets: every aggregated
+    verkey equals g~ * master secret and every aggregated sigma_2 equals (x + sum y m) h — the
+    reference's check_key_aggregation identity (signature.rs:554-559) at config-4 scale."""
+    import torch
+    import bench_modes
+    from coconut import _lib
+    ctx = ctxs["G2"]
+    n = 10000
+    b = bench_modes.make_aggregate_batch(ctx, 0, n, seed=44)
+    ctx.set_issuers(b["iss"], b["X"], b["Y"], b["q"])
+    t, q, sb, ob = b["t"], b["q"], b["sb"], b["ob"]
+    dev = torch.device("cuda", 0)
+    d_ids = torch.from_numpy(b["ids"].view(np.int64).copy()).to(dev)
+    d_s1 = torch.frombuffer(bytearray(b["s1"]), dtype=torch.uint8).to(dev)
+    d_s2 = torch.frombuffer(bytearray(b["s2"]), dtype=torch.uint8).to(dev)
+    o1, o2 = (torch.zeros(n * sb, dtype=torch.uint8, device=dev) for _ in range(2))
+    oX = torch.zeros(n * ob, dtype=torch.uint8, device=dev)
+    oY = torch.zeros(n * q * ob, dtype=torch.uint8, device=dev)
+    P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    torch.cuda.synchronize()
+    lib = _lib.lib
+    assert lib.cc_signature_aggregate_batch_device(ctx.h, n, t, t, P(d_ids), P(d_s1), P(d_s2), P(o1), P(o2), None) == 0
+    assert lib.cc_verkey_aggregate_ids_device(ctx.h, n, t, t, P(d_ids), P(oX), P(oY), None) == 0
+    torch.cuda.synchronize()  # the calls ran on the context's own stream
+    assert bytes(oX.cpu().numpy()) == b["want_X"] * n
+    assert bytes(oY.cpu().numpy()) == b["want_Y"] * n
+    assert bytes(o2.cpu().numpy()) == b["want_s2"]
+    assert bytes(o1.cpu().numpy()) == b["want_s1"]
+
+
+def test_config5_full_size_pok_device(ctxs):
+    """65,536 PoK proofs (q = 32, 8 revealed) through cc_pok_verify_batch_device: verdicts equal
+    construction (1/16 corrupted responses); the host entry point agrees on a slice."""
+    import torch
+    import bench_modes
+    from coconut import _lib, pok_verify_batch
+    ctx = ctxs["G2"]
+    n = 65536
+    b = bench_modes.make_pok_batch(ctx, 0, n, seed=55)
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    q, r, nresp = b["q"], len(b["revealed"]), b["nresp"]
+    dev = torch.device("cuda", 0)
+    D = {k: torch.frombuffer(bytearray(b[k]), dtype=torch.uint8).to(dev) for k in ("s1", "s2", "J", "T", "resp", "chal", "rev")}
+    v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    P = lambda k: ctypes.c_void_p(D[k].data_ptr())  # noqa: E731
+    torch.cuda.synchronize()
+    st = _lib.lib.cc_pok_verify_batch_device(ctx.h, n, q, r, nresp, P("s1"), P("s2"), P("J"), P("T"), P("resp"),
+                                             P("chal"), (ctypes.c_uint64 * r)(*b["revealed"]), P("rev"),
+                                             ctypes.c_void_p(v.data_ptr()), None, None)
+    assert st == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), b["expect"])
+    k = 64
+    vh = pok_verify_batch(ctx, k, q, b["revealed"], nresp, b["s1"][:k * 192], b["s2"][:k * 192], b["J"][:k * 97],
+                          b["T"][:k * 97], b["resp"][:k * nresp * 48], b["chal"][:k * 48], b["rev"][:k * r * 48])
+    assert np.array_equal(vh, b["expect"][:k])
+
+
+def test_signature_aggregate_threshold_zero_and_small_order_safe(ctxs):
+    """t = 0 aggregates to the identity with sigma_1 from entry 0 (reference: empty MSM)."""
+    from coconut import signature_aggregate_batch
+    d = golden("aggregate_g2.json")
+    ctx = ctxs["G2"]
+    case = d["cases"][0]
+    o1, o2 = signature_aggregate_batch(ctx, 1, 3, 0, [case["ids"]], _cat(case["sigma1"]), _cat(case["sigma2"]))
+    assert o1.hex() == case["sigma1"][0]
+    assert o2 == bytes(96) + (1).to_bytes(48, "big") + bytes(48)

@@ -556,6 +556,168 @@ def verify_sigg1(cred, vk_aff, gtil_aff, q):
     return int(ok), gt_bytes(r), counts
 
 
+# ---------------------------------------------------------------- aggregation (aggregate.hip)
+def lagrange0(ids_first_t, i):
+    S = sorted(set(ids_first_t))
+    num, den = 1, 1
+    for j in S:
+        if j != i:
+            num = num * j % R
+            den = den * (j - i) % R
+    return num * pow(den, R - 2, R) % R
+
+
+def recode_w4(k):
+    d, carry = [], 0
+    for w in range(64):
+        v = ((k >> (4 * w)) & 0xF) + carry
+        carry = 1 if v > 8 else 0
+        d.append(v - 16 * carry)
+    d.append(carry)
+    return d
+
+
+def straus(g, pts, scalars):
+    """k_msm_straus: signed 4-bit windows, multiples 1P..8P batch-normalised with one inversion."""
+    ent = []
+    acc_z = g.one
+    for P in pts:
+        J = (P[0], P[1], g.one) if P else g.inf()
+        for d in range(8):
+            if d == 1:
+                J = g.dbl_j(J)
+            elif d > 1 and P:
+                J = g.add_aff(J, P)
+            ent.append(J)
+            if not g.is_inf(J):
+                acc_z = g.mul(acc_z, J[2])
+    inv = g.inv(acc_z)
+    aff = [None] * len(ent)
+    for e in range(len(ent) - 1, -1, -1):
+        J = ent[e]
+        if g.is_inf(J):
+            continue
+        pz = g.one
+        for f in range(e):  # the stored prefix (uncounted: it was recorded on the way up)
+            if not g.is_inf(ent[f]):
+                pz = _raw_mul(g, pz, ent[f][2])
+        zi = g.mul(inv, pz)
+        inv = g.mul(inv, J[2])
+        zi2 = g.sqr(zi)
+        x = g.mul(J[0], zi2)
+        zi3 = g.mul(zi2, zi)
+        aff[e] = (x, g.mul(J[1], zi3))
+    digs = [recode_w4(k) for k in scalars]
+    acc = g.inf()
+    for win in range(64, -1, -1):
+        if win != 64 and not g.is_inf(acc):
+            for _ in range(4):
+                acc = g.dbl_j(acc)
+        for k in range(len(pts)):
+            d = digs[k][win]
+            if d == 0 or aff[k * 8 + abs(d) - 1] is None:
+                continue
+            e = aff[k * 8 + abs(d) - 1]
+            if d < 0:
+                e = (e[0], g.neg(e[1]))
+            acc = g.add_aff(acc, e)
+    return g.to_aff(acc)
+
+
+def _raw_mul(g, a, b):
+    m = C.M
+    r = g.mul(a, b)
+    C.M = m
+    return r
+
+
+def fixed_sum(g, pts, scalars):
+    """k_vk_agg_fixed / msm_fixed: sum of 8-bit-window table entries (entries precomputed, uncounted)."""
+    acc = g.inf()
+    for P, k in zip(pts, scalars):
+        if P is None:
+            continue
+        acc = fixed_table_mul_add(g, acc, k, P, 0, 32)
+    return g.to_aff(acc)
+
+
+def aggregate_case(d, case):
+    """Signature::aggregate (Straus, SignatureGroup) + Verkey::aggregate (issuer tables, OtherGroup)."""
+    gs, go = (G2, G1) if d["mode"] == "G2" else (G1, G2)
+    t, q = d["threshold"], d["q"]
+    ids = case["ids"][:t]
+    ls = [lagrange0(ids, i) for i in ids]
+    s2 = [decode(gs, bytes.fromhex(h)) for h in case["sigma2"][:t]]
+    C.take()
+    sig = straus(gs, s2, ls)
+    straus_m = C.take()
+    Xs = [decode(go, bytes.fromhex(h)) for h in case["X"][:t]]
+    Ys = [[decode(go, bytes.fromhex(h)) for h in row] for row in case["Y"][:t]]
+    C.take()
+    vkX = fixed_sum(go, Xs, ls)
+    vkY = [fixed_sum(go, [Ys[k][j] for k in range(t)], ls) for j in range(q)]
+    fixed_m = C.take()
+    return sig, vkX, vkY, {"straus_sigma2": straus_m, "fixed_verkey": fixed_m}
+
+
+def enc(g, a):
+    if a is None:
+        return (b"\x04" + b"\x00" * 48 + (1).to_bytes(48, "big")) if not g.two else \
+            b"\x00" * 96 + (1).to_bytes(48, "big") + b"\x00" * 48
+    if g.two:
+        return b"".join(v.to_bytes(48, "big") for v in (a[0][0], a[0][1], a[1][0], a[1][1]))
+    return b"\x04" + a[0].to_bytes(48, "big") + a[1].to_bytes(48, "big")
+
+
+# ---------------------------------------------------------------- PoK verify (k_prep_pok, SigG2)
+def pok_sigg2(d, p, vk_aff, gtil):
+    """k_prep_pok<Fp2, Fp> -> k_miller<2,false> -> k_fexp."""
+    counts = {}
+    q, rev = d["q"], d["revealed"]
+    X, Ys = vk_aff
+    s1 = decode(G2, bytes.fromhex(p["sigma1"]))
+    s2 = decode(G2, bytes.fromhex(p["sigma2"]))
+    Ja = decode(G1, bytes.fromhex(p["J"]))
+    resp = [int(h, 16) % R for h in p["responses"]]
+    chal = int(p["chal"], 16) % R
+    acc = fixed_table_mul_add(G1, G1.inf(), resp[0], gtil, 0, 32)
+    slot = 1
+    for h in range(q):
+        if h in rev:
+            continue
+        acc = fixed_table_mul_add(G1, acc, resp[slot], Ys[h], 0, 32)
+        slot += 1
+    if Ja:
+        sacc = G1.inf()
+        for b in range(254, -1, -1):
+            sacc = G1.dbl_j(sacc)
+            if (chal >> b) & 1:
+                sacc = G1.add_aff(sacc, Ja)
+        acc = G1.add_j(acc, sacc)
+    Ta = decode(G1, bytes.fromhex(p["T"]))
+    if Ta:
+        acc = G1.add_aff(acc, (Ta[0], G1.neg(Ta[1])))
+    schnorr_ok = G1.is_inf(acc)
+    jp = (X[0], X[1], 1)
+    if Ja:
+        jp = G1.add_aff(jp, Ja)
+    for z, h in enumerate(rev):
+        jp = fixed_table_mul_add(G1, jp, int(p["revealed_msgs"][z], 16) % R, Ys[h], 0, 32)
+    jinf = G1.is_inf(jp)
+    pe = (fmul(jp[0], jp[2]), jp[1], fmul(fmul(jp[2], jp[2]), jp[2])) if not jinf else (0, 0, 0)
+    counts["prep"] = C.take()
+    skip0 = s1 is None or jinf
+    skip1 = s2 is None
+    q0 = s1 if s1 else ((0, 0), (0, 0))
+    q1 = (s2[0], f2_neg(s2[1])) if s2 else ((0, 0), (0, 0))
+    f = miller2([(q0, pe, skip0), (q1, (gtil[0], gtil[1], None), skip1)])
+    counts["miller"] = C.take()
+    r = final_exp(f)
+    counts["fexp"] = C.take()
+    ok = f12_is_one(r) and s1 is not None and s2 is not None and schnorr_ok
+    return int(ok), counts
+
+
 def vk_from_fixture(d):
     g = G1 if d["mode"] == "G2" else G2
     dec = lambda h: decode(g, bytes.fromhex(h))  # noqa: E731
@@ -592,6 +754,30 @@ def main():
         res["configs"][key] = {"credentials_averaged": len(rows),
                                "M_per_credential": {k: round(v, 1) for k, v in avg.items()},
                                "mads_per_credential": {k: round(v * 288) for k, v in avg.items()}}
+    with open(os.path.join(root, "tests", "golden", "aggregate_g2_t67_subsets.json")) as f:
+        d = json.load(f)
+    sig, vkX, vkY, cnt = aggregate_case(d, d["cases"][0])
+    assert enc(G2, sig).hex() == d["cases"][0]["out_sigma2"] and enc(G1, vkX).hex() == d["cases"][0]["out_X"]
+    res["configs"]["aggregate_sigg2_t67"] = {
+        "credentials_averaged": 1, "M_per_credential": cnt,
+        "mads_per_credential": {k: v * 288 for k, v in cnt.items()},
+        "note": "straus_sigma2 = Signature::aggregate (67-point G2 Straus MSM); fixed_verkey = Verkey::aggregate "
+                "(q+1 = 7 67-point G1 fixed-base MSMs from the issuer tables); case 0 of "
+                "tests/golden/aggregate_g2_t67_subsets.json, outputs checked against the fixture"}
+    with open(os.path.join(root, "tests", "golden", "pok_g2_q32.json")) as f:
+        d = json.load(f)
+    vk, gt = vk_from_fixture(d)
+    rows = []
+    for p in d["proofs"]:
+        v, cnt = pok_sigg2(d, p, vk, gt)
+        assert v == p["verdict"], p["kind"]
+        if p["kind"] == "valid":
+            rows.append(cnt)
+    res["configs"]["pok_sigg2_q32_r8"] = {
+        "credentials_averaged": len(rows),
+        "M_per_credential": {k: round(sum(r[k] for r in rows) / len(rows), 1) for k in rows[0]},
+        "mads_per_credential": {k: round(sum(r[k] for r in rows) / len(rows) * 288) for k in rows[0]},
+        "note": "valid proofs of tests/golden/pok_g2_q32.json (verdicts of every kind checked)"}
     out = os.path.join(root, "tests", "fixtures", "opcount.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:
