@@ -2,9 +2,11 @@
 //
 //   k_lagrange     : secret_sharing `Polynomial::lagrange_basis_at_0` [EXT] over the de-duplicated
 //                    id set of the first t entries (reference src/signature.rs:454-463, 496-509)
-//   k_msm_tasks    : one Lagrange-weighted MSM per lane — Signature::aggregate (signature.rs:465,
-//                    SignatureGroup) and the q+1 MSMs of Verkey::aggregate (signature.rs:512-524,
-//                    OtherGroup); output encoded as amcl_wrapper `to_bytes`
+//   k_msm_straus   : one Lagrange-weighted MSM per 16-lane group, windowed Straus over variable
+//                    bases — Signature::aggregate (signature.rs:465, SignatureGroup) and the q+1 MSMs
+//                    of Verkey::aggregate (signature.rs:512-524, OtherGroup) given per-entry verkeys;
+//                    output encoded as amcl_wrapper `to_bytes`
+//   k_vk_agg_fixed : Verkey::aggregate from the resident issuer table (fixed-base windows)
 //   k_prep_pok     : ps_sig PoKOfSignatureProof::verify [EXT] (reference pok_sig.rs:103-105):
 //                    Schnorr check MSM(g~, Y~_hidden.., J; responses.., chal) == T, then
 //                    J' = X~ + J + sum_revealed Y~_i m_i, written in the verify kernels' Miller-loop
@@ -101,52 +103,6 @@ __global__ void k_lagrange(size_t n, size_t len, size_t t, const uint64_t* __res
     for (int k = 0; k < 8; k++) o[k] = li.v[k];
 }
 
-// ================================================================ Lagrange-weighted MSM tasks
-// task -> points at pts + (task / l_div) * pt_stride + (task % l_div) * pt_jstride + k * pt_step,
-// k < t; scalars l[(task / l_div) * t + k]; output encoding at out + task * ebytes.
-template <class F>
-__global__ __launch_bounds__(256) void k_msm_tasks(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
-                                                   size_t pt_stride, size_t pt_jstride, size_t pt_step,
-                                                   const uint32_t* __restrict__ l, size_t l_div,
-                                                   uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
-    size_t task = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (task >= ntask) return;
-    constexpr int FS = sizeof(F) / sizeof(Fp);
-    const size_t cred = task / l_div;
-    const uint8_t* base = pts + cred * pt_stride + (task % l_div) * pt_jstride;
-    const uint32_t* lk = l + cred * t * 8;
-    Soa S{scratch, ntask};
-    // decode once into the lane's scratch column (slot (k * 2FS + c)); inf flag in bit k of masks
-    for (size_t k = 0; k < t; k++) {
-        Aff<F> a;
-        bool ok = decode_pt<F>(a, base + k * pt_step);
-        if (!ok) {
-            // identity base contributes nothing: zero its scalar by marking x = y = 0 (flag below)
-        }
-        const Fp* pa = reinterpret_cast<const Fp*>(&a);
-        for (int c = 0; c < 2 * FS; c++) st_fp(S, k * 2 * FS + c, task, pa[c]);
-        // store flag in an extra slot word: use slot (t * 2FS) region, one word per k
-        S.p[(t * 2 * FS * NL + k) * S.n + task] = ok ? 0u : 1u;
-    }
-    Jac<F> acc;
-    jac_set_inf(acc);
-    for (int b = 254; b >= 0; b--) {
-        jac_dbl(acc, acc);
-        for (size_t k = 0; k < t; k++) {
-            uint32_t bit = (lk[k * 8 + (b >> 5)] >> (b & 31)) & 1u;
-            if (bit && !S.p[(t * 2 * FS * NL + k) * S.n + task]) {
-                Aff<F> a;
-                Fp* pa = reinterpret_cast<Fp*>(&a);
-                for (int c = 0; c < 2 * FS; c++) ld_fp(pa[c], S, k * 2 * FS + c, task);
-                jac_add_aff(acc, acc, a);
-            }
-        }
-    }
-    Aff<F> r;
-    bool fin = jac_to_aff(r, acc);
-    encode_pt<F>(out + task * ebytes<F>(), r, fin);
-}
-
 // ================================================================ windowed Straus MSM (variable bases)
 // One Lagrange-weighted MSM per lane with signed 4-bit windows: per base the multiples 1P..8P are
 // built in Jacobian form, batch-normalised to affine with ONE inversion per task (Montgomery's
@@ -174,13 +130,40 @@ DEV void recode_w4(int8_t* d, const uint32_t k[8]) {
     d[64] = (int8_t)carry;
 }
 
-template <class F>
-__global__ __launch_bounds__(64) void k_msm_straus(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
-                                                   size_t pt_stride, size_t pt_jstride, size_t pt_step,
-                                                   const uint32_t* __restrict__ l, size_t l_div,
-                                                   uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
-    const size_t task = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (task >= ntask) return;
+// Sum of Jacobian points across the L consecutive lanes of a task (L a power of two <= 64):
+// butterfly over __shfl_xor, every lane ends with the same sum.
+template <class F, int L>
+DEV void lane_group_sum(Jac<F>& acc) {
+    constexpr int JW = sizeof(Jac<F>) / 4;
+#pragma unroll 1
+    for (int m = L >> 1; m > 0; m >>= 1) {
+        Jac<F> o;
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(&acc);
+        uint32_t* w = reinterpret_cast<uint32_t*>(&o);
+        for (int c = 0; c < JW; c++) w[c] = (uint32_t)__shfl_xor((int)a[c], m);
+        // same operand order on both partners so they hold the same representation
+        if (threadIdx.x & m) {
+            Jac<F> t = acc;
+            acc = o;
+            o = t;
+        }
+        jac_add(acc, acc, o);
+    }
+}
+
+// L lanes per task: lane l takes the bases k = l, l + L, ... (t = 67, L = 16: 4-5 bases per lane),
+// builds and normalises their multiples, runs the 65 windows over them, and the L partial sums are
+// added across the lane group.  One lane per task would leave 10,000 tasks as 157 waves — a
+// latency-bound GPU (each lane doing ~146k serial Fp multiplications).
+template <class F, int L>
+__global__ __launch_bounds__(256) void k_msm_straus(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
+                                                    size_t pt_stride, size_t pt_jstride, size_t pt_step,
+                                                    const uint32_t* __restrict__ l, size_t l_div,
+                                                    uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t task = g / L;
+    const int lane = (int)(g % L);
+    if (task >= ntask) return;  // uniform over the lane group (L divides the block)
     using T = FT<F>;
     constexpr int FS = sizeof(F) / sizeof(Fp);
     constexpr int JW = 3 * FS * NL, PW = FS * NL;
@@ -190,12 +173,11 @@ __global__ __launch_bounds__(64) void k_msm_straus(size_t ntask, size_t t, const
     uint32_t* ent = scratch + task * straus_words<F>(t);
     uint32_t* pre = ent + t * 8 * JW;
     int8_t* dig = reinterpret_cast<int8_t*>(pre + t * 8 * PW);
-    const size_t m = t * 8;
-    // multiples 1P..8P (Jacobian) and the running product of their Z coordinates
+    // multiples 1P..8P (Jacobian) of this lane's bases and the running product of their Z
     F acc_z;
     T::one(acc_z);
 #pragma unroll 1
-    for (size_t k = 0; k < t; k++) {
+    for (size_t k = lane; k < t; k += L) {
         Aff<F> P;
         const bool ok = decode_pt<F>(P, base + k * pt_step);
         recode_w4(dig + k * 65, lk + k * 8);
@@ -221,31 +203,37 @@ __global__ __launch_bounds__(64) void k_msm_straus(size_t ntask, size_t t, const
             if (!jac_is_inf(J)) T::mul(acc_z, acc_z, J.z);
         }
     }
-    // one inversion, then walk back: z_e^-1 = inv * prefix_e; inv *= z_e
+    // one inversion per lane, then walk back: z_e^-1 = inv * prefix_e; inv *= z_e
     F inv;
     T::inv(inv, acc_z);
+    if (t > (size_t)lane) {
+        const long long kmax = (long long)(((t - 1 - lane) / L) * L + lane);
 #pragma unroll 1
-    for (size_t e = m; e-- > 0;) {
-        Jac<F> J;
-        uint32_t* w = ent + e * JW;
-        uint32_t* jw = reinterpret_cast<uint32_t*>(&J);
-        for (int c = 0; c < JW; c++) jw[c] = w[c];
-        const bool inf = jac_is_inf(J);
-        if (!inf) {
-            F pz, zi, zi2;
-            uint32_t* pw = reinterpret_cast<uint32_t*>(&pz);
-            for (int c = 0; c < PW; c++) pw[c] = pre[e * PW + c];
-            T::mul(zi, inv, pz);
-            T::mul(inv, inv, J.z);
-            T::sqr(zi2, zi);
-            T::mul(J.x, J.x, zi2);
-            T::mul(zi2, zi2, zi);
-            T::mul(J.y, J.y, zi2);
+        for (long long kk = kmax; kk >= lane; kk -= L) {
+            for (int d = 7; d >= 0; d--) {
+                const size_t e = (size_t)kk * 8 + d;
+                Jac<F> J;
+                uint32_t* w = ent + e * JW;
+                uint32_t* jw = reinterpret_cast<uint32_t*>(&J);
+                for (int c = 0; c < JW; c++) jw[c] = w[c];
+                const bool inf = jac_is_inf(J);
+                if (!inf) {
+                    F pz, zi, zi2;
+                    uint32_t* pw = reinterpret_cast<uint32_t*>(&pz);
+                    for (int c = 0; c < PW; c++) pw[c] = pre[e * PW + c];
+                    T::mul(zi, inv, pz);
+                    T::mul(inv, inv, J.z);
+                    T::sqr(zi2, zi);
+                    T::mul(J.x, J.x, zi2);
+                    T::mul(zi2, zi2, zi);
+                    T::mul(J.y, J.y, zi2);
+                }
+                for (int c = 0; c < 2 * PW; c++) w[c] = jw[c];  // affine x, y
+                w[2 * PW] = inf ? 1u : 0u;
+            }
         }
-        for (int c = 0; c < 2 * PW; c++) w[c] = jw[c];  // affine x, y
-        w[2 * PW] = inf ? 1u : 0u;
     }
-    // 65 signed windows, most significant first
+    // 65 signed windows over this lane's bases, most significant first
     Jac<F> acc;
     jac_set_inf(acc);
 #pragma unroll 1
@@ -253,7 +241,7 @@ __global__ __launch_bounds__(64) void k_msm_straus(size_t ntask, size_t t, const
         if (win != 64 && !jac_is_inf(acc))
             for (int z = 0; z < 4; z++) jac_dbl(acc, acc);
 #pragma unroll 1
-        for (size_t k = 0; k < t; k++) {
+        for (size_t k = lane; k < t; k += L) {
             const int d = dig[k * 65 + win];
             if (!d) continue;
             const uint32_t* w = ent + (k * 8 + (d < 0 ? -d : d) - 1) * JW;
@@ -265,9 +253,12 @@ __global__ __launch_bounds__(64) void k_msm_straus(size_t ntask, size_t t, const
             jac_add_aff(acc, acc, e);
         }
     }
-    Aff<F> r;
-    bool fin = jac_to_aff(r, acc);
-    encode_pt<F>(out + task * ebytes<F>(), r, fin);
+    lane_group_sum<F, L>(acc);
+    if (lane == 0) {
+        Aff<F> r;
+        bool fin = jac_to_aff(r, acc);
+        encode_pt<F>(out + task * ebytes<F>(), r, fin);
+    }
 }
 
 // ================================================================ issuer-table Verkey::aggregate
@@ -286,7 +277,7 @@ DEV bool aff_is_zero_pair(const Aff<F>& a) {
     return o == 0;
 }
 
-template <class F>
+template <class F, int L>
 __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size_t t, int q,
                                                       const uint64_t* __restrict__ ids,
                                                       const uint32_t* __restrict__ l,
@@ -294,15 +285,17 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
                                                       const uint32_t* __restrict__ table,
                                                       const uint32_t* __restrict__ binf,
                                                       uint8_t* __restrict__ outX, uint8_t* __restrict__ outY) {
-    const size_t task = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (task >= n * (size_t)(q + 1)) return;
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t task = g / L;
+    const int lane = (int)(g % L);
+    if (task >= n * (size_t)(q + 1)) return;  // uniform over the lane group
     const size_t cred = task / (q + 1);
     const int j = (int)(task % (q + 1));
     constexpr int EW = sizeof(Aff<F>) / 4;
     Jac<F> acc;
     jac_set_inf(acc);
 #pragma unroll 1
-    for (size_t k = 0; k < t; k++) {
+    for (size_t k = lane; k < t; k += L) {
         const uint64_t id = ids[cred * len + k];
         int lo = 0, hi = n_iss;
         while (lo < hi) {
@@ -323,6 +316,8 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
             jac_add_aff(acc, acc, e);
         }
     }
+    lane_group_sum<F, L>(acc);
+    if (lane) return;
     Aff<F> r;
     const bool fin = jac_to_aff(r, acc);
     uint8_t* o = j == 0 ? outX + cred * ebytes<F>() : outY + (cred * q + (j - 1)) * ebytes<F>();
@@ -473,34 +468,20 @@ int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// scratch: ntask * (t * 2 * FS * 12 + t) words
-int cck_msm_tasks(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
-                  size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
-                  hipStream_t st) {
-    if (!ntask) return 0;
-    dim3 g(nblocks(ntask, 64)), b(64);
-    if (group == 1)
-        hipLaunchKernelGGL(k_msm_tasks<Fp>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
-                           d_scratch, d_out);
-    else
-        hipLaunchKernelGGL(k_msm_tasks<Fp2>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
-                           d_scratch, d_out);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 size_t cck_straus_words(int group, size_t t) { return group == 1 ? straus_words<Fp>(t) : straus_words<Fp2>(t); }
 
 int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
                    size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
                    hipStream_t st) {
     if (!ntask) return 0;
-    dim3 g(nblocks(ntask, 64)), b(64);
+    constexpr int L = 16;
+    dim3 g(nblocks(ntask * L, 256)), b(256);
     if (group == 1)
-        hipLaunchKernelGGL(k_msm_straus<Fp>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
-                           d_scratch, d_out);
+        hipLaunchKernelGGL((k_msm_straus<Fp, L>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l,
+                           l_div, d_scratch, d_out);
     else
-        hipLaunchKernelGGL(k_msm_straus<Fp2>, g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div,
-                           d_scratch, d_out);
+        hipLaunchKernelGGL((k_msm_straus<Fp2, L>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l,
+                           l_div, d_scratch, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -508,13 +489,14 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
                      const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, const uint32_t* d_binf,
                      uint8_t* d_outX, uint8_t* d_outY, hipStream_t st) {
     if (!n) return 0;
+    constexpr int L = 4;
     const size_t ntask = n * (size_t)(q + 1);
-    dim3 g(nblocks(ntask, 256)), b(256);
+    dim3 g(nblocks(ntask * L, 256)), b(256);
     if (group == 1)
-        hipLaunchKernelGGL(k_vk_agg_fixed<Fp>, g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table, d_binf,
-                           d_outX, d_outY);
+        hipLaunchKernelGGL((k_vk_agg_fixed<Fp, L>), g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
+                           d_binf, d_outX, d_outY);
     else
-        hipLaunchKernelGGL(k_vk_agg_fixed<Fp2>, g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
+        hipLaunchKernelGGL((k_vk_agg_fixed<Fp2, L>), g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
                            d_binf, d_outX, d_outY);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

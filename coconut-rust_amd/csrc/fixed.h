@@ -1,0 +1,68 @@
+// Fixed-base window tables — device code shared by the prep, RLC, PoK and aggregation kernels.
+//
+// The verifier's MSMs (multi_scalar_mul_var_time over X~, Y~_j, g~) have FIXED
+// bases per verkey, so cc_set_verkey precomputes, per base B, nwin = ceil(256 / wbits) windows of the
+// 2^wbits - 1 affine multiples d * 2^(wbits w) * B (AoS, Montgomery).  A scalar multiplication is then
+// nwin mixed additions and no doublings.  The shared-verkey tables use wbits = 16 (16 windows: half
+// the additions of 8-bit windows; 100 MB per G1 base, 200 MB per G2 base — the tables live in HBM and
+// every lookup is one random 96/192-byte read, which the ~8 TB/s HBM serves far faster than the
+// VALU-bound additions consume them); the issuer tables (hundreds of bases) and the one-off
+// cc_fixed_base_mul use wbits = 8.
+// An entry equal to the identity (only possible for a small-order base) is stored as (0, 0), which
+// lies on neither curve, and skipped.
+#pragma once
+#include "curve.h"
+
+namespace cc {
+
+__host__ __device__ constexpr int ft_nwin(int wbits) { return (256 + wbits - 1) / wbits; }
+__host__ __device__ constexpr size_t ft_went(int wbits) { return ((size_t)1 << wbits) - 1; }
+// words of one base's table
+template <class F>
+__host__ __device__ constexpr size_t ft_base_words(int wbits) {
+    return (size_t)ft_nwin(wbits) * ft_went(wbits) * (sizeof(Aff<F>) / 4);
+}
+
+// window w of a canonical scalar given as 8 little-endian 32-bit limbs
+DEV uint32_t ft_digit(const uint32_t k[8], int w, int wbits) {
+    if (wbits == 16) return (k[w >> 1] >> (16 * (w & 1))) & 0xffffu;
+    return (k[w >> 2] >> (8 * (w & 3))) & 0xffu;
+}
+
+template <class F>
+DEV void ft_load(Aff<F>& a, const uint32_t* p) {
+    constexpr int W = sizeof(Aff<F>) / 16;
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4* d = reinterpret_cast<uint4*>(&a);
+#pragma unroll
+    for (int k = 0; k < W; k++) d[k] = q[k];
+}
+
+template <class F>
+DEV bool ft_is_empty(const Aff<F>& a) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
+    uint32_t o = 0;
+#pragma unroll
+    for (int c = 0; c < (int)(sizeof(Aff<F>) / 4); c++) o |= w[c];
+    return o == 0;
+}
+
+// acc += (k restricted to windows [w0, w1)) * B_j
+template <class F>
+DEV void ft_add(Jac<F>& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j, int w0,
+                int w1) {
+    constexpr int EW = sizeof(Aff<F>) / 4;
+    const size_t went = ft_went(wbits);
+    const uint32_t* tj = table + (size_t)j * ft_base_words<F>(wbits);
+#pragma unroll 1
+    for (int w = w0; w < w1; w++) {
+        const uint32_t d = ft_digit(k, w, wbits);
+        if (!d) continue;
+        Aff<F> e;
+        ft_load<F>(e, tj + ((size_t)w * went + d - 1) * EW);
+        if (ft_is_empty(e)) continue;
+        jac_add_aff(acc, acc, e);
+    }
+}
+
+}  // namespace cc
