@@ -12,6 +12,7 @@
 //                    J' = X~ + J + sum_revealed Y~_i m_i, written in the verify kernels' Miller-loop
 //                    operand layout so k_miller_* / k_fexp finish the 2-pairing check.
 #include "codec.h"
+#include "fixed.h"
 #include "fr.h"
 #include "pairing.h"
 
@@ -54,24 +55,6 @@ template <class F>
 DEV void ld_aff_aos(Aff<F>& a, const uint32_t* p) {
     uint32_t* d = reinterpret_cast<uint32_t*>(&a);
     for (int k = 0; k < (int)(sizeof(Aff<F>) / 4); k++) d[k] = p[k];
-}
-
-constexpr int NWIN = 32, WENT = 255;
-
-// fixed-base: acc += k * B_j via the 8-bit window table of base j (k canonical, LE limbs)
-template <class F>
-DEV void add_fixed(Jac<F>& acc, const uint32_t kv[8], const uint32_t* table, int j) {
-    constexpr int EW = sizeof(Aff<F>) / 4;
-    const uint32_t* tj = table + (size_t)j * NWIN * WENT * EW;
-#pragma unroll 1
-    for (int w = 0; w < NWIN; w++) {
-        uint32_t d = (kv[w >> 2] >> (8 * (w & 3))) & 0xffu;
-        if (d) {
-            Aff<F> e;
-            ld_aff_aos<F>(e, tj + ((size_t)w * WENT + d - 1) * EW);
-            jac_add_aff(acc, acc, e);
-        }
-    }
 }
 
 }  // namespace
@@ -269,14 +252,6 @@ __global__ __launch_bounds__(256) void k_msm_straus(size_t ntask, size_t t, cons
 // j = 1..q -> Y~_{j-1}.  Issuer ids are sorted; each entry's id is found by binary search (the
 // host entry point has checked they all exist).  Table entries that are the identity (possible only
 // for small-order bases) are stored as (0, 0), which is on neither curve, and skipped.
-template <class F>
-DEV bool aff_is_zero_pair(const Aff<F>& a) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(&a);
-    uint32_t o = 0;
-    for (int c = 0; c < (int)(sizeof(Aff<F>) / 4); c++) o |= w[c];
-    return o == 0;
-}
-
 template <class F, int L>
 __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size_t t, int q,
                                                       const uint64_t* __restrict__ ids,
@@ -291,7 +266,6 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
     if (task >= n * (size_t)(q + 1)) return;  // uniform over the lane group
     const size_t cred = task / (q + 1);
     const int j = (int)(task % (q + 1));
-    constexpr int EW = sizeof(Aff<F>) / 4;
     Jac<F> acc;
     jac_set_inf(acc);
 #pragma unroll 1
@@ -304,17 +278,7 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
         }
         const int b = lo * (q + 1) + j;
         if (binf[b]) continue;
-        const uint32_t* kv = l + (cred * t + k) * 8;
-        const uint32_t* tb = table + (size_t)b * NWIN * WENT * EW;
-#pragma unroll 1
-        for (int w = 0; w < NWIN; w++) {
-            const uint32_t d = (kv[w >> 2] >> (8 * (w & 3))) & 0xffu;
-            if (!d) continue;
-            Aff<F> e;
-            ld_aff_aos<F>(e, tb + ((size_t)w * WENT + d - 1) * EW);
-            if (aff_is_zero_pair(e)) continue;
-            jac_add_aff(acc, acc, e);
-        }
+        ft_add<F>(acc, l + (cred * t + k) * 8, table, 8, b, 0, ft_nwin(8));
     }
     lane_group_sum<F, L>(acc);
     if (lane) return;
@@ -337,7 +301,7 @@ __global__ __launch_bounds__(256) void k_prep_pok(size_t n, int q, int r, const 
                                                   const uint8_t* __restrict__ rev_msgs,
                                                   const uint32_t* __restrict__ rev_idx,
                                                   const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                                                  const uint32_t* __restrict__ table,
+                                                  const uint32_t* __restrict__ table, int wbits,
                                                   const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
                                                   uint32_t* __restrict__ flags) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -373,7 +337,8 @@ __global__ __launch_bounds__(256) void k_prep_pok(size_t n, int q, int r, const 
         Fr k;
         const uint8_t* rp = resp + i * (size_t)(q - r + 1) * 48;
         fr_from_be48(k, rp);
-        if (!binf[q]) add_fixed<FO>(acc, k.v, table, q);  // table base q = g~
+        const int nwin = ft_nwin(wbits);
+        if (!binf[q]) ft_add<FO>(acc, k.v, table, wbits, q, 0, nwin);  // table base q = g~
         int slot = 1;
         for (int h = 0; h < q; h++) {
             bool revealed = false;
@@ -381,7 +346,7 @@ __global__ __launch_bounds__(256) void k_prep_pok(size_t n, int q, int r, const 
             if (revealed) continue;
             fr_from_be48(k, rp + (size_t)slot * 48);
             slot++;
-            if (!binf[h]) add_fixed<FO>(acc, k.v, table, h);
+            if (!binf[h]) ft_add<FO>(acc, k.v, table, wbits, h, 0, nwin);
         }
         // J * chal (variable base)
         fr_from_be48(k, chal + i * 48);
@@ -415,7 +380,7 @@ __global__ __launch_bounds__(256) void k_prep_pok(size_t n, int q, int r, const 
         Fr m;
         fr_from_be48(m, rev_msgs + ((size_t)i * r + z) * 48);
         int h = (int)rev_idx[z];
-        if (!binf[h]) add_fixed<FO>(jp, m.v, table, h);
+        if (!binf[h]) ft_add<FO>(jp, m.v, table, wbits, h, 0, ft_nwin(wbits));
     }
     if (jac_is_inf(jp)) fl |= 4u;
     if (kSigG2) {
@@ -451,7 +416,7 @@ __global__ __launch_bounds__(256) void k_fixed_mul(size_t n, const uint8_t* __re
     if (!base_inf) {
         Fr k;
         fr_from_be48(k, ks + i * 48);
-        add_fixed<F>(acc, k.v, table, 0);
+        ft_add<F>(acc, k.v, table, 8, 0, 0, ft_nwin(8));
     }
     Aff<F> r;
     bool fin = jac_to_aff(r, acc);
@@ -503,16 +468,16 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
 
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
-                 const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table,
+                 const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
                  const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st) {
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
     if (mode == 0)
         hipLaunchKernelGGL((k_prep_pok<Fp2, Fp>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
-                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, d_binf, d_prep, d_flags);
+                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags);
     else
         hipLaunchKernelGGL((k_prep_pok<Fp, Fp2>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
-                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, d_binf, d_prep, d_flags);
+                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

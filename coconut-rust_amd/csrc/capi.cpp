@@ -17,13 +17,13 @@
 
 extern "C" {
 int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_out, uint32_t* d_inf, hipStream_t st);
-int cck_build_table(int group, int nbases, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
+int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
                     uint32_t* d_table, hipStream_t st);
 int cck_gtilde_lines(const uint32_t* d_gtilde_aff, uint32_t* d_lines, hipStream_t st);
 int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* d_Y, uint32_t* d_bases,
                   uint32_t* d_binf, const uint8_t* d_msgs, uint8_t* d_msgs_canon, hipStream_t st);
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
-             const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, const uint32_t* d_binf_fixed,
+             const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
 int cck_miller_pl_g2(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                      uint32_t* d_f, hipStream_t st);
@@ -43,20 +43,30 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
 int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
                   uint8_t* d_out, hipStream_t st);
 int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
-                 const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, const uint32_t* d_binf,
+                 const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
                  uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, hipStream_t st);
 int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any, uint32_t* d_partial,
                    hipStream_t st);
 int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t* d_flag, hipStream_t st);
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
-                 const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table,
+                 const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
                  const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
 }
 
 namespace {
 
-constexpr int NWIN = 32, WENT = 255;
+// fixed-base window tables (fixed.h): per base ceil(256 / wbits) windows of 2^wbits - 1 affine entries
+static inline size_t tab_words(int group, int wbits) {
+    return (size_t)((256 + wbits - 1) / wbits) * (((size_t)1 << wbits) - 1) * (group == 1 ? 24 : 48);
+}
+static inline size_t tab_nwin(int wbits) { return (size_t)((256 + wbits - 1) / wbits); }
+// shared-verkey tables: 16-bit windows (half the additions of 8-bit ones; 100/200 MB per G1/G2 base in
+// HBM); COCONUT_TABLE_BITS=8 selects the small L2-resident form
+static int verkey_table_bits() {
+    const char* e = getenv("COCONUT_TABLE_BITS");
+    return (e && atoi(e) == 8) ? 8 : 16;
+}
 constexpr int PREP_SLOTS = 14;  // soa.h
 
 struct DevBuf {
@@ -100,6 +110,7 @@ struct cc_ctx {
     DevBuf vk_inf;       // (q + 3) flags
     DevBuf table;        // fixed-base tables for Y~[0..q), g~ and X~ (q + 2 bases; X~ for RLC)
     DevBuf table_inf;    // q + 2 base flags
+    int wbits = 16;      // window width of `table`
     uint32_t X_inf = 0;
     // workspaces
     DevBuf in_s1, in_s2, in_msgs, in_vkX, in_vkY, in_aux[6];
@@ -281,14 +292,15 @@ static cc_status rebuild_tables(cc_ctx* c) {
     int og = oth_group(c->mode);
     size_t aw = aff_words(og);
     int nb = (int)c->q + 2;
-    if (c->table.ensure((size_t)nb * NWIN * WENT * aw * 4)) return CC_ERR_HIP;
+    c->wbits = verkey_table_bits();
+    if (c->table.ensure((size_t)nb * tab_words(og, c->wbits) * 4)) return CC_ERR_HIP;
     if (c->table_inf.ensure((size_t)nb * 4)) return CC_ERR_HIP;
     // [Y~..., g~, X~] are contiguous in vk_aff (X~ at 0, Y~ at 1..q, g~ at q+1, X~ again at q+2)
     HIPCK(hipMemcpyAsync(c->table_inf.p, c->vk_inf.as<uint32_t>() + 1, (size_t)nb * 4, hipMemcpyDeviceToDevice,
                          c->stream));
     DevBuf pw;
-    if (pw.ensure((size_t)nb * NWIN * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
-    KCK(cck_build_table(og, nb, c->vk_aff.as<uint32_t>() + aw, c->table_inf.as<uint32_t>(), pw.as<uint32_t>(),
+    if (pw.ensure((size_t)nb * tab_nwin(c->wbits) * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
+    KCK(cck_build_table(og, nb, c->wbits, c->vk_aff.as<uint32_t>() + aw, c->table_inf.as<uint32_t>(), pw.as<uint32_t>(),
                         c->table.as<uint32_t>(), c->stream));
     HIPCK(hipStreamSynchronize(c->stream));
     pw.release();
@@ -374,7 +386,7 @@ static cc_status launch_verify(cc_ctx* c, size_t n, size_t q, int fixed, const u
                                const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_prep(c->mode, fixed, n, (int)q, d_s1, d_s2, d_msgs, c->vk_aff.as<uint32_t>(), c->X_inf,
-                 c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(), c->vkb.as<uint32_t>(),
+                 c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->vkb.as<uint32_t>(),
                  c->vkbinf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
@@ -449,7 +461,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_prep_rlc(c->mode, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
-                     c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
+                     c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
                      c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
@@ -563,14 +575,14 @@ cc_status cc_fixed_base_mul(cc_ctx* c, int group, const uint8_t* base, size_t n,
     size_t eb = group == 1 ? 97 : 192, aw = aff_words(group);
     hipStream_t st = c->stream;
     DevBuf aff, inf, pw, table, ks, o;
-    if (aff.ensure(aw * 4) || inf.ensure(4) || pw.ensure((size_t)NWIN * (group == 1 ? 36 : 72) * 4) ||
-        table.ensure((size_t)NWIN * WENT * aw * 4) || ks.ensure(n * 48) || o.ensure(n * eb))
+    if (aff.ensure(aw * 4) || inf.ensure(4) || pw.ensure(tab_nwin(8) * (group == 1 ? 36 : 72) * 4) ||
+        table.ensure(tab_words(group, 8) * 4) || ks.ensure(n * 48) || o.ensure(n * eb))
         return CC_ERR_HIP;
     cc_status s = decode_points_host(c, group, 1, base, aff.as<uint32_t>(), inf.as<uint32_t>());
     if (s) return s;
     uint32_t binf = 0;
     HIPCK(hipMemcpy(&binf, inf.p, 4, hipMemcpyDeviceToHost));
-    KCK(cck_build_table(group, 1, aff.as<uint32_t>(), inf.as<uint32_t>(), pw.as<uint32_t>(), table.as<uint32_t>(), st));
+    KCK(cck_build_table(group, 1, 8, aff.as<uint32_t>(), inf.as<uint32_t>(), pw.as<uint32_t>(), table.as<uint32_t>(), st));
     HIPCK(hipMemcpyAsync(ks.p, scalars, n * 48, hipMemcpyHostToDevice, st));
     KCK(cck_fixed_mul(group, n, ks.as<uint8_t>(), table.as<uint32_t>(), binf, o.as<uint8_t>(), st));
     HIPCK(hipMemcpyAsync(out, o.p, n * eb, hipMemcpyDeviceToHost, st));
@@ -713,14 +725,14 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
         for (size_t j = 0; j < q; j++) memcpy(&enc[(r * (q + 1) + 1 + j) * ob], Y + (k * q + j) * ob, ob);
     }
     if (c->iss_ids.ensure(n_iss * 8) || c->iss_aff.ensure(nb * aw * 4) || c->iss_inf.ensure(nb * 4) ||
-        c->iss_table.ensure(nb * NWIN * WENT * aw * 4))
+        c->iss_table.ensure(nb * tab_words(og, 8) * 4))
         return CC_ERR_HIP;
     cc_status s = decode_points_host(c, og, nb, enc.data(), c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>());
     if (s) return s;
     HIPCK(hipMemcpy(c->iss_ids.p, sid.data(), n_iss * 8, hipMemcpyHostToDevice));
     DevBuf pw;
-    if (pw.ensure(nb * NWIN * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
-    KCK(cck_build_table(og, (int)nb, c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>(), pw.as<uint32_t>(),
+    if (pw.ensure(nb * tab_nwin(8) * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
+    KCK(cck_build_table(og, (int)nb, 8, c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>(), pw.as<uint32_t>(),
                         c->iss_table.as<uint32_t>(), c->stream));
     HIPCK(hipStreamSynchronize(c->stream));
     pw.release();
@@ -807,8 +819,8 @@ static cc_status launch_pok(cc_ctx* c, size_t n, size_t q, size_t r, const uint8
                             hipStream_t st) {
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_prep_pok(c->mode, n, (int)q, (int)r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_idx,
-                     c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(), c->table_inf.as<uint32_t>(),
-                     c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
+                     c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(), c->wbits,
+                     c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));

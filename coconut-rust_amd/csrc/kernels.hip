@@ -13,6 +13,7 @@
 // Group assignment is a template parameter: kSigG2 (reference default, sigma in G2, vk in G1)
 // or SigG1 (sigma in G1, vk in G2).
 #include "codec.h"
+#include "fixed.h"
 #include "pairing.h"
 #include "soa.h"
 #include "tower_pl.h"  // pl::swp (lane-pair exchange)
@@ -20,10 +21,6 @@
 using namespace cc;
 
 namespace {
-
-constexpr int WIN = 8;                 // fixed-base window bits
-constexpr int NWIN = 32;               // 256 / WIN windows per scalar
-constexpr int WENT = (1 << WIN) - 1;   // entries per window (digit 1..255)
 
 // AoS point loads (table entries, constants): F words contiguous
 template <class F>
@@ -90,14 +87,15 @@ __global__ __launch_bounds__(64) void k_decode_points(size_t n, const uint8_t* _
     inf[i] = ok ? 0u : 1u;
 }
 
-// ================================================================ fixed-base tables
-// T1: per (base j, window w): 2^(8w) * B_j (Jacobian, AoS)
+// ================================================================ fixed-base tables (fixed.h layout)
+// T1: per (base j, window w): 2^(wbits w) * B_j (Jacobian, AoS)
 template <class F>
-__global__ __launch_bounds__(64) void k_table_pow2(int nbases, const uint32_t* __restrict__ bases, const uint32_t* __restrict__ inf,
-                             uint32_t* __restrict__ pw) {
+__global__ __launch_bounds__(64) void k_table_pow2(int nbases, int wbits, const uint32_t* __restrict__ bases,
+                                                   const uint32_t* __restrict__ inf, uint32_t* __restrict__ pw) {
+    const int nwin = ft_nwin(wbits);
     int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= nbases * NWIN) return;
-    int j = t / NWIN, w = t % NWIN;
+    if (t >= nbases * nwin) return;
+    int j = t / nwin, w = t % nwin;
     Jac<F> P;
     if (inf[j]) {
         jac_set_inf(P);
@@ -105,36 +103,88 @@ __global__ __launch_bounds__(64) void k_table_pow2(int nbases, const uint32_t* _
         Aff<F> b;
         ld_aff_aos<F>(b, bases + (size_t)j * (sizeof(Aff<F>) / 4));
         jac_from_aff(P, b);
-        for (int k = 0; k < WIN * w; k++) jac_dbl(P, P);
+        for (int k = 0; k < wbits * w; k++) jac_dbl(P, P);
     }
     st_jac_aos<F>(pw + (size_t)t * (sizeof(Jac<F>) / 4), P);
 }
 
-// T2: per (j, w, d): d * 2^(8w) * B_j, affine AoS entry
+// T2: entries d * 2^(wbits w) * B_j for a run of FILL_RUN consecutive digits per thread: the first by
+// double-and-add, the rest by one mixed addition each, then ONE inversion for the whole run
+// (Montgomery's trick) to write them affine.  Identity entries are written as (0, 0).
+constexpr int FILL_RUN = 32;
 template <class F>
-__global__ __launch_bounds__(64) void k_table_fill(int nbases, const uint32_t* __restrict__ pw, uint32_t* __restrict__ table) {
-    size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (t >= (size_t)nbases * NWIN * WENT) return;
-    int d = (int)(t % WENT) + 1;
-    size_t jw = t / WENT;
-    Jac<F> P, acc;
+__global__ __launch_bounds__(64) void k_table_fill(int nbases, int wbits, const uint32_t* __restrict__ pw,
+                                                   uint32_t* __restrict__ table) {
+    using T = FT<F>;
+    constexpr int EW = sizeof(Aff<F>) / 4, PW = sizeof(F) / 4;
+    const int nwin = ft_nwin(wbits);
+    const size_t went = ft_went(wbits);
+    const size_t runs = (went + FILL_RUN - 1) / FILL_RUN;
+    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (t >= (size_t)nbases * nwin * runs) return;
+    const size_t jw = t / runs, r = t % runs;
+    const size_t d0 = r * FILL_RUN + 1;
+    const int cnt = (int)(went - d0 + 1 < (size_t)FILL_RUN ? went - d0 + 1 : FILL_RUN);
+    uint32_t* out = table + (jw * went + d0 - 1) * EW;
+    Jac<F> P;
     ld_jac_aos<F>(P, pw + jw * (sizeof(Jac<F>) / 4));
-    jac_set_inf(acc);
-    for (int b = WIN - 1; b >= 0; b--) {
-        jac_dbl(acc, acc);
-        if ((d >> b) & 1) jac_add(acc, acc, P);
+    Aff<F> Pa;
+    if (!jac_to_aff(Pa, P)) {
+        for (int i = 0; i < cnt * EW; i++) out[i] = 0u;
+        return;
     }
-    Aff<F> a;
-    jac_to_aff(a, acc);  // entries are never O for a non-identity base of order r
-    st_aff_aos<F>(table + t * (sizeof(Aff<F>) / 4), a);
+    Jac<F> acc;
+    jac_set_inf(acc);
+    for (int b = wbits - 1; b >= 0; b--) {
+        jac_dbl(acc, acc);
+        if ((d0 >> b) & 1) jac_add_aff(acc, acc, Pa);
+    }
+    F z[FILL_RUN], pre[FILL_RUN];
+    F run;
+    T::one(run);
+#pragma unroll 1
+    for (int i = 0; i < cnt; i++) {
+        if (i) jac_add_aff(acc, acc, Pa);
+        uint32_t* o = out + (size_t)i * EW;
+        const uint32_t* xw = reinterpret_cast<const uint32_t*>(&acc.x);
+        const uint32_t* yw = reinterpret_cast<const uint32_t*>(&acc.y);
+        for (int c = 0; c < PW; c++) {
+            o[c] = xw[c];
+            o[PW + c] = yw[c];
+        }
+        z[i] = acc.z;
+        pre[i] = run;
+        if (!jac_is_inf(acc)) T::mul(run, run, acc.z);
+    }
+    F inv;
+    T::inv(inv, run);
+#pragma unroll 1
+    for (int i = cnt - 1; i >= 0; i--) {
+        uint32_t* o = out + (size_t)i * EW;
+        if (T::is_zero(z[i])) {
+            for (int c = 0; c < EW; c++) o[c] = 0u;
+            continue;
+        }
+        F zi, zi2, v;
+        T::mul(zi, inv, pre[i]);
+        T::mul(inv, inv, z[i]);
+        T::sqr(zi2, zi);
+        uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+        for (int c = 0; c < PW; c++) vw[c] = o[c];
+        T::mul(v, v, zi2);
+        for (int c = 0; c < PW; c++) o[c] = vw[c];
+        T::mul(zi2, zi2, zi);
+        for (int c = 0; c < PW; c++) vw[c] = o[PW + c];
+        T::mul(v, v, zi2);
+        for (int c = 0; c < PW; c++) o[PW + c] = vw[c];
+    }
 }
 
 // ================================================================ MSM helpers
 // fixed-base: acc = X~ + sum_j m_j Y~_j using the window tables
 template <class F>
 DEV void msm_fixed(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                   const uint32_t* __restrict__ table, const uint32_t* __restrict__ binf) {
-    constexpr int EW = sizeof(Aff<F>) / 4;
+                   const uint32_t* __restrict__ table, int wbits, const uint32_t* __restrict__ binf) {
     if (Xinf) {
         jac_set_inf(acc);
     } else {
@@ -146,25 +196,15 @@ DEV void msm_fixed(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t* __re
         if (binf[j]) continue;  // uniform across the batch (shared verkey)
         Fr m;
         fr_from_be48(m, msgs + (size_t)j * 48);
-        const uint32_t* tj = table + (size_t)j * NWIN * WENT * EW;
-#pragma unroll 1
-        for (int w = 0; w < NWIN; w++) {
-            uint32_t dgt = (m.v[w >> 2] >> (8 * (w & 3))) & 0xffu;
-            if (dgt) {
-                Aff<F> e;
-                ld_aff_aos<F>(e, tj + ((size_t)w * WENT + dgt - 1) * EW);
-                jac_add_aff(acc, acc, e);
-            }
-        }
+        ft_add<F>(acc, m.v, table, wbits, j, 0, ft_nwin(wbits));
     }
 }
 
 // fixed-base over windows [w0, w1) only, X~ included on request (the lane-pair split of msm_fixed)
 template <class F>
 DEV void msm_fixed_part(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                        bool with_x, const uint32_t* __restrict__ table, const uint32_t* __restrict__ binf, int w0,
-                        int w1) {
-    constexpr int EW = sizeof(Aff<F>) / 4;
+                        bool with_x, const uint32_t* __restrict__ table, int wbits,
+                        const uint32_t* __restrict__ binf, int w0, int w1) {
     if (!with_x || Xinf) {
         jac_set_inf(acc);
     } else {
@@ -176,16 +216,7 @@ DEV void msm_fixed_part(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t*
         if (binf[j]) continue;  // uniform across the batch (shared verkey)
         Fr m;
         fr_from_be48(m, msgs + (size_t)j * 48);
-        const uint32_t* tj = table + (size_t)j * NWIN * WENT * EW;
-#pragma unroll 1
-        for (int w = w0; w < w1; w++) {
-            uint32_t dgt = (m.v[w >> 2] >> (8 * (w & 3))) & 0xffu;
-            if (dgt) {
-                Aff<F> e;
-                ld_aff_aos<F>(e, tj + ((size_t)w * WENT + dgt - 1) * EW);
-                jac_add_aff(acc, acc, e);
-            }
-        }
+        ft_add<F>(acc, m.v, table, wbits, j, w0, w1);
     }
 }
 
@@ -260,7 +291,7 @@ __global__ __launch_bounds__(256) void k_prep_sigg2(size_t n, int q, const uint8
                                                     const uint8_t* __restrict__ s2b,
                                                     const uint8_t* __restrict__ msgs,
                                                     const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                                                    const uint32_t* __restrict__ table,
+                                                    const uint32_t* __restrict__ table, int wbits,
                                                     const uint32_t* __restrict__ binf_fixed,
                                                     uint32_t* __restrict__ vkb, size_t vk_stride,
                                                     const uint32_t* __restrict__ binf_var,
@@ -281,7 +312,7 @@ __global__ __launch_bounds__(256) void k_prep_sigg2(size_t n, int q, const uint8
     }
     Jac<Fp> pr;
     if (kFixed) {
-        msm_fixed<Fp>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, table, binf_fixed);
+        msm_fixed<Fp>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, table, wbits, binf_fixed);
     } else {
         msm_var<Fp>(pr, msgs + i * (size_t)q * 48, q, Soa{vkb, vk_stride}, binf_var, i, vk_stride);
     }
@@ -305,7 +336,7 @@ __global__ __launch_bounds__(256) void k_prep_sigg2_pair(size_t n, int q, const 
                                                          const uint8_t* __restrict__ s2b,
                                                          const uint8_t* __restrict__ msgs,
                                                          const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                                                         const uint32_t* __restrict__ table,
+                                                         const uint32_t* __restrict__ table, int wbits,
                                                          const uint32_t* __restrict__ binf_fixed,
                                                          uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
     const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -323,8 +354,9 @@ __global__ __launch_bounds__(256) void k_prep_sigg2_pair(size_t n, int q, const 
         st_f2(S, slot + 2, i, a.y);
     }
     Jac<Fp> pr, o;
-    msm_fixed_part<Fp>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, h == 0, table, binf_fixed, h ? NWIN / 2 : 0,
-                       h ? NWIN : NWIN / 2);
+    const int nwin = ft_nwin(wbits);
+    msm_fixed_part<Fp>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, h == 0, table, wbits, binf_fixed,
+                       h ? nwin / 2 : 0, h ? nwin : nwin / 2);
     o.x = pl::swp(pr.x);
     o.y = pl::swp(pr.y);
     o.z = pl::swp(pr.z);
@@ -355,7 +387,7 @@ __global__ __launch_bounds__(256) void k_prep_sigg1(size_t n, int q, const uint8
                                                     const uint8_t* __restrict__ s2b,
                                                     const uint8_t* __restrict__ msgs,
                                                     const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                                                    const uint32_t* __restrict__ table,
+                                                    const uint32_t* __restrict__ table, int wbits,
                                                     const uint32_t* __restrict__ binf_fixed,
                                                     uint32_t* __restrict__ vkb, size_t vk_stride,
                                                     const uint32_t* __restrict__ binf_var,
@@ -376,7 +408,7 @@ __global__ __launch_bounds__(256) void k_prep_sigg1(size_t n, int q, const uint8
     }
     Jac<Fp2> pr;
     if (kFixed) {
-        msm_fixed<Fp2>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, table, binf_fixed);
+        msm_fixed<Fp2>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, table, wbits, binf_fixed);
     } else {
         msm_var<Fp2>(pr, msgs + i * (size_t)q * 48, q, Soa{vkb, vk_stride}, binf_var, i, vk_stride);
     }
@@ -443,17 +475,18 @@ int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_o
     return 0;
 }
 
-// table: nbases * 32 * 255 entries; pw scratch: nbases * 32 Jacobian points
-int cck_build_table(int group, int nbases, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
+// table: nbases * ft_base_words(wbits) words (fixed.h); pw scratch: nbases * ft_nwin(wbits) Jacobian points
+int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
                     uint32_t* d_table, hipStream_t st) {
     if (!nbases) return 0;
-    size_t t1 = (size_t)nbases * NWIN, t2 = t1 * WENT;
+    if (wbits != 8 && wbits != 16) return -1;
+    size_t t1 = (size_t)nbases * ft_nwin(wbits), t2 = t1 * ((ft_went(wbits) + FILL_RUN - 1) / FILL_RUN);
     if (group == 1) {
-        hipLaunchKernelGGL(k_table_pow2<Fp>, dim3(nblocks(t1, 64)), dim3(64), 0, st, nbases, d_bases, d_inf, d_pw);
-        hipLaunchKernelGGL(k_table_fill<Fp>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, d_pw, d_table);
+        hipLaunchKernelGGL(k_table_pow2<Fp>, dim3(nblocks(t1, 64)), dim3(64), 0, st, nbases, wbits, d_bases, d_inf, d_pw);
+        hipLaunchKernelGGL(k_table_fill<Fp>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, wbits, d_pw, d_table);
     } else {
-        hipLaunchKernelGGL(k_table_pow2<Fp2>, dim3(nblocks(t1, 64)), dim3(64), 0, st, nbases, d_bases, d_inf, d_pw);
-        hipLaunchKernelGGL(k_table_fill<Fp2>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, d_pw, d_table);
+        hipLaunchKernelGGL(k_table_pow2<Fp2>, dim3(nblocks(t1, 64)), dim3(64), 0, st, nbases, wbits, d_bases, d_inf, d_pw);
+        hipLaunchKernelGGL(k_table_fill<Fp2>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, wbits, d_pw, d_table);
     }
     CC_CHECK(hipGetLastError());
     return 0;
@@ -480,24 +513,24 @@ int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* 
 
 // fixed != 0: shared verkey tables; else per-credential bases decoded by cck_decode_vk
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
-             const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, const uint32_t* d_binf_fixed,
+             const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st) {
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
     if (mode == 0) {
         if (fixed)
             hipLaunchKernelGGL(k_prep_sigg2_pair, dim3(nblocks(2 * n, 256)), b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff,
-                               Xinf, d_table, d_binf_fixed, d_prep, d_flags);
+                               Xinf, d_table, wbits, d_binf_fixed, d_prep, d_flags);
         else
             hipLaunchKernelGGL(k_prep_sigg2<false>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
-                               d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
+                               wbits, d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
     } else {
         if (fixed)
             hipLaunchKernelGGL(k_prep_sigg1<true>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
-                               d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
+                               wbits, d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
         else
             hipLaunchKernelGGL(k_prep_sigg1<false>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
-                               d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
+                               wbits, d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
     }
     CC_CHECK(hipGetLastError());
     return 0;

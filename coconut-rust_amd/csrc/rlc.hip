@@ -20,6 +20,7 @@
 //   k_rlc_partial_out / k_rlc_combine   : 145-word partial (Fp12 Montgomery words + identity flag),
 //                                         and the product of gathered partials ahead of k_fexp
 #include "codec.h"
+#include "fixed.h"
 #include "fr.h"
 #include "pairing.h"
 #include "soa.h"
@@ -27,31 +28,6 @@
 using namespace cc;
 
 namespace {
-
-constexpr int NWIN = 32, WENT = 255;
-
-template <class F>
-DEV void ld_aff_words(Aff<F>& a, const uint32_t* p) {
-    uint32_t* d = reinterpret_cast<uint32_t*>(&a);
-#pragma unroll
-    for (int k = 0; k < (int)(sizeof(Aff<F>) / 4); k++) d[k] = p[k];
-}
-
-// acc += k * B_j through base j's 8-bit window table; k canonical (8 LE limbs), nwin windows
-template <class F>
-DEV void fixed_add(Jac<F>& acc, const uint32_t k[NR], const uint32_t* table, int j, int nwin) {
-    constexpr int EW = sizeof(Aff<F>) / 4;
-    const uint32_t* tj = table + (size_t)j * NWIN * WENT * EW;
-#pragma unroll 1
-    for (int w = 0; w < nwin; w++) {
-        const uint32_t d = (k[w >> 2] >> (8 * (w & 3))) & 0xffu;
-        if (d) {
-            Aff<F> e;
-            ld_aff_words<F>(e, tj + ((size_t)w * WENT + d - 1) * EW);
-            jac_add_aff(acc, acc, e);
-        }
-    }
-}
 
 // G1 Jacobian -> line-evaluation form (X Z, Y, Z^3) in three SoA slots
 DEV void st_eval(const Soa& S, int slot, size_t i, const Jac<Fp>& P) {
@@ -73,7 +49,7 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg2(size_t n, int q, uint64_
                                                         const uint8_t* __restrict__ s1b,
                                                         const uint8_t* __restrict__ s2b,
                                                         const uint8_t* __restrict__ msgs,
-                                                        const uint32_t* __restrict__ table,
+                                                        const uint32_t* __restrict__ table, int wbits,
                                                         const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
                                                         uint32_t* __restrict__ flags, uint32_t* __restrict__ any) {
     const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -96,19 +72,20 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg2(size_t n, int q, uint64_
     rlc_delta(d, kk, base_index + i);
     Jac<Fp> acc;
     jac_set_inf(acc);
-    if (!binf[q + 1]) fixed_add<Fp>(acc, d, table, q + 1, 16);  // delta X~ (128-bit delta: 16 windows)
+    const int nwin = ft_nwin(wbits);
+    if (!binf[q + 1]) ft_add<Fp>(acc, d, table, wbits, q + 1, 0, nwin / 2);  // delta X~ (128-bit delta)
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
         fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
         uint32_t dm[NR];
         fr_mul_canon(dm, d, m.v);
-        fixed_add<Fp>(acc, dm, table, j, NWIN);
+        ft_add<Fp>(acc, dm, table, wbits, j, 0, nwin);
     }
     if (jac_is_inf(acc)) fl |= 4u;
     st_eval(S, S_P1, i, acc);
     jac_set_inf(acc);
-    if (!binf[q]) fixed_add<Fp>(acc, d, table, q, 16);  // delta g~
+    if (!binf[q]) ft_add<Fp>(acc, d, table, wbits, q, 0, nwin / 2);  // delta g~
     if (jac_is_inf(acc)) fl |= 16u;
     st_eval(S, S_P2, i, acc);
     flags[i] = fl;
@@ -120,7 +97,7 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg1(size_t n, int q, uint64_
                                                         const uint8_t* __restrict__ s1b,
                                                         const uint8_t* __restrict__ s2b,
                                                         const uint8_t* __restrict__ msgs,
-                                                        const uint32_t* __restrict__ table,
+                                                        const uint32_t* __restrict__ table, int wbits,
                                                         const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
                                                         uint32_t* __restrict__ flags, uint32_t* __restrict__ any) {
     const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -153,14 +130,15 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg1(size_t n, int q, uint64_
     }
     Jac<Fp2> acc;
     jac_set_inf(acc);
-    if (!binf[q + 1]) fixed_add<Fp2>(acc, d, table, q + 1, 16);
+    const int nwin = ft_nwin(wbits);
+    if (!binf[q + 1]) ft_add<Fp2>(acc, d, table, wbits, q + 1, 0, nwin / 2);
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
         fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
         uint32_t dm[NR];
         fr_mul_canon(dm, d, m.v);
-        fixed_add<Fp2>(acc, dm, table, j, NWIN);
+        ft_add<Fp2>(acc, dm, table, wbits, j, 0, nwin);
     }
     Aff<Fp2> a2;
     if (!jac_to_aff(a2, acc)) fl |= 4u;
@@ -220,16 +198,16 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 extern "C" {
 
 int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
-                 const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, const uint32_t* d_binf,
+                 const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
                  uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, hipStream_t st) {
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
     if (mode == 0)
         hipLaunchKernelGGL(k_prep_rlc_sigg2, g, b, 0, st, n, q, base_index, d_key, d_s1, d_s2, d_msgs, d_table,
-                           d_binf, d_prep, d_flags, d_any);
+                           wbits, d_binf, d_prep, d_flags, d_any);
     else
         hipLaunchKernelGGL(k_prep_rlc_sigg1, g, b, 0, st, n, q, base_index, d_key, d_s1, d_s2, d_msgs, d_table,
-                           d_binf, d_prep, d_flags, d_any);
+                           wbits, d_binf, d_prep, d_flags, d_any);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

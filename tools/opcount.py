@@ -453,12 +453,16 @@ def decode(g, enc):
     return a if g.on_curve(a) else None
 
 
-def fixed_table_mul_add(g, acc, k, base_aff, w0, w1):
-    """kernels.hip msm_fixed_part: acc += sum over 8-bit windows w0..w1-1 of digit * 2^(8w) * base."""
+VK_WBITS = 16  # shared-verkey tables (fixed.h; capi.cpp verkey_table_bits)
+
+
+def fixed_table_mul_add(g, acc, k, base_aff, w0, w1, wbits=8):
+    """fixed.h ft_add: acc += sum over wbits-bit windows w0..w1-1 of digit * 2^(wbits w) * base."""
+    mask = (1 << wbits) - 1
     for w in range(w0, w1):
-        d = (k >> (8 * w)) & 0xFF
+        d = (k >> (wbits * w)) & mask
         if d:
-            e = mul_aff(g, base_aff, d << (8 * w))  # the table entry (precomputed, not counted)
+            e = mul_aff(g, base_aff, d << (wbits * w))  # the table entry (precomputed, not counted)
             acc = g.add_aff(acc, e)
     return acc
 
@@ -487,9 +491,10 @@ def verify_sigg2(cred, vk_aff, gtil_aff, q):
     # lane pair: windows 0..15 (with X) on the even lane, 16..31 on the odd lane, then one jac_add
     lo = (X[0], X[1], 1) if X else G1.inf()
     hi = G1.inf()
+    nw = 256 // VK_WBITS
     for j in range(q):
-        lo = fixed_table_mul_add(G1, lo, msgs[j], Ys[j], 0, 16)
-        hi = fixed_table_mul_add(G1, hi, msgs[j], Ys[j], 16, 32)
+        lo = fixed_table_mul_add(G1, lo, msgs[j], Ys[j], 0, nw // 2, VK_WBITS)
+        hi = fixed_table_mul_add(G1, hi, msgs[j], Ys[j], nw // 2, nw, VK_WBITS)
     pr = G1.add_j(lo, hi)
     pr_inf = G1.is_inf(pr)
     pe = None
@@ -519,7 +524,7 @@ def verify_sigg1(cred, vk_aff, gtil_aff, q):
     X, Ys = vk_aff
     acc = (X[0], X[1], F2_ONE) if X else G2.inf()
     for j in range(q):
-        acc = fixed_table_mul_add(G2, acc, msgs[j], Ys[j], 0, 32)
+        acc = fixed_table_mul_add(G2, acc, msgs[j], Ys[j], 0, 256 // VK_WBITS, VK_WBITS)
     pr = G2.to_aff(acc)
     counts["prep"] = C.take()
     # pair 0: (pr, sigma_1); pair 1: (g~ [precomputed lines: no line cost], -sigma_2)
@@ -680,12 +685,13 @@ def pok_sigg2(d, p, vk_aff, gtil):
     Ja = decode(G1, bytes.fromhex(p["J"]))
     resp = [int(h, 16) % R for h in p["responses"]]
     chal = int(p["chal"], 16) % R
-    acc = fixed_table_mul_add(G1, G1.inf(), resp[0], gtil, 0, 32)
+    nw = 256 // VK_WBITS
+    acc = fixed_table_mul_add(G1, G1.inf(), resp[0], gtil, 0, nw, VK_WBITS)
     slot = 1
     for h in range(q):
         if h in rev:
             continue
-        acc = fixed_table_mul_add(G1, acc, resp[slot], Ys[h], 0, 32)
+        acc = fixed_table_mul_add(G1, acc, resp[slot], Ys[h], 0, nw, VK_WBITS)
         slot += 1
     if Ja:
         sacc = G1.inf()
@@ -702,7 +708,7 @@ def pok_sigg2(d, p, vk_aff, gtil):
     if Ja:
         jp = G1.add_aff(jp, Ja)
     for z, h in enumerate(rev):
-        jp = fixed_table_mul_add(G1, jp, int(p["revealed_msgs"][z], 16) % R, Ys[h], 0, 32)
+        jp = fixed_table_mul_add(G1, jp, int(p["revealed_msgs"][z], 16) % R, Ys[h], 0, nw, VK_WBITS)
     jinf = G1.is_inf(jp)
     pe = (fmul(jp[0], jp[2]), jp[1], fmul(fmul(jp[2], jp[2]), jp[2])) if not jinf else (0, 0, 0)
     counts["prep"] = C.take()
