@@ -266,6 +266,16 @@ def verkey_aggregate_ids(ctx: Context, n: int, length: int, t: int, ids):
     return oX[:n * ob].tobytes(), oY[:n * q * ob].tobytes()
 
 
+def subgroup_check(ctx: Context, group: int, points: bytes):
+    """Per point: 0 identity / invalid encoding, 1 on-curve outside the subgroup, 2 in G1/G2."""
+    eb = G1_BYTES if group == 1 else G2_BYTES
+    n = len(points) // eb
+    st = np.zeros(max(n, 1), dtype=np.uint8)
+    p, k = buf(points)
+    check(lib.cc_subgroup_check(ctx.h, group, n, p, ctypes.c_void_p(st.ctypes.data)), "cc_subgroup_check")
+    return st[:n]
+
+
 # Standard BLS12-381 generators (amcl_wrapper encodings) — public curve constants.
 G1_GENERATOR = bytes.fromhex(
     "04"

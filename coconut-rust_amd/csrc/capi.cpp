@@ -20,6 +20,7 @@ int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_o
 int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
                     uint32_t* d_table, hipStream_t st);
 int cck_gtilde_lines(const uint32_t* d_gtilde_aff, uint32_t* d_lines, hipStream_t st);
+int cck_subgroup(int group, size_t n, const uint8_t* d_bytes, uint8_t* d_status, hipStream_t st);
 int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* d_Y, uint32_t* d_bases,
                   uint32_t* d_binf, const uint8_t* d_msgs, uint8_t* d_msgs_canon, hipStream_t st);
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
@@ -100,6 +101,7 @@ struct cc_ctx {
     hipStream_t stream = nullptr;
     // params
     bool have_params = false;
+    std::vector<uint8_t> gtilde_bytes;  // encoding as given (subgroup status at cc_set_verkey)
     DevBuf gtilde_aff;   // OtherGroup affine (Montgomery, AoS)
     uint32_t gtilde_inf = 0;
     DevBuf gtilde_lines; // SigG1: Miller lines of g~
@@ -111,6 +113,7 @@ struct cc_ctx {
     DevBuf table;        // fixed-base tables for Y~[0..q), g~ and X~ (q + 2 bases; X~ for RLC)
     DevBuf table_inf;    // q + 2 base flags
     int wbits = 16;      // window width of `table`
+    bool vk_subgroup = false;  // X~, Y~ and g~ all in the order-r subgroup (RLC soundness needs it)
     uint32_t X_inf = 0;
     // workspaces
     DevBuf in_s1, in_s2, in_msgs, in_vkX, in_vkY, in_aux[6];
@@ -287,6 +290,17 @@ static cc_status decode_points_host(cc_ctx* c, int group, size_t n, const uint8_
     return CC_OK;
 }
 
+static cc_status subgroup_host(cc_ctx* c, int group, size_t n, const uint8_t* bytes, uint8_t* status) {
+    size_t eb = group == 1 ? 97 : 192;
+    DevBuf tmp, st;
+    if (tmp.ensure(eb * n + 16) || st.ensure(n + 16)) return CC_ERR_HIP;
+    HIPCK(hipMemcpyAsync(tmp.p, bytes, eb * n, hipMemcpyHostToDevice, c->stream));
+    KCK(cck_subgroup(group, n, tmp.as<uint8_t>(), st.as<uint8_t>(), c->stream));
+    HIPCK(hipMemcpyAsync(status, st.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCK(hipStreamSynchronize(c->stream));
+    return CC_OK;
+}
+
 static cc_status rebuild_tables(cc_ctx* c) {
     // bases for the fixed-base tables: Y~[0..q), g~ (PoK Schnorr base), X~ (RLC) -> q + 2 bases
     int og = oth_group(c->mode);
@@ -326,6 +340,7 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
     cc_status s = decode_points_host(c, og, 1, g_tilde, c->gtilde_aff.as<uint32_t>(), inf.as<uint32_t>());
     if (s) return s;
     HIPCK(hipMemcpy(&c->gtilde_inf, inf.p, 4, hipMemcpyDeviceToHost));
+    c->gtilde_bytes.assign(g_tilde, g_tilde + oth_bytes(c->mode));
     inf.release();
     if (c->mode == 1) {
         if (c->gtilde_lines.ensure(68 * 72 * 4)) return CC_ERR_HIP;
@@ -368,6 +383,18 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
     HIPCK(hipMemcpy(c->vk_aff.as<uint32_t>() + (q + 2) * aw, c->vk_aff.p, aw * 4, hipMemcpyDeviceToDevice));
     HIPCK(hipMemcpy(c->vk_inf.as<uint32_t>() + (q + 2), c->vk_inf.p, 4, hipMemcpyDeviceToDevice));
     HIPCK(hipMemcpy(&c->X_inf, c->vk_inf.p, 4, hipMemcpyDeviceToHost));
+    {
+        // subgroup status of the verkey points and g~: RLC accepts only when all are in the subgroup
+        std::vector<uint8_t> st(q + 2);
+        cc_status s2 = subgroup_host(c, og, q + 1, all.data(), st.data());
+        if (s2) return s2;
+        uint8_t gst = 0;
+        s2 = subgroup_host(c, og, 1, c->gtilde_bytes.data(), &gst);
+        if (s2) return s2;
+        bool ok = gst == 2;
+        for (size_t k = 0; k <= q; k++) ok = ok && st[k] == 2;
+        c->vk_subgroup = ok;
+    }
     c->q = q;
     c->have_vk = true;
     return rebuild_tables(c);
@@ -463,13 +490,22 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     KCK(cck_prep_rlc(c->mode, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
                      c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
                      c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), st));
+    if (!c->vk_subgroup) {
+        // a verkey / g~ point outside the subgroup: the linear-combination argument does not hold,
+        // so the batch is never accepted here and the caller verifies per credential (exact)
+        static const uint32_t one = 1;
+        HIPCK(hipMemcpyAsync(c->rlc_any.p, &one, 4, hipMemcpyHostToDevice, st));
+    }
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st, 1));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_rlc_reduce(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,
                        st));
-    if (c->timing) (void)hipEventRecord(c->ev[3], st);
+    if (c->timing) {
+        (void)hipEventRecord(c->ev[3], st);
+        collect_timing(c);
+    }
     return CC_OK;
 }
 
@@ -694,6 +730,15 @@ cc_status cc_verkey_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, s
     if (q) HIPCK(hipMemcpyAsync(outY, d_oY.p, ntask_y * ob, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     return CC_OK;
+}
+
+// ---------------------------------------------------------------- codec: subgroup membership (§8(f) row 1)
+cc_status cc_subgroup_check(cc_ctx* c, int group, size_t n, const uint8_t* points, uint8_t* status) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || (group != 1 && group != 2) || (n && (!points || !status))) return CC_ERR_DECODE;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    return subgroup_host(c, group, n, points, status);
 }
 
 // ---------------------------------------------------------------- issuer table (config 4)

@@ -16,6 +16,7 @@
 #include "fixed.h"
 #include "pairing.h"
 #include "soa.h"
+#include "subgroup.h"
 #include "tower_pl.h"  // pl::swp (lane-pair exchange)
 
 using namespace cc;
@@ -85,6 +86,29 @@ __global__ __launch_bounds__(64) void k_decode_points(size_t n, const uint8_t* _
     bool ok = decode_point<F>(a, bytes + i * enc_bytes<F>());
     st_aff_aos<F>(out + i * (sizeof(Aff<F>) / 4), a);
     inf[i] = ok ? 0u : 1u;
+}
+
+// ================================================================ subgroup membership (subgroup.h)
+// status per point: 0 = identity (AMCL decodes a bad encoding / off-curve point to infinity),
+// 1 = on the curve but outside the order-r subgroup, 2 = in G1 / G2
+template <class F>
+DEV bool in_subgroup(const Aff<F>& a);
+template <>
+DEV bool in_subgroup<Fp>(const Aff<Fp>& a) { return g1_in_subgroup(a); }
+template <>
+DEV bool in_subgroup<Fp2>(const Aff<Fp2>& a) { return g2_in_subgroup(a); }
+
+template <class F>
+__global__ __launch_bounds__(64) void k_subgroup(size_t n, const uint8_t* __restrict__ bytes,
+                                                 uint8_t* __restrict__ status) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Aff<F> a;
+    if (!decode_point<F>(a, bytes + i * enc_bytes<F>())) {
+        status[i] = 0;
+        return;
+    }
+    status[i] = in_subgroup<F>(a) ? 2 : 1;
 }
 
 // ================================================================ fixed-base tables (fixed.h layout)
@@ -488,6 +512,16 @@ int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, c
         hipLaunchKernelGGL(k_table_pow2<Fp2>, dim3(nblocks(t1, 64)), dim3(64), 0, st, nbases, wbits, d_bases, d_inf, d_pw);
         hipLaunchKernelGGL(k_table_fill<Fp2>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, wbits, d_pw, d_table);
     }
+    CC_CHECK(hipGetLastError());
+    return 0;
+}
+
+int cck_subgroup(int group, size_t n, const uint8_t* d_bytes, uint8_t* d_status, hipStream_t st) {
+    if (!n) return 0;
+    if (group == 1)
+        hipLaunchKernelGGL(k_subgroup<Fp>, dim3(nblocks(n, 64)), dim3(64), 0, st, n, d_bytes, d_status);
+    else
+        hipLaunchKernelGGL(k_subgroup<Fp2>, dim3(nblocks(n, 64)), dim3(64), 0, st, n, d_bytes, d_status);
     CC_CHECK(hipGetLastError());
     return 0;
 }

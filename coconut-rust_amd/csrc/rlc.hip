@@ -24,6 +24,7 @@
 #include "fr.h"
 #include "pairing.h"
 #include "soa.h"
+#include "subgroup.h"
 
 using namespace cc;
 
@@ -59,9 +60,11 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg2(size_t n, int q, uint64_
     {
         Aff<Fp2> a;
         if (!g2_decode(a, s1b + i * 192)) fl |= 1u;
+        else if (!g2_in_subgroup(a)) fl |= 32u;
         st_f2(S, S_Q1, i, a.x);
         st_f2(S, S_Q1 + 2, i, a.y);
         if (!g2_decode(a, s2b + i * 192)) fl |= 2u;
+        else if (!g2_in_subgroup(a)) fl |= 32u;
         f2_neg(a.y, a.y);
         st_f2(S, S_Q2, i, a.x);
         st_f2(S, S_Q2 + 2, i, a.y);
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg2(size_t n, int q, uint64_
     if (jac_is_inf(acc)) fl |= 16u;
     st_eval(S, S_P2, i, acc);
     flags[i] = fl;
-    if (fl & 3u) atomicOr(any, 1u);
+    if (fl & 35u) atomicOr(any, 1u);  // identity or non-subgroup sigma: the batch falls back
 }
 
 __global__ __launch_bounds__(256) void k_prep_rlc_sigg1(size_t n, int q, uint64_t base_index,
@@ -111,12 +114,14 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg1(size_t n, int q, uint64_
     {
         Aff<Fp> a;
         if (!g1_decode(a, s1b + i * 97)) fl |= 1u;
+        else if (!g1_in_subgroup(a)) fl |= 32u;
         st_fp(S, S_P1, i, a.x);
         st_fp(S, S_P1 + 1, i, a.y);
         // -delta sigma_2 (variable base, 128-bit double-and-add)
         Jac<Fp> s;
         jac_set_inf(s);
         if (g1_decode(a, s2b + i * 97)) {
+            if (!g1_in_subgroup(a)) fl |= 32u;
             for (int b = 127; b >= 0; b--) {
                 jac_dbl(s, s);
                 if ((d[b >> 5] >> (b & 31)) & 1u) jac_add_aff(s, s, a);
@@ -145,7 +150,7 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg1(size_t n, int q, uint64_
     st_f2(S, S_Q1, i, a2.x);
     st_f2(S, S_Q1 + 2, i, a2.y);
     flags[i] = fl;
-    if (fl & 3u) atomicOr(any, 1u);
+    if (fl & 35u) atomicOr(any, 1u);  // identity or non-subgroup sigma: the batch falls back
 }
 
 // out[t] = in[2t] * in[2t+1] (in[2t] alone for an odd tail); SoA strides n_in / n_out

@@ -45,7 +45,7 @@ DEV void ld_f2_aos(Fp2& a, const uint32_t* p) {
 // Prep SoA slots written by k_prep_* / k_prep_pok and read by the Miller kernels:
 //   Q1 0..3 | Q2 4..7 | P1 8..10 (px, py, pz) | P2 11..13 (pz only in RLC mode) ; flags word per lane:
 //   bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 pair-0 degenerate (pr = O), bit3 PoK Schnorr failed,
-//   bit4 pair-1 degenerate (RLC: delta * point = O)
+//   bit4 pair-1 degenerate (RLC: delta * point = O), bit5 sigma outside G1/G2 (RLC: forces fallback)
 enum { S_Q1 = 0, S_Q2 = 4, S_P1 = 8, S_P2 = 11, PREP_SLOTS = 14 };
 constexpr int NLINES = 68;  // Miller steps: 63 doublings + 5 additions
 

@@ -170,6 +170,14 @@ cc_status cc_pok_verify_batch_device(cc_ctx* ctx, size_t n, size_t q, size_t r, 
                                      const uint8_t* d_revealed_msgs, uint8_t* d_verdicts, uint8_t* d_gt_or_null,
                                      void* stream);
 
+/* Codec check: decode n encodings of `group` (1 = G1 97 B, 2 = G2 192 B) and
+ * report per point 0 = identity (AMCL maps a bad prefix / off-curve point to infinity), 1 = on the
+ * curve but outside the order-r subgroup, 2 = in G1 / G2.  The reference never tests membership on
+ * verify, so cc_verify_batch keeps its semantics; the RLC batch mode uses the same tests internally
+ * (a sigma or verkey point outside the subgroup makes the batch fall back to per-credential).
+ * Tests: G1 phi(P) == -[x^2] P, G2 psi(Q) == [x] Q (eprint 2021/1130, 2022/352). */
+cc_status cc_subgroup_check(cc_ctx* ctx, int group, size_t n, const uint8_t* points, uint8_t* status);
+
 /* Batch fixed-base scalar multiplication out_i = k_i * base (group 1 = G1, 2 = G2); scalars n x 48 B
  * big-endian Fr, out n encodings.  The keygen derivation g~ * x_i (reference src/keygen.rs:27-32)
  * and the issuer's h^e (src/signature.rs:423-428) in batch form. */

@@ -251,6 +251,33 @@ def make_pok(mode, q, revealed, nproof, seed):
             "proofs": proofs}
 
 
+def make_subgroup(seed):
+    """Encodings with their codec status (0 identity / invalid, 1 on-curve outside the order-r
+    subgroup, 2 in G1 / G2), status by the DEFINITION [r] P == O and cross-checked by the
+    endomorphism tests the device runs (oracle/subgroup.py)."""
+    from oracle import subgroup as S
+    rng = C.Drbg(seed)
+    h1 = 0x396C8C005555E1568C00AAAB0000AAAB
+    out = {}
+    for name, curve, enc, endo in (("G1", B.G1, B.g1_to_bytes, S.in_g1_endo), ("G2", B.G2, B.g2_to_bytes, S.in_g2_endo)):
+        pts = [curve.mul(curve.gen, rng.fr()) for _ in range(3)]
+        pts += [S.random_curve_point(curve, rng.fr()) for _ in range(4)]
+        if name == "G1":
+            pts.append(curve.mul_any(S.random_curve_point(curve, rng.fr()), h1))  # cofactor-cleared
+        recs = []
+        for Pt in pts:
+            st = 2 if S.in_subgroup_def(curve, Pt) else 1
+            assert (st == 2) == endo(Pt)
+            recs.append({"point": hx(enc(Pt)), "status": st})
+        recs.append({"point": hx(enc(None)), "status": 0})
+        bad = bytearray(enc(pts[0]))
+        bad[-1] ^= 1  # off the curve
+        recs.append({"point": hx(bytes(bad)), "status": 0})
+        out[name] = recs
+        print(f"  subgroup {name}: {[r['status'] for r in recs]}", flush=True)
+    return out
+
+
 def make_pairing_kat(seed):
     """Single-pairing KATs: e(a*G1, b*G2) bytes + the generator pairing."""
     rng = C.Drbg(seed)
@@ -282,6 +309,8 @@ def main():
 
     if want("kat"):
         write("pairing_kat.json", make_pairing_kat(11))
+    if want("subgroup"):
+        write("subgroup.json", make_subgroup(13))
     for mode in ("G2", "G1"):
         if want("verify"):
             write(f"verify_{mode.lower()}_q6.json", make_verify(mode, 6, 30, 2))

@@ -195,3 +195,22 @@ def test_c_oracle_lagrange(oc):
     oc.oc_lagrange(ctypes.c_size_t(3), (ctypes.c_uint64 * 3)(*ids), out)
     for k, i in enumerate(ids):
         assert int.from_bytes(out.raw[48 * k:48 * (k + 1)], "big") == C.lagrange_basis_at_0(set(ids), i)
+
+
+def test_subgroup_fixture_definition_and_endomorphism_tests_agree():
+    """tests/golden/subgroup.json: status by the definition [r] P == O equals the endomorphism tests
+    (G1 phi(P) == -[x^2] P, G2 psi(Q) == [x] Q) the device runs; off-curve / bad encodings decode to
+    the identity (status 0) as AMCL does."""
+    from oracle import bls12_381 as B
+    from oracle import subgroup as S
+    d = golden("subgroup.json")
+    for name, curve, dec, endo in (("G1", B.G1, B.g1_from_bytes, S.in_g1_endo),
+                                   ("G2", B.G2, B.g2_from_bytes, S.in_g2_endo)):
+        for rec in d[name]:
+            Pt = dec(bytes.fromhex(rec["point"]))
+            if Pt is None:
+                assert rec["status"] == 0
+                continue
+            assert curve.on_curve(Pt)
+            assert rec["status"] == (2 if S.in_subgroup_def(curve, Pt) else 1)
+            assert endo(Pt) == (rec["status"] == 2)
