@@ -7,6 +7,6 @@ importing this package on a machine without the built library raises immediately
 """
 from .errors import CoconutError, CoconutErrorKind  # noqa: F401
 from .signature import (GroupMode, Params, Verkey, Signature, Context, verify_batch,  # noqa: F401
-                        signature_aggregate_batch, verkey_aggregate_batch, verkey_aggregate_ids, fixed_base_mul, subgroup_check,
+                        signature_aggregate_batch, verkey_aggregate_batch, verkey_aggregate_ids, fixed_base_mul, subgroup_check, hash_to_curve, hash_msg, params_new,
                         G1_GENERATOR, G2_GENERATOR)
 from .pok_sig import PoKOfSignatureProof, pok_verify_batch  # noqa: F401

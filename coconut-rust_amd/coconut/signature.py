@@ -266,6 +266,43 @@ def verkey_aggregate_ids(ctx: Context, n: int, length: int, t: int, ids):
     return oX[:n * ob].tobytes(), oY[:n * q * ob].tobytes()
 
 
+def _pack(msgs):
+    offs = np.zeros(len(msgs) + 1, dtype=np.uint64)
+    for i, m in enumerate(msgs):
+        offs[i + 1] = offs[i] + len(m)
+    return b"".join(msgs), offs
+
+
+def hash_to_curve(ctx: Context, group: int, msgs: Sequence[bytes]) -> List[bytes]:
+    """amcl_wrapper `from_msg_hash` for a batch of messages on the GPU (cc_hash_to_curve)."""
+    eb = G1_BYTES if group == 1 else G2_BYTES
+    data, offs = _pack(msgs)
+    out = np.zeros(max(len(msgs), 1) * eb, dtype=np.uint8)
+    p, k = buf(data)
+    check(lib.cc_hash_to_curve(ctx.h, group, len(msgs), p, ctypes.c_void_p(offs.ctypes.data),
+                               ctypes.c_void_p(out.ctypes.data)), "cc_hash_to_curve")
+    raw = out.tobytes()
+    return [raw[i * eb:(i + 1) * eb] for i in range(len(msgs))]
+
+
+def hash_msg(ctx: Context, msgs: Sequence[bytes]) -> List[bytes]:
+    data, offs = _pack(msgs)
+    out = np.zeros(max(len(msgs), 1) * 48, dtype=np.uint8)
+    p, k = buf(data)
+    check(lib.cc_hash_msg(ctx.h, len(msgs), p, ctypes.c_void_p(offs.ctypes.data), ctypes.c_void_p(out.ctypes.data)),
+          "cc_hash_msg")
+    raw = out.tobytes()
+    return [raw[i * 48:(i + 1) * 48] for i in range(len(msgs))]
+
+
+def params_new(ctx: Context, msg_count: int, label: bytes) -> Params:
+    """Params::new (src/signature.rs:22-32) in one batch per group."""
+    sg = 2 if ctx.mode == GroupMode.SIG_G2 else 1
+    sig = hash_to_curve(ctx, sg, [label + b" : g"] + [label + b" : y" + str(i).encode() for i in range(msg_count)])
+    gt = hash_to_curve(ctx, 3 - sg, [label + b" : g_tilde"])[0]
+    return Params(g=sig[0], g_tilde=gt, h=sig[1:])
+
+
 def subgroup_check(ctx: Context, group: int, points: bytes):
     """Per point: 0 identity / invalid encoding, 1 on-curve outside the subgroup, 2 in G1/G2."""
     eb = G1_BYTES if group == 1 else G2_BYTES

@@ -21,6 +21,9 @@ int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, c
                     uint32_t* d_table, hipStream_t st);
 int cck_gtilde_lines(const uint32_t* d_gtilde_aff, uint32_t* d_lines, hipStream_t st);
 int cck_subgroup(int group, size_t n, const uint8_t* d_bytes, uint8_t* d_status, hipStream_t st);
+int cck_hash_to_curve(int group, size_t n, const uint8_t* d_data, const uint64_t* d_offsets, uint8_t* d_out,
+                      uint32_t* d_fail, hipStream_t st);
+int cck_shake256_48(size_t n, const uint8_t* d_data, const uint64_t* d_offsets, uint8_t* d_out, hipStream_t st);
 int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* d_Y, uint32_t* d_bases,
                   uint32_t* d_binf, const uint8_t* d_msgs, uint8_t* d_msgs_canon, hipStream_t st);
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
@@ -739,6 +742,55 @@ cc_status cc_subgroup_check(cc_ctx* c, int group, size_t n, const uint8_t* point
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     return subgroup_host(c, group, n, points, status);
+}
+
+// ---------------------------------------------------------------- hash-to-curve (§8(f) row 2)
+static cc_status stage_messages(cc_ctx* c, size_t n, const uint8_t* data, const uint64_t* offsets, DevBuf& d_data,
+                                DevBuf& d_off) {
+    if (offsets[0] != 0) return CC_ERR_DECODE;
+    for (size_t i = 0; i < n; i++)
+        if (offsets[i + 1] < offsets[i]) return CC_ERR_DECODE;
+    const size_t total = offsets[n];
+    if (total && !data) return CC_ERR_DECODE;
+    if (d_data.ensure(total + 16) || d_off.ensure((n + 1) * 8)) return CC_ERR_HIP;
+    if (total) HIPCK(hipMemcpyAsync(d_data.p, data, total, hipMemcpyHostToDevice, c->stream));
+    HIPCK(hipMemcpyAsync(d_off.p, offsets, (n + 1) * 8, hipMemcpyHostToDevice, c->stream));
+    return CC_OK;
+}
+
+cc_status cc_hash_to_curve(cc_ctx* c, int group, size_t n, const uint8_t* data, const uint64_t* offsets, uint8_t* out) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || (group != 1 && group != 2) || (n && (!offsets || !out))) return CC_ERR_DECODE;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    const size_t eb = group == 1 ? 97 : 192;
+    DevBuf d_data, d_off, d_out, d_fail;
+    cc_status s = stage_messages(c, n, data, offsets, d_data, d_off);
+    if (s) return s;
+    if (d_out.ensure(n * eb) || d_fail.ensure(4)) return CC_ERR_HIP;
+    HIPCK(hipMemsetAsync(d_fail.p, 0, 4, c->stream));
+    KCK(cck_hash_to_curve(group, n, d_data.as<uint8_t>(), d_off.as<uint64_t>(), d_out.as<uint8_t>(),
+                          d_fail.as<uint32_t>(), c->stream));
+    uint32_t fail = 0;
+    HIPCK(hipMemcpyAsync(out, d_out.p, n * eb, hipMemcpyDeviceToHost, c->stream));
+    HIPCK(hipMemcpyAsync(&fail, d_fail.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCK(hipStreamSynchronize(c->stream));
+    return fail ? CC_ERR_DECODE : CC_OK;  // 4,096 failed tries (probability ~2^-4096)
+}
+
+cc_status cc_hash_msg(cc_ctx* c, size_t n, const uint8_t* data, const uint64_t* offsets, uint8_t* out48) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || (n && (!offsets || !out48))) return CC_ERR_DECODE;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    DevBuf d_data, d_off, d_out;
+    cc_status s = stage_messages(c, n, data, offsets, d_data, d_off);
+    if (s) return s;
+    if (d_out.ensure(n * 48)) return CC_ERR_HIP;
+    KCK(cck_shake256_48(n, d_data.as<uint8_t>(), d_off.as<uint64_t>(), d_out.as<uint8_t>(), c->stream));
+    HIPCK(hipMemcpyAsync(out48, d_out.p, n * 48, hipMemcpyDeviceToHost, c->stream));
+    HIPCK(hipStreamSynchronize(c->stream));
+    return CC_OK;
 }
 
 // ---------------------------------------------------------------- issuer table (config 4)

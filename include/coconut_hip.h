@@ -178,6 +178,17 @@ cc_status cc_pok_verify_batch_device(cc_ctx* ctx, size_t n, size_t q, size_t r, 
  * Tests: G1 phi(P) == -[x^2] P, G2 psi(Q) == [x] Q (eprint 2021/1130, 2022/352). */
 cc_status cc_subgroup_check(cc_ctx* ctx, int group, size_t n, const uint8_t* points, uint8_t* status);
 
+/* Batched amcl_wrapper `from_msg_hash`: n messages, message i =
+ * data[offsets[i] .. offsets[i+1]) (offsets: n + 1 entries, offsets[0] = 0), each hashed with
+ * SHAKE256 to 48 bytes and mapped to `group` (1 = G1, 2 = G2) by AMCL's try-and-increment `mapit`
+ * with cofactor clearing; out: n encodings.  Params::new (signature.rs:22-32) hashes label || " : g",
+ * " : g_tilde", " : y" || i; SignatureRequest::compute_h (signature.rs:197-206) hashes
+ * commitment.to_bytes() || m_i.to_bytes().  Parity unpinned (AMCL restated, see oracle/).
+ * cc_hash_msg: the 48-byte SHAKE256 digests alone (amcl_wrapper hash_msg). */
+cc_status cc_hash_to_curve(cc_ctx* ctx, int group, size_t n, const uint8_t* data, const uint64_t* offsets,
+                           uint8_t* out);
+cc_status cc_hash_msg(cc_ctx* ctx, size_t n, const uint8_t* data, const uint64_t* offsets, uint8_t* out48);
+
 /* Batch fixed-base scalar multiplication out_i = k_i * base (group 1 = G1, 2 = G2); scalars n x 48 B
  * big-endian Fr, out n encodings.  The keygen derivation g~ * x_i (reference src/keygen.rs:27-32)
  * and the issuer's h^e (src/signature.rs:423-428) in batch form. */

@@ -278,6 +278,29 @@ def make_subgroup(seed):
     return out
 
 
+def make_hash_to_curve():
+    """amcl_wrapper from_msg_hash vectors (PARITY UNPINNED: AMCL mapit restated, oracle/hash_to_curve.py):
+    messages across the SHAKE256 block boundary (rate 136) and Params::new(6, "test") in both group
+    assignments (the reference's test label, signature.rs:668-679)."""
+    from oracle import hash_to_curve as H
+    import hashlib
+    msgs = [b"", b"a", bytes(range(47)), bytes(135), bytes(range(136)), bytes(137), b"x" * 271, b"y" * 272,
+            bytes((7 * i) & 0xFF for i in range(300))]
+    out = {"messages": []}
+    for m in msgs:
+        out["messages"].append({"msg": hx(m), "shake256_48": hashlib.shake_256(m).hexdigest(48),
+                                "g1": hx(B.g1_to_bytes(H.g1_from_msg_hash(m))),
+                                "g2": hx(B.g2_to_bytes(H.g2_from_msg_hash(m)))})
+        print(f"  h2c msg len {len(m)}", flush=True)
+    for mode in ("G2", "G1"):
+        g, gt, h = H.params_new(mode, 6, b"test")
+        sig_enc = B.g2_to_bytes if mode == "G2" else B.g1_to_bytes
+        oth_enc = B.g1_to_bytes if mode == "G2" else B.g2_to_bytes
+        out[f"params_{mode}"] = {"label": "test", "msg_count": 6, "g": hx(sig_enc(g)), "g_tilde": hx(oth_enc(gt)),
+                                 "h": [hx(sig_enc(x)) for x in h]}
+    return out
+
+
 def make_pairing_kat(seed):
     """Single-pairing KATs: e(a*G1, b*G2) bytes + the generator pairing."""
     rng = C.Drbg(seed)
@@ -309,6 +332,8 @@ def main():
 
     if want("kat"):
         write("pairing_kat.json", make_pairing_kat(11))
+    if want("h2c"):
+        write("hash_to_curve.json", make_hash_to_curve())
     if want("subgroup"):
         write("subgroup.json", make_subgroup(13))
     for mode in ("G2", "G1"):

@@ -214,3 +214,22 @@ def test_subgroup_fixture_definition_and_endomorphism_tests_agree():
             assert curve.on_curve(Pt)
             assert rec["status"] == (2 if S.in_subgroup_def(curve, Pt) else 1)
             assert endo(Pt) == (rec["status"] == 2)
+
+
+def test_hash_to_curve_fixture_is_consistent():
+    """hash_to_curve.json (parity unpinned: AMCL mapit restated): digests are SHAKE256 (hashlib), every
+    point is on its curve and in the order-r subgroup (cofactor cleared), and the oracle reproduces
+    every vector."""
+    import hashlib
+    from oracle import bls12_381 as B
+    from oracle import hash_to_curve as H
+    from oracle import subgroup as S
+    d = golden("hash_to_curve.json")
+    for rec in d["messages"][:4]:
+        m = bytes.fromhex(rec["msg"])
+        assert hashlib.shake_256(m).hexdigest(48) == rec["shake256_48"] == H.hash_msg(m).hex()
+        p1 = B.g1_from_bytes(bytes.fromhex(rec["g1"]))
+        q2 = B.g2_from_bytes(bytes.fromhex(rec["g2"]))
+        assert S.in_g1_endo(p1) and S.in_g2_endo(q2)
+        assert B.g1_to_bytes(H.g1_from_msg_hash(m)).hex() == rec["g1"]
+        assert B.g2_to_bytes(H.g2_from_msg_hash(m)).hex() == rec["g2"]
