@@ -24,6 +24,14 @@ int cck_subgroup(int group, size_t n, const uint8_t* d_bytes, uint8_t* d_status,
 int cck_hash_to_curve(int group, size_t n, const uint8_t* d_data, const uint64_t* d_offsets, uint8_t* d_out,
                       uint32_t* d_fail, hipStream_t st);
 int cck_shake256_48(size_t n, const uint8_t* d_data, const uint64_t* d_offsets, uint8_t* d_out, hipStream_t st);
+size_t cck_sigreq_proof_bytes(int group, int k);
+int cck_blind_assemble(int group, size_t n, int q, int k, const uint8_t* d_cts, const uint8_t* d_h,
+                       const uint8_t* d_known, const uint8_t* d_x, const uint8_t* d_y, uint8_t* d_pts, uint32_t* d_sc,
+                       hipStream_t st);
+size_t cck_sigreq_scratch_words(int group, size_t n, int k);
+int cck_sigreq_verify(int group, size_t n, int k, const uint8_t* d_g, const uint8_t* d_hvec, const uint8_t* d_comm,
+                      const uint8_t* d_cts, const uint8_t* d_pk, const uint8_t* d_proof, const uint8_t* d_chal,
+                      const uint8_t* d_hpts, uint32_t* d_scratch, uint8_t* d_ok, uint8_t* d_verdicts, hipStream_t st);
 int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* d_Y, uint32_t* d_bases,
                   uint32_t* d_binf, const uint8_t* d_msgs, uint8_t* d_msgs_canon, hipStream_t st);
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
@@ -790,6 +798,113 @@ cc_status cc_hash_msg(cc_ctx* c, size_t n, const uint8_t* data, const uint64_t* 
     KCK(cck_shake256_48(n, d_data.as<uint8_t>(), d_off.as<uint64_t>(), d_out.as<uint8_t>(), c->stream));
     HIPCK(hipMemcpyAsync(out48, d_out.p, n * 48, hipMemcpyDeviceToHost, c->stream));
     HIPCK(hipStreamSynchronize(c->stream));
+    return CC_OK;
+}
+
+// ---------------------------------------------------------------- issuance (§8(f) row 3)
+// h_r = compute_h(commitment_r, known_r) for every request, on the device (hash.hip)
+static cc_status compute_h_batch(cc_ctx* c, size_t n, size_t q, size_t k, const uint8_t* comm, const uint8_t* known,
+                                 DevBuf& d_h) {
+    const size_t sb = (size_t)sig_bytes(c->mode), kn = q - k, len = sb + 48 * kn;
+    std::vector<uint8_t> data(n * len);
+    std::vector<uint64_t> off(n + 1);
+    for (size_t r = 0; r < n; r++) {
+        memcpy(&data[r * len], comm + r * sb, sb);
+        if (kn) memcpy(&data[r * len + sb], known + r * kn * 48, kn * 48);
+        off[r] = r * len;
+    }
+    off[n] = n * len;
+    DevBuf d_data, d_off, d_fail;
+    cc_status s = stage_messages(c, n, data.data(), off.data(), d_data, d_off);
+    if (s) return s;
+    if (d_h.ensure(n * sb) || d_fail.ensure(4)) return CC_ERR_HIP;
+    HIPCK(hipMemsetAsync(d_fail.p, 0, 4, c->stream));
+    KCK(cck_hash_to_curve(sig_group(c->mode), n, d_data.as<uint8_t>(), d_off.as<uint64_t>(), d_h.as<uint8_t>(),
+                          d_fail.as<uint32_t>(), c->stream));
+    HIPCK(hipStreamSynchronize(c->stream));
+    return CC_OK;
+}
+
+cc_status cc_blind_sign_batch(cc_ctx* c, size_t n, size_t q, size_t k, const uint8_t* commitment, const uint8_t* known,
+                              const uint8_t* ciphertexts, const uint8_t* x, const uint8_t* y, uint8_t* out_h,
+                              uint8_t* out_c1, uint8_t* out_c2) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || !x || (q && !y) || (n && (!commitment || !out_h || !out_c1 || !out_c2 || (k && !ciphertexts) ||
+                                        (q > k && !known))))
+        return CC_ERR_DECODE;
+    if (k > q) return CC_ERR_LEN;  // reference: hidden + known == y.len() (assert_eq!)
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    const size_t sb = (size_t)sig_bytes(c->mode), t = k + 1;
+    const int sg = sig_group(c->mode);
+    hipStream_t st = c->stream;
+    DevBuf d_h, d_cts, d_known, d_x, d_y, d_pts, d_sc, d_out;
+    cc_status s = compute_h_batch(c, n, q, k, commitment, known, d_h);
+    if (s) return s;
+    if (d_cts.ensure(n * k * 2 * sb + 16) || d_known.ensure(n * (q - k) * 48 + 16) || d_x.ensure(48) ||
+        d_y.ensure(q * 48 + 16) || d_pts.ensure(2 * n * t * sb) || d_sc.ensure(2 * n * t * 32) ||
+        d_out.ensure(2 * n * sb))
+        return CC_ERR_HIP;
+    s = agg_scratch(c, sg, 2 * n, t);
+    if (s) return s;
+    if (k) HIPCK(hipMemcpyAsync(d_cts.p, ciphertexts, n * k * 2 * sb, hipMemcpyHostToDevice, st));
+    if (q > k) HIPCK(hipMemcpyAsync(d_known.p, known, n * (q - k) * 48, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_x.p, x, 48, hipMemcpyHostToDevice, st));
+    if (q) HIPCK(hipMemcpyAsync(d_y.p, y, q * 48, hipMemcpyHostToDevice, st));
+    KCK(cck_blind_assemble(sg, n, (int)q, (int)k, d_cts.as<uint8_t>(), d_h.as<uint8_t>(), d_known.as<uint8_t>(),
+                           d_x.as<uint8_t>(), d_y.as<uint8_t>(), d_pts.as<uint8_t>(), d_sc.as<uint32_t>(), st));
+    KCK(cck_msm_straus(sg, 2 * n, t, d_pts.as<uint8_t>(), t * sb, 0, sb, d_sc.as<uint32_t>(), 1,
+                       c->agg_scratch.as<uint32_t>(), d_out.as<uint8_t>(), st));
+    std::vector<uint8_t> o(2 * n * sb);
+    HIPCK(hipMemcpyAsync(o.data(), d_out.p, 2 * n * sb, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(out_h, d_h.p, n * sb, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    for (size_t r = 0; r < n; r++) {
+        memcpy(out_c1 + r * sb, &o[(2 * r) * sb], sb);
+        memcpy(out_c2 + r * sb, &o[(2 * r + 1) * sb], sb);
+    }
+    return CC_OK;
+}
+
+size_t cc_sigreq_proof_bytes(const cc_ctx* c, size_t k) {
+    c = primary(c);
+    return c ? cck_sigreq_proof_bytes(sig_group(c->mode), (int)k) : 0;
+}
+
+cc_status cc_sigreq_verify_batch(cc_ctx* c, size_t n, size_t q, size_t k, const uint8_t* g, const uint8_t* hvec,
+                                 const uint8_t* commitment, const uint8_t* known, const uint8_t* ciphertexts,
+                                 const uint8_t* elgamal_pk, const uint8_t* proofs, const uint8_t* chal,
+                                 uint8_t* verdicts) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || !g || (k && !hvec) ||
+        (n && (!commitment || !elgamal_pk || !proofs || !chal || !verdicts || (k && !ciphertexts) || (q > k && !known))))
+        return CC_ERR_DECODE;
+    if (k > q) return CC_ERR_LEN;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    const size_t sb = (size_t)sig_bytes(c->mode);
+    const int sg = sig_group(c->mode);
+    const size_t pb = cck_sigreq_proof_bytes(sg, (int)k);
+    hipStream_t st = c->stream;
+    DevBuf d_h, d_g, d_hv, d_comm, d_cts, d_pk, d_pr, d_ch, d_scr, d_ok, d_v;
+    cc_status s = compute_h_batch(c, n, q, k, commitment, known, d_h);
+    if (s) return s;
+    if (d_g.ensure(sb) || d_hv.ensure(k * sb + 16) || d_comm.ensure(n * sb) || d_cts.ensure(n * k * 2 * sb + 16) ||
+        d_pk.ensure(n * sb) || d_pr.ensure(n * pb) || d_ch.ensure(n * 48) ||
+        d_scr.ensure(cck_sigreq_scratch_words(sg, n, (int)k) * 4) || d_ok.ensure(n * (2 + 2 * k)) || d_v.ensure(n))
+        return CC_ERR_HIP;
+    HIPCK(hipMemcpyAsync(d_g.p, g, sb, hipMemcpyHostToDevice, st));
+    if (k) HIPCK(hipMemcpyAsync(d_hv.p, hvec, k * sb, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_comm.p, commitment, n * sb, hipMemcpyHostToDevice, st));
+    if (k) HIPCK(hipMemcpyAsync(d_cts.p, ciphertexts, n * k * 2 * sb, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_pk.p, elgamal_pk, n * sb, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_pr.p, proofs, n * pb, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_ch.p, chal, n * 48, hipMemcpyHostToDevice, st));
+    KCK(cck_sigreq_verify(sg, n, (int)k, d_g.as<uint8_t>(), d_hv.as<uint8_t>(), d_comm.as<uint8_t>(),
+                          d_cts.as<uint8_t>(), d_pk.as<uint8_t>(), d_pr.as<uint8_t>(), d_ch.as<uint8_t>(),
+                          d_h.as<uint8_t>(), d_scr.as<uint32_t>(), d_ok.as<uint8_t>(), d_v.as<uint8_t>(), st));
+    HIPCK(hipMemcpyAsync(verdicts, d_v.p, n, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
     return CC_OK;
 }
 

@@ -189,6 +189,26 @@ cc_status cc_hash_to_curve(cc_ctx* ctx, int group, size_t n, const uint8_t* data
                            uint8_t* out);
 cc_status cc_hash_msg(cc_ctx* ctx, size_t n, const uint8_t* data, const uint64_t* offsets, uint8_t* out48);
 
+/* Issuer-side batch, n signature requests with k hidden of q messages,
+ * SignatureGroup encodings:
+ *   cc_blind_sign_batch  : BlindSignature::new (signature.rs:382-433) under one issuer key
+ *       commitment n x SG | known n x (q-k) x 48 | ciphertexts n x k x (c1, c2) | x 48 | y q x 48
+ *       -> out_h (= compute_h), out_c1, out_c2 (n x SG each)
+ *   cc_sigreq_verify_batch : SignatureRequestProof::verify (signature.rs:324-377), verdicts n bytes;
+ *       g and h[0..k) are the Params' SignatureGroup generators; elgamal_pk n x SG; chal n x 48;
+ *       proofs n x cc_sigreq_proof_bytes(ctx, k) bytes, per request:
+ *         T_sk | r_sk | T_comm | r_comm[k+1] | k x (T_1 | r_1 | T_2 | r_2a | r_2b)
+ *       (T = Schnorr commitment encodings, r = 48-byte responses).
+ * CC_ERR_LEN if k > q (the reference's assert_eq!). */
+cc_status cc_blind_sign_batch(cc_ctx* ctx, size_t n, size_t q, size_t k, const uint8_t* commitment,
+                              const uint8_t* known, const uint8_t* ciphertexts, const uint8_t* x, const uint8_t* y,
+                              uint8_t* out_h, uint8_t* out_c1, uint8_t* out_c2);
+size_t cc_sigreq_proof_bytes(const cc_ctx* ctx, size_t k);
+cc_status cc_sigreq_verify_batch(cc_ctx* ctx, size_t n, size_t q, size_t k, const uint8_t* g, const uint8_t* h,
+                                 const uint8_t* commitment, const uint8_t* known, const uint8_t* ciphertexts,
+                                 const uint8_t* elgamal_pk, const uint8_t* proofs, const uint8_t* chal,
+                                 uint8_t* verdicts);
+
 /* Batch fixed-base scalar multiplication out_i = k_i * base (group 1 = G1, 2 = G2); scalars n x 48 B
  * big-endian Fr, out n encodings.  The keygen derivation g~ * x_i (reference src/keygen.rs:27-32)
  * and the issuer's h^e (src/signature.rs:423-428) in batch form. */

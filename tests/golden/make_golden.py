@@ -301,6 +301,59 @@ def make_hash_to_curve():
     return out
 
 
+ISSUE_KINDS = ["valid", "bad_sk_response", "bad_comm_response", "resp_mismatch", "bad_ct_proof", "wrong_chal", "valid"]
+
+
+def make_issuance(mode, q, k, nreq, seed):
+    """SignatureRequest -> SignatureRequestPoK proof -> verify, and BlindSignature::new -> unblind ->
+    Signature::verify (reference check_signing_on_random_msgs, signature.rs:582-638)."""
+    from oracle import issuance as I
+    grp = C.Groups(mode)
+    rng = C.Drbg(seed)
+    params = C.params_from_rng(grp, q, rng)
+    x, y = rng.fr(), [rng.fr() for _ in range(q)]
+    vk = (grp.other.mul(params["g_tilde"], x), [grp.other.mul(params["g_tilde"], v) for v in y])
+    fr = lambda v: hx(B.fr_to_bytes(v % B.R))  # noqa: E731
+    se = lambda pt: hx(grp.sig_to_bytes(pt))  # noqa: E731
+    reqs = []
+    for c in range(nreq):
+        kind = ISSUE_KINDS[c % len(ISSUE_KINDS)]
+        sk, pk = I.elgamal_keygen(grp, params, rng)
+        msgs = [rng.fr() for _ in range(q)]
+        req, rnd = I.signature_request_new(grp, msgs, k, pk, params, rng)
+        pok = I.sigreq_pok_init(grp, req, pk, params, rng)
+        chal = rng.fr()
+        proof = I.sigreq_gen_proof(pok, msgs[:k], rnd, sk, chal)
+        if kind == "bad_sk_response":
+            proof["sk"]["responses"][0] += 1
+        elif kind == "bad_comm_response":
+            proof["comm"]["responses"][-1] += 1
+        elif kind == "resp_mismatch" and k:
+            proof["cts"][0][1]["responses"][1] += 1
+        elif kind == "bad_ct_proof" and k:
+            proof["cts"][0][0]["T"] = grp.sig.add(proof["cts"][0][0]["T"], grp.sig.gen)
+        elif kind == "wrong_chal":
+            chal += 1
+        verdict = I.sigreq_proof_verify(grp, proof, req, pk, chal, params)
+        assert verdict == (kind == "valid" or (k == 0 and kind in ("resp_mismatch", "bad_ct_proof"))), kind
+        rec_p = se(proof["sk"]["T"]) + fr(proof["sk"]["responses"][0]) + se(proof["comm"]["T"])
+        rec_p += "".join(fr(v) for v in proof["comm"]["responses"])
+        for p1, p2 in proof["cts"]:
+            rec_p += se(p1["T"]) + fr(p1["responses"][0]) + se(p2["T"]) + fr(p2["responses"][0]) + fr(p2["responses"][1])
+        h, c1, c2 = I.blind_sign(grp, req, (x, y))
+        sig = I.unblind(grp, (h, c1, c2), sk)
+        assert C.verify(grp, sig, msgs, vk, params["g_tilde"]), "unblinded signature must verify"
+        reqs.append({"kind": kind, "commitment": se(req["commitment"]), "known": [fr(m) for m in req["known"]],
+                     "ciphertexts": [[se(a), se(b)] for a, b in req["ciphertexts"]], "pk": se(pk), "proof": rec_p,
+                     "chal": fr(chal), "verdict": int(verdict), "h": se(h), "c1": se(c1), "c2": se(c2),
+                     "sigma2": se(sig[1]), "msgs": [fr(m) for m in msgs], "elgamal_sk": fr(sk)})
+        print(f"  issuance {mode} k={k} req {c} {kind} -> {int(verdict)}", flush=True)
+    return {"mode": mode, "q": q, "k": k, "g": se(params["g"]), "h": [se(v) for v in params["h"]],
+            "g_tilde": hx(grp.oth_to_bytes(params["g_tilde"])), "x": fr(x), "y": [fr(v) for v in y],
+            "vk": {"X": hx(grp.oth_to_bytes(vk[0])), "Y": [hx(grp.oth_to_bytes(v)) for v in vk[1]]},
+            "requests": reqs}
+
+
 def make_pairing_kat(seed):
     """Single-pairing KATs: e(a*G1, b*G2) bytes + the generator pairing."""
     rng = C.Drbg(seed)
@@ -332,6 +385,10 @@ def main():
 
     if want("kat"):
         write("pairing_kat.json", make_pairing_kat(11))
+    if want("issue"):
+        for mode in ("G2", "G1"):
+            write(f"issuance_{mode.lower()}.json", {"cases": [make_issuance(mode, 6, 2, 7, 21), make_issuance(mode, 4, 0, 3, 22),
+                                                              make_issuance(mode, 3, 3, 3, 23)]})
     if want("h2c"):
         write("hash_to_curve.json", make_hash_to_curve())
     if want("subgroup"):
