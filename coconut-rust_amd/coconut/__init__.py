@@ -10,4 +10,4 @@ from .signature import (GroupMode, Params, Verkey, Signature, Context, verify_ba
                         signature_aggregate_batch, verkey_aggregate_batch, verkey_aggregate_ids, fixed_base_mul, subgroup_check, hash_to_curve, hash_msg, params_new,
                         G1_GENERATOR, G2_GENERATOR)
 from .pok_sig import PoKOfSignatureProof, pok_verify_batch  # noqa: F401
-from .issuance import blind_sign_batch, sigreq_verify_batch  # noqa: F401
+from .issuance import blind_sign_batch, sigreq_verify_batch, vss_verify_batch  # noqa: F401

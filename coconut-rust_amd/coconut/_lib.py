@@ -47,6 +47,7 @@ _SIGS = {
     "cc_blind_sign_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "cc_sigreq_proof_bytes": (c_sz, [c_p, c_sz]),
     "cc_sigreq_verify_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "cc_vss_verify_batch": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_sz, c_p, c_p, c_p, c_p]),
     "cc_fixed_base_mul": (c_int, [c_p, c_int, c_p, c_sz, c_p, c_p]),
     "cc_rlc_partial_device": (c_int, [c_p, c_sz, c_sz, ctypes.c_uint64, c_p, c_p, c_p, c_p, c_p, c_p]),
     "cc_rlc_finish_device": (c_int, [c_p, c_sz, c_p, c_p, c_p, c_p]),

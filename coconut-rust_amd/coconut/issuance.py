@@ -47,3 +47,19 @@ def sigreq_verify_batch(ctx: Context, q: int, k: int, g: bytes, h: Sequence[byte
                                      ptr[4] if ct else None, ptr[5], ptr[6], ptr[7], ctypes.c_void_p(v.ctypes.data)),
           "cc_sigreq_verify_batch")
     return v[:n]
+
+
+def vss_verify_batch(ctx: Context, t: int, g: bytes, h: bytes, commitment_sets: Sequence[Sequence[bytes]],
+                     set_of: Sequence[int], ids: Sequence[int], shares: Sequence[tuple]) -> np.ndarray:
+    """PedersenVSS::verify_share for a batch of (id, (s, s')) against their dealer's commitments (G1)."""
+    n = len(ids)
+    cm = b"".join(c for cs in commitment_sets for c in cs)
+    so = np.ascontiguousarray(np.asarray(set_of, dtype=np.uint32))
+    iv = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64))
+    sh = b"".join(a + b for a, b in shares)
+    keep = [buf(v) for v in (g, h, cm, sh)]
+    v = np.zeros(max(n, 1), dtype=np.uint8)
+    check(lib.cc_vss_verify_batch(ctx.h, n, t, keep[0][0], keep[1][0], keep[2][0], len(commitment_sets),
+                                  ctypes.c_void_p(so.ctypes.data), ctypes.c_void_p(iv.ctypes.data), keep[3][0],
+                                  ctypes.c_void_p(v.ctypes.data)), "cc_vss_verify_batch")
+    return v[:n]

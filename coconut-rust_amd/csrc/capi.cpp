@@ -25,6 +25,9 @@ int cck_hash_to_curve(int group, size_t n, const uint8_t* d_data, const uint64_t
                       uint32_t* d_fail, hipStream_t st);
 int cck_shake256_48(size_t n, const uint8_t* d_data, const uint64_t* d_offsets, uint8_t* d_out, hipStream_t st);
 size_t cck_sigreq_proof_bytes(int group, int k);
+int cck_vss_verify(size_t n, int t, const uint8_t* d_g, const uint8_t* d_h, const uint8_t* d_comms,
+                   const uint32_t* d_set_of, const uint64_t* d_ids, const uint8_t* d_shares, uint32_t* d_scratch,
+                   uint8_t* d_ok, hipStream_t st);
 int cck_blind_assemble(int group, size_t n, int q, int k, const uint8_t* d_cts, const uint8_t* d_h,
                        const uint8_t* d_known, const uint8_t* d_x, const uint8_t* d_y, uint8_t* d_pts, uint32_t* d_sc,
                        hipStream_t st);
@@ -904,6 +907,35 @@ cc_status cc_sigreq_verify_batch(cc_ctx* c, size_t n, size_t q, size_t k, const 
                           d_cts.as<uint8_t>(), d_pk.as<uint8_t>(), d_pr.as<uint8_t>(), d_ch.as<uint8_t>(),
                           d_h.as<uint8_t>(), d_scr.as<uint32_t>(), d_ok.as<uint8_t>(), d_v.as<uint8_t>(), st));
     HIPCK(hipMemcpyAsync(verdicts, d_v.p, n, hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    return CC_OK;
+}
+
+// ---------------------------------------------------------------- keygen: Pedersen VSS (§8(f) row 4)
+cc_status cc_vss_verify_batch(cc_ctx* c, size_t n, size_t t, const uint8_t* g, const uint8_t* h,
+                              const uint8_t* commitments, size_t n_sets, const uint32_t* set_of, const uint64_t* ids,
+                              const uint8_t* shares, uint8_t* verdicts) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || !g || !h || (n && (!commitments || !set_of || !ids || !shares || !verdicts)) || t == 0 || t > 4096)
+        return CC_ERR_DECODE;
+    for (size_t i = 0; i < n; i++)
+        if (set_of[i] >= n_sets) return CC_ERR_DECODE;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    DevBuf d_g, d_h, d_c, d_set, d_ids, d_sh, d_scr, d_ok;
+    if (d_g.ensure(97) || d_h.ensure(97) || d_c.ensure(n_sets * t * 97) || d_set.ensure(n * 4) || d_ids.ensure(n * 8) ||
+        d_sh.ensure(n * 96) || d_scr.ensure(n * (t + 2) * 33 * 4) || d_ok.ensure(n))
+        return CC_ERR_HIP;
+    HIPCK(hipMemcpyAsync(d_g.p, g, 97, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_h.p, h, 97, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_c.p, commitments, n_sets * t * 97, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_set.p, set_of, n * 4, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_ids.p, ids, n * 8, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemcpyAsync(d_sh.p, shares, n * 96, hipMemcpyHostToDevice, st));
+    KCK(cck_vss_verify(n, (int)t, d_g.as<uint8_t>(), d_h.as<uint8_t>(), d_c.as<uint8_t>(), d_set.as<uint32_t>(),
+                       d_ids.as<uint64_t>(), d_sh.as<uint8_t>(), d_scr.as<uint32_t>(), d_ok.as<uint8_t>(), st));
+    HIPCK(hipMemcpyAsync(verdicts, d_ok.p, n, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
     return CC_OK;
 }

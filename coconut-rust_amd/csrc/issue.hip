@@ -202,6 +202,67 @@ __global__ __launch_bounds__(64) void k_sigreq_combine(size_t n, int k, size_t s
     verdicts[r] = good ? 1 : 0;
 }
 
+// Pedersen VSS verify_share (secret_sharing [EXT]; reference keygen.rs:334-349), one share per lane:
+//     sum_{i<t} id^i C_i - s g - s' h == O      (G1; C = the dealer's coefficient commitments)
+// by interleaved double-and-add over the t + 2 decoded points kept in the lane's scratch.
+__global__ __launch_bounds__(64) void k_vss_verify(size_t n, int t, const uint8_t* __restrict__ g,
+                                                   const uint8_t* __restrict__ h, const uint8_t* __restrict__ comms,
+                                                   const uint32_t* __restrict__ set_of,
+                                                   const uint64_t* __restrict__ ids,
+                                                   const uint8_t* __restrict__ shares,
+                                                   uint32_t* __restrict__ scratch, uint8_t* __restrict__ ok) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    constexpr int AW = sizeof(Aff<Fp>) / 4, EWS = AW + 8 + 1;
+    uint32_t* sp = scratch + i * (size_t)(t + 2) * EWS;
+    auto put = [&](int m, const uint8_t* base, const uint32_t sc[8]) {
+        uint32_t* e = sp + (size_t)m * EWS;
+        Aff<Fp> a;
+        const bool fin = g1_decode(a, base);
+        const uint32_t* aw = reinterpret_cast<const uint32_t*>(&a);
+        for (int w = 0; w < AW; w++) e[w] = aw[w];
+        for (int w = 0; w < 8; w++) e[AW + w] = sc[w];
+        e[AW + 8] = fin ? 1u : 0u;
+    };
+    // -s, -s' (mod r)
+    for (int z = 0; z < 2; z++) {
+        Fr v;
+        fr_from_be48(v, shares + (i * 2 + z) * 48);
+        uint32_t o = 0, neg[8], br = 0;
+        for (int w = 0; w < 8; w++) o |= v.v[w];
+        for (int w = 0; w < 8; w++) neg[w] = __builtin_subc(rl(w), v.v[w], br, &br);
+        if (!o)
+            for (int w = 0; w < 8; w++) neg[w] = 0;
+        put(z, z ? h : g, neg);
+    }
+    // id^k, k < t
+    const uint64_t id = ids[i];
+    uint32_t pw[8] = {1u, 0, 0, 0, 0, 0, 0, 0}, idv[8] = {(uint32_t)id, (uint32_t)(id >> 32), 0, 0, 0, 0, 0, 0};
+    const uint8_t* C = comms + (size_t)set_of[i] * t * 97;
+    for (int k = 0; k < t; k++) {
+        put(2 + k, C + (size_t)k * 97, pw);
+        uint32_t nx[8];
+        fr_mul_canon(nx, pw, idv);
+        for (int w = 0; w < 8; w++) pw[w] = nx[w];
+    }
+    Jac<Fp> acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (int b = 254; b >= 0; b--) {
+        jac_dbl(acc, acc);
+#pragma unroll 1
+        for (int m = 0; m < t + 2; m++) {
+            const uint32_t* e = sp + (size_t)m * EWS;
+            if (!e[AW + 8] || !((e[AW + (b >> 5)] >> (b & 31)) & 1u)) continue;
+            Aff<Fp> a;
+            uint32_t* aw = reinterpret_cast<uint32_t*>(&a);
+            for (int w = 0; w < AW; w++) aw[w] = e[w];
+            jac_add_aff(acc, acc, a);
+        }
+    }
+    ok[i] = jac_is_inf(acc) ? 1 : 0;
+}
+
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 extern "C" {
@@ -242,6 +303,15 @@ int cck_sigreq_verify(int group, size_t n, int k, const uint8_t* d_g, const uint
                            d_cts, d_pk, d_proof, d_chal, d_hpts, d_scratch, d_ok);
     hipLaunchKernelGGL(k_sigreq_combine, dim3(nblocks(n, 64)), dim3(64), 0, st, n, k, (size_t)(group == 1 ? 97 : 192),
                        d_proof, d_ok, d_verdicts);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int cck_vss_verify(size_t n, int t, const uint8_t* d_g, const uint8_t* d_h, const uint8_t* d_comms,
+                   const uint32_t* d_set_of, const uint64_t* d_ids, const uint8_t* d_shares, uint32_t* d_scratch,
+                   uint8_t* d_ok, hipStream_t st) {
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_vss_verify, dim3(nblocks(n, 64)), dim3(64), 0, st, n, t, d_g, d_h, d_comms, d_set_of, d_ids,
+                       d_shares, d_scratch, d_ok);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

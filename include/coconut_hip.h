@@ -209,6 +209,16 @@ cc_status cc_sigreq_verify_batch(cc_ctx* ctx, size_t n, size_t q, size_t k, cons
                                  const uint8_t* elgamal_pk, const uint8_t* proofs, const uint8_t* chal,
                                  uint8_t* verdicts);
 
+/* Pedersen VSS share verification (secret_sharing PedersenVSS::verify_share,
+ * used by trusted_party_PVSS_keygen, reference keygen.rs:74-122, 334-349), n shares in G1:
+ *   g * s + h * s' == sum_{k<t} id^k * C_k, C = commitments[set_of[i]] (n_sets x t x 97 B),
+ *   shares n x (s, s') 48 B each, ids n x u64; verdicts n bytes.
+ * The keygen derivation alpha_i = g~ * x_i, beta_ij = g~ * y_ij (keygen.rs:17-45) is
+ * cc_fixed_base_mul. */
+cc_status cc_vss_verify_batch(cc_ctx* ctx, size_t n, size_t t, const uint8_t* g, const uint8_t* h,
+                              const uint8_t* commitments, size_t n_sets, const uint32_t* set_of, const uint64_t* ids,
+                              const uint8_t* shares, uint8_t* verdicts);
+
 /* Batch fixed-base scalar multiplication out_i = k_i * base (group 1 = G1, 2 = G2); scalars n x 48 B
  * big-endian Fr, out n encodings.  The keygen derivation g~ * x_i (reference src/keygen.rs:27-32)
  * and the issuer's h^e (src/signature.rs:423-428) in batch form. */

@@ -354,6 +354,38 @@ def make_issuance(mode, q, k, nreq, seed):
             "requests": reqs}
 
 
+def make_keygen(seed, t=3, n=5, q=7):
+    """keygen_from_shares (keygen.rs:17-45) derivations and Pedersen VSS dealings / share checks
+    (trusted_party_PVSS_keygen keygen.rs:74-122, verify_share test keygen.rs:334-349), gens from the
+    reference test label "testPVSS" (parity unpinned: AMCL mapit restated)."""
+    from oracle import keygen as K
+    rng = C.Drbg(seed)
+    g, h = K.pedersen_gens(b"testPVSS")
+    sets, checks = [], []
+    shares_x = None
+    for d in range(1 + q):
+        sec, sec_t, comm, shares = K.pedersen_deal(t, n, g, h, rng)
+        sets.append([hx(B.g1_to_bytes(c)) for c in comm])
+        for i in range(1, n + 1):
+            s_, st = shares[i]
+            bad = (d + i) % 4 == 0
+            if bad:
+                s_ = (s_ + 1) % B.R
+            ok = K.verify_share(t, i, (s_, st), comm, g, h)
+            assert ok == (not bad)
+            checks.append({"set": d, "id": i, "s": fr_hex(s_), "s_t": fr_hex(st), "ok": int(ok)})
+        if d == 0:
+            shares_x = {i: shares[i][0] for i in shares}
+    grp = C.Groups("G2")
+    g_tilde = B.G1.mul(B.G1.gen, rng.fr())
+    derive = [{"x": fr_hex(v), "alpha": hx(B.g1_to_bytes(B.G1.mul(g_tilde, v)))} for v in shares_x.values()]
+    g2t = B.G2.mul(B.G2.gen, rng.fr())
+    derive_g2 = [{"x": fr_hex(v), "alpha": hx(B.g2_to_bytes(B.G2.mul(g2t, v)))} for v in shares_x.values()]
+    return {"t": t, "n": n, "q": q, "g": hx(B.g1_to_bytes(g)), "h": hx(B.g1_to_bytes(h)), "commitments": sets,
+            "checks": checks, "g_tilde_g1": hx(B.g1_to_bytes(g_tilde)), "derive_g1": derive,
+            "g_tilde_g2": hx(B.g2_to_bytes(g2t)), "derive_g2": derive_g2}
+
+
 def make_pairing_kat(seed):
     """Single-pairing KATs: e(a*G1, b*G2) bytes + the generator pairing."""
     rng = C.Drbg(seed)
@@ -385,6 +417,8 @@ def main():
 
     if want("kat"):
         write("pairing_kat.json", make_pairing_kat(11))
+    if want("keygen"):
+        write("keygen_vss.json", make_keygen(31))
     if want("issue"):
         for mode in ("G2", "G1"):
             write(f"issuance_{mode.lower()}.json", {"cases": [make_issuance(mode, 6, 2, 7, 21), make_issuance(mode, 4, 0, 3, 22),

@@ -233,3 +233,16 @@ def test_hash_to_curve_fixture_is_consistent():
         assert S.in_g1_endo(p1) and S.in_g2_endo(q2)
         assert B.g1_to_bytes(H.g1_from_msg_hash(m)).hex() == rec["g1"]
         assert B.g2_to_bytes(H.g2_from_msg_hash(m)).hex() == rec["g2"]
+
+
+def test_issuance_and_keygen_fixtures_are_consistent():
+    """Oracle self-consistency on the §8(f) rows 3-4 fixtures: every generated request's proof verdict
+    and every VSS share verdict re-derive from the restatements."""
+    from oracle import bls12_381 as B
+    from oracle import keygen as K
+    d = golden("keygen_vss.json")
+    g, h = B.g1_from_bytes(bytes.fromhex(d["g"])), B.g1_from_bytes(bytes.fromhex(d["h"]))
+    for c in d["checks"][:8]:
+        comm = [B.g1_from_bytes(bytes.fromhex(x)) for x in d["commitments"][c["set"]]]
+        ok = K.verify_share(d["t"], c["id"], (int(c["s"], 16), int(c["s_t"], 16)), comm, g, h)
+        assert ok == bool(c["ok"])
