@@ -417,7 +417,7 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
 static cc_status ensure_work(cc_ctx* c, size_t n) {
     size_t words = n * 12;  // one Fp slot
     if (c->prep.ensure(words * 4 * PREP_SLOTS) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
-        c->scratch.ensure(words * 4 * 48) || c->verdicts.ensure(n))
+        c->scratch.ensure(words * 4 * 72) || c->verdicts.ensure(n))
         return CC_ERR_HIP;
     return CC_OK;
 }

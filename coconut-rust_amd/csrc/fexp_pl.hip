@@ -51,7 +51,9 @@ static __device__ __noinline__ void fx_cube(Soa src, Soa dst, size_t i) {
 
 // dst <- src^x, x = -|x| (cyclotomic square-and-multiply, then conj).  The base is re-read from src at
 // each of the 5 multiplications instead of being held in registers across the 63 squarings.
-static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, size_t i) {
+// Fallback of fx_pow_x below for the (never honestly reached) case of a zero decompression
+// denominator.
+static __device__ __noinline__ void fx_pow_x_gs(Soa src, Soa dst, size_t i) {
     Fp12 acc;
     ld_f12(acc, src, i);
     for (int b = 62; b >= 0; b--) {
@@ -67,6 +69,179 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, size_t i) {
     st_f12(dst, i, acc);
 }
 
+// ---------------------------------------------------------------- compressed cyclotomic squaring
+// Karabina's compression (eprint 2010/542) restated for this tower.  For x = a + b w + c w^2 in the
+// cyclotomic subgroup (a = a0 + a1 s, b = b0 + b1 s, c = c0 + c1 s), Granger-Scott's b', c' depend on
+// b and c only:
+//     b0' = 6 xi c0 c1 + 2 b0      b1' = 3 (c0^2 + xi c1^2) - 2 b1
+//     c0' = 3 (b0^2 + xi b1^2) - 2 c0      c1' = 6 b0 b1 + 2 c1
+// with 2 uv = (u + v)^2 - u^2 - v^2: six Fp2 squarings (392 mads a lane each) against Granger-Scott's
+// six Fp2 multiplications (588).  a is recovered from x conj(x) = 1 (its w and w^2 coefficients are
+// linear in a0, a1):
+//     a0 = (b0 Nb + xi c1 Nc) / D,  a1 = (c0 Nc + b1 Nb) / D,
+//     Nb = b0^2 - xi b1^2,  Nc = c0^2 - xi c1^2,  D = 2 (b0 c0 - xi b1 c1).
+// (tests/test_fexp_algebra.py checks both against the oracle's Fp12 arithmetic.)
+struct Cyc4 {
+    Fp2 b0, b1, c0, c1;
+};
+
+// r = 3 u + 2 v  /  3 u - 2 v   (u + 2 (u +- v))
+DEV void f2_3u_p2v(Fp2& r, const Fp2& u, const Fp2& v) {
+    Fp2 t;
+    f2_add(t, u, v);
+    f2_dbl(t, t);
+    f2_add(r, t, u);
+}
+DEV void f2_3u_m2v(Fp2& r, const Fp2& u, const Fp2& v) {
+    Fp2 t;
+    f2_sub(t, u, v);
+    f2_dbl(t, t);
+    f2_add(r, t, u);
+}
+
+DEV void cyc4_sqr(Cyc4& x) {
+    Fp2 s0, s1, t, Tb, Xb, Tc, Xc;
+    f2_sqr(s0, x.b0);
+    f2_sqr(s1, x.b1);
+    f2_add_lz(t, x.b0, x.b1);
+    f2_sqr(Xb, t);
+    f2_sub(Xb, Xb, s0);
+    f2_sub(Xb, Xb, s1);  // 2 b0 b1
+    f2_mul_xi(s1, s1);
+    f2_add(Tb, s0, s1);  // b0^2 + xi b1^2
+    f2_sqr(s0, x.c0);
+    f2_sqr(s1, x.c1);
+    f2_add_lz(t, x.c0, x.c1);
+    f2_sqr(Xc, t);
+    f2_sub(Xc, Xc, s0);
+    f2_sub(Xc, Xc, s1);
+    f2_mul_xi(Xc, Xc);   // 2 xi c0 c1
+    f2_mul_xi(s1, s1);
+    f2_add(Tc, s0, s1);  // c0^2 + xi c1^2
+    f2_3u_p2v(x.b0, Xc, x.b0);
+    f2_3u_m2v(x.b1, Tc, x.b1);
+    f2_3u_m2v(x.c0, Tb, x.c0);
+    f2_3u_p2v(x.c1, Xb, x.c1);
+}
+
+// numerators (n0, n1) and denominator D of a0, a1
+DEV void cyc4_num(Fp2& n0, Fp2& n1, Fp2& den, const Cyc4& x) {
+    Fp2 s0, s1, Nb, Nc, t;
+    f2_sqr(s0, x.b0);
+    f2_sqr(s1, x.b1);
+    f2_mul_xi(s1, s1);
+    f2_sub(Nb, s0, s1);
+    f2_sqr(s0, x.c0);
+    f2_sqr(s1, x.c1);
+    f2_mul_xi(s1, s1);
+    f2_sub(Nc, s0, s1);
+    f2_mul(n0, x.b0, Nb);
+    f2_mul(t, x.c1, Nc);
+    f2_mul_xi(t, t);
+    f2_add(n0, n0, t);
+    f2_mul(n1, x.c0, Nc);
+    f2_mul(t, x.b1, Nb);
+    f2_add(n1, n1, t);
+    f2_mul(den, x.b0, x.c0);
+    f2_mul(t, x.b1, x.c1);
+    f2_mul_xi(t, t);
+    f2_sub(den, den, t);
+    f2_dbl(den, den);
+}
+
+DEV void cyc4_expand(Fp12& r, const Cyc4& x, const Fp2& n0, const Fp2& n1, const Fp2& inv) {
+    f2_mul(r.a.a, n0, inv);
+    f2_mul(r.a.b, n1, inv);
+    r.b.a = x.b0;
+    r.b.b = x.b1;
+    r.c.a = x.c0;
+    r.c.b = x.c1;
+}
+
+// snapshot slots (Fp2 pairs) in the K region: per snapshot b0 b1 c0 c1 n0 n1
+DEV void st_cyc4(const Soa& K, int base, size_t i, const Cyc4& x) {
+    st_f2(K, base + 0, i, x.b0);
+    st_f2(K, base + 2, i, x.b1);
+    st_f2(K, base + 4, i, x.c0);
+    st_f2(K, base + 6, i, x.c1);
+}
+DEV void ld_cyc4(Cyc4& x, const Soa& K, int base, size_t i) {
+    ld_f2(x.b0, K, base + 0, i);
+    ld_f2(x.b1, K, base + 2, i);
+    ld_f2(x.c0, K, base + 4, i);
+    ld_f2(x.c1, K, base + 6, i);
+}
+
+// dst <- src^x.  |x| = 2^63 + 2^62 + 2^60 + 2^57 + 2^48 + 2^16: 57 compressed squarings with
+// snapshots g^(2^16), g^(2^48) stored to K; the three compressed values g^(2^16), g^(2^48), g^(2^57)
+// decompressed with ONE inversion (Montgomery's trick); then g^(2^60), g^(2^62), g^(2^63) by six
+// Granger-Scott squarings of g^(2^57) (cheaper than three more decompressions).  Five Fp12
+// multiplications as before.  A zero denominator (b = c = 0 pattern; never reached by honest inputs,
+// e.g. src = 1) sends the lane pair to the Granger-Scott ladder.
+static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i) {
+    Cyc4 c;
+    ld_f2(c.b0, src, 4, i);
+    ld_f2(c.b1, src, 6, i);
+    ld_f2(c.c0, src, 8, i);
+    ld_f2(c.c1, src, 10, i);
+    for (int k = 1; k <= 57; k++) {
+        cyc4_sqr(c);
+        if (k == 16) st_cyc4(K, 0, i, c);
+        if (k == 48) st_cyc4(K, 12, i, c);
+    }
+    Fp2 n0, n1, d57, d16, d48, p1, p2, inv;
+    {
+        Cyc4 s;
+        ld_cyc4(s, K, 0, i);
+        cyc4_num(n0, n1, d16, s);
+        st_f2(K, 8, i, n0);
+        st_f2(K, 10, i, n1);
+        ld_cyc4(s, K, 12, i);
+        cyc4_num(n0, n1, d48, s);
+        st_f2(K, 20, i, n0);
+        st_f2(K, 22, i, n1);
+    }
+    cyc4_num(n0, n1, d57, c);
+    f2_mul(p1, d16, d48);
+    f2_mul(p2, p1, d57);
+    if (f2_is_zero(p2)) {  // pair-uniform
+        fx_pow_x_gs(src, dst, i);
+        return;
+    }
+    f2_inv(inv, p2);
+    Fp12 y, acc, t;
+    {
+        Fp2 i57;
+        f2_mul(i57, inv, p1);
+        cyc4_expand(y, c, n0, n1, i57);  // g^(2^57)
+    }
+    f2_mul(inv, inv, d57);               // (d16 d48)^-1
+    {
+        Cyc4 s;
+        Fp2 ik;
+        f2_mul(ik, inv, d48);
+        ld_cyc4(s, K, 0, i);
+        ld_f2(n0, K, 8, i);
+        ld_f2(n1, K, 10, i);
+        cyc4_expand(acc, s, n0, n1, ik);  // g^(2^16)
+        f2_mul(ik, inv, d16);
+        ld_cyc4(s, K, 12, i);
+        ld_f2(n0, K, 20, i);
+        ld_f2(n1, K, 22, i);
+        cyc4_expand(t, s, n0, n1, ik);    // g^(2^48)
+    }
+    f12_mul(acc, acc, t);
+    f12_mul(acc, acc, y);
+    for (int k = 0; k < 3; k++) f12_cyc_sqr(y, y);
+    f12_mul(acc, acc, y);  // 2^60
+    for (int k = 0; k < 2; k++) f12_cyc_sqr(y, y);
+    f12_mul(acc, acc, y);  // 2^62
+    f12_cyc_sqr(y, y);
+    f12_mul(acc, acc, y);  // 2^63
+    f12_conj(acc, acc);
+    st_f12(dst, i, acc);
+}
+
 // dst <- op_a(a) * op_b(b)
 static __device__ __noinline__ void fx_mul(Soa a, int opa, Soa b, int opb, Soa dst, size_t i) {
     Fp12 x, y;
@@ -78,7 +253,7 @@ static __device__ __noinline__ void fx_mul(Soa a, int opa, Soa b, int opb, Soa d
     st_f12(dst, i, x);
 }
 
-// fbuf: Miller output f (12 slots); scratch: 4 x 12 slots (T, A, S, R)
+// fbuf: Miller output f (12 slots); scratch: 4 x 12 slots (T, A, S, R) + 24 slots K (fx_pow_x snapshots)
 __global__ __launch_bounds__(256, 2) void k_fexp(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
                                               const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
                                               uint8_t* __restrict__ gt_out) {
@@ -86,23 +261,23 @@ __global__ __launch_bounds__(256, 2) void k_fexp(size_t n, uint32_t* __restrict_
     if (i >= n) return;  // pair-uniform
     const Soa F{fbuf, n};
     const Soa T{scratch, n}, A{scratch + (size_t)12 * NL * n, n}, S{scratch + (size_t)24 * NL * n, n},
-        R{scratch + (size_t)36 * NL * n, n};
+        R{scratch + (size_t)36 * NL * n, n}, K{scratch + (size_t)48 * NL * n, n};
     fx_inv(F, T, i);
     fx_mul(F, OP_CONJ, T, OP_ID, F, i);  // f^(p^6 - 1)
     fx_mul(F, OP_FROB2, F, OP_ID, F, i); // ^(p^2 + 1)
     fx_cube(F, R, i);                    // res = f^3
-    fx_pow_x(F, T, i);
+    fx_pow_x(F, T, K, i);
     fx_mul(T, OP_ID, F, OP_CONJ, T, i);  // t = f^(x-1)
-    fx_pow_x(T, A, i);
+    fx_pow_x(T, A, K, i);
     fx_mul(A, OP_ID, T, OP_CONJ, A, i);  // a = f^((x-1)^2)
     fx_mul(A, OP_FROB2, A, OP_CONJ, S, i);
     fx_mul(S, OP_FROB, R, OP_ID, R, i);  // res *= (a^(p^2) a^-1)^p
-    fx_pow_x(A, T, i);                   // b = a^x
+    fx_pow_x(A, T, K, i);                   // b = a^x
     fx_mul(T, OP_FROB2, T, OP_CONJ, S, i);
     fx_mul(S, OP_ID, R, OP_ID, R, i);    // res *= b^(p^2) b^-1
-    fx_pow_x(T, A, i);                   // c = b^x
+    fx_pow_x(T, A, K, i);                   // c = b^x
     fx_mul(A, OP_FROB, R, OP_ID, R, i);  // res *= c^p
-    fx_pow_x(A, T, i);                   // d = c^x
+    fx_pow_x(A, T, K, i);                   // d = c^x
     fx_mul(T, OP_ID, R, OP_ID, R, i);    // res *= d
     Fp12 res;
     ld_f12(res, R, i);

@@ -193,24 +193,10 @@ DEV void f2_mul_xi(Fp2& r, const Fp2& x) {
     }
     fp_add(r.c, x.c, w);  // x + w < 2p
 }
-// a^(p-2) with the pair's two lanes splitting the right-to-left binary method: the real lane squares
-// s = a^(2^i), the imaginary lane multiplies acc by the partner's s (DPP) where bit i of p-2 is set
-// (by Montgomery one elsewhere), both in the same fp_mul.  381 multiplications of critical path
-// against 380 squarings + 228 multiplications for square-and-multiply on one lane (≈27 % fewer mads).
-// a must be equal on both lanes; the result is returned on both.
-DEV void fp_inv_pair(Fp& r, const Fp& a) {
-    const bool im = half_id() != 0;
-    Fp one;
-    fp_one(one);
-    Fp v = fp_sel(im, one, a);
-    for (int bit = 0; bit <= 32 * (NL - 1) + 28; bit++) {
-        const Fp sp = swp(v);
-        const bool set = ((kPm2[bit >> 5] >> (bit & 31)) & 1u) != 0;
-        const Fp y = fp_sel(im, set ? sp : one, v);
-        fp_mul(v, v, y);
-    }
-    r = fp_sel(im, v, swp(v));
-}
+// a must be equal on both lanes; both lanes run the same divsteps (field.h fp_inv), so the pair
+// stays convergent and the result is returned on both.  The divstep inversion costs ~1/20 of the
+// Fermat ladder it replaces, so splitting it across the pair no longer pays.
+DEV void fp_inv_pair(Fp& r, const Fp& a) { fp_inv(r, a); }
 
 // (a + b i)^-1 = (a - b i) / (a^2 + b^2); the norm is computed on both lanes, its inverse split
 DEV void f2_inv(Fp2& r, const Fp2& x) {

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 GPU session: parity tests, micro-benchmark, benches of every mode, rocprof kernel stats.
-# Usage (from the repo root, on the GPU box): bash tools/gpu_r02.sh <tag> [tests|bench|prof|all]
+# Usage (from the repo root, on the GPU box): bash tools/gpu_r02.sh <tag> [tests|bench|quick|modes|prof|all]
 set -o pipefail
 TAG=${1:-r02}
 WHAT=${2:-all}
@@ -26,6 +26,11 @@ if [ "$WHAT" = bench ] || [ "$WHAT" = all ]; then
     run 300 "$OUT/bench_rlc.json" python -u bench.py --mode rlc --steps 5 --warmup 1
     run 400 "$OUT/bench_aggregate.json" python -u bench.py --mode aggregate --steps 3 --warmup 1
     run 400 "$OUT/bench_pok.json" python -u bench.py --mode pok --steps 3 --warmup 1
+fi
+if [ "$WHAT" = quick ]; then
+    run 900 "$OUT/pytest_gpu.log" python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
+    run 300 "$OUT/bench_verify.json" python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline
+    run 300 "$OUT/bench_rlc.json" python -u bench.py --mode rlc --steps 5 --warmup 1 --no-cpu-baseline
 fi
 if [ "$WHAT" = modes ]; then
     run 400 "$OUT/bench_aggregate.json" python -u bench.py --mode aggregate --steps 3 --warmup 1
