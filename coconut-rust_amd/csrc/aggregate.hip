@@ -113,26 +113,6 @@ DEV void recode_w4(int8_t* d, const uint32_t k[8]) {
     d[64] = (int8_t)carry;
 }
 
-// Sum of Jacobian points across the L consecutive lanes of a task (L a power of two <= 64):
-// butterfly over __shfl_xor, every lane ends with the same sum.
-template <class F, int L>
-DEV void lane_group_sum(Jac<F>& acc) {
-    constexpr int JW = sizeof(Jac<F>) / 4;
-#pragma unroll 1
-    for (int m = L >> 1; m > 0; m >>= 1) {
-        Jac<F> o;
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(&acc);
-        uint32_t* w = reinterpret_cast<uint32_t*>(&o);
-        for (int c = 0; c < JW; c++) w[c] = (uint32_t)__shfl_xor((int)a[c], m);
-        // same operand order on both partners so they hold the same representation
-        if (threadIdx.x & m) {
-            Jac<F> t = acc;
-            acc = o;
-            o = t;
-        }
-        jac_add(acc, acc, o);
-    }
-}
 
 // L lanes per task: lane l takes the bases k = l, l + L, ... (t = 67, L = 16: 4-5 bases per lane),
 // builds and normalises their multiples, runs the 65 windows over them, and the L partial sums are

@@ -40,10 +40,14 @@ int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* 
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
-int cck_miller_pl_g2(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-                     uint32_t* d_f, hipStream_t st);
-int cck_miller_pl_g1(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-                     uint32_t* d_f, hipStream_t st);
+int cck_miller_pl_g2(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+                     const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, hipStream_t st);
+int cck_miller_pl_g1(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+                     const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, hipStream_t st);
+size_t cck_fold_words(int mode, size_t n);
+int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok,
+             int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
+             uint32_t* d_flags2, hipStream_t st);
 int cck_fexp_pl(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                 uint8_t* d_gt, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
@@ -59,7 +63,8 @@ int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_ta
                   uint8_t* d_out, hipStream_t st);
 int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
                  const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
-                 uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, hipStream_t st);
+                 uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, uint32_t* d_pts, int8_t* d_dig,
+                 hipStream_t st);
 int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any, uint32_t* d_partial,
                    hipStream_t st);
 int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t* d_flag, hipStream_t st);
@@ -134,6 +139,10 @@ struct cc_ctx {
     DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, vkbinf, msgs_canon, lag;
     // RLC batch mode: ChaCha20 key, identity flag word, partial / gathered partials, verdict
     DevBuf rlc_key, rlc_any, rlc_part, rlc_flag, rlc_accept;
+    // RLC g~-side fold (fold.hip): fold points, delta digits, sort/partials workspace, the 1,024
+    // pseudo-credentials' prep SoA (bucket sums + the fixed points P_w,d = (256^w d) g~) and flags
+    DevBuf rlc_pts, rlc_dig, rlc_work, rlc_prep2, rlc_finf, rlc_flags2;
+    bool rlc_fixed_ok = false;  // P_w,d in rlc_prep2 match the current tables
     DevBuf pok_idx;  // revealed indices of the last PoK batch
     // issuer table (cc_set_issuers): sorted ids, decoded verkeys, per-base 8-bit window tables
     size_t iss_n = 0, iss_q = 0;
@@ -147,6 +156,10 @@ struct cc_ctx {
     float last_ms[3] = {0, 0, 0};
     // orders a caller-supplied stream against the context stream (StreamOrder below)
     hipEvent_t ev_order = nullptr;
+    // RLC fold side stream: the fold and its pseudo-credentials' Miller launch run concurrently with
+    // the credentials' Miller launch (ev_fork after prep, ev_join after the pseudo Miller)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // device set (cc_ctx_create_multi): one single-device context per GPU and one RCCL communicator
     // per GPU (ncclCommInitAll, this process drives every device); empty for a single-device context
     std::vector<cc_ctx*> peers;
@@ -177,12 +190,20 @@ struct StreamOrder {
 };
 
 // mode 0 (SigG2): d_const = g~ affine G1 (24 words); mode 1 (SigG1): g~ Miller lines (68 x 72 words).
-// lane2: pair 1's G1 point is per lane (prep slots S_P2.., Jacobian evaluation form; RLC mode).
-// Pairing kernels run one credential per lane pair (tower_pl.h).
+// np = 1: pair 0 only (RLC credentials; their second pairs are folded, fold.hip).  Pairing kernels
+// run one credential per lane pair (tower_pl.h).  Miller values go to SoA elements [foff, foff + n)
+// of stride fstride (default: n, 0).
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-                      uint32_t* d_f, hipStream_t st, int lane2 = 0) {
-    return mode == 0 ? cck_miller_pl_g2(lane2, n, d_prep, d_flags, d_const, d_f, st)
-                     : cck_miller_pl_g1(lane2, n, d_prep, d_flags, d_const, d_f, st);
+                      uint32_t* d_f, hipStream_t st, int np = 2, size_t fstride = 0, size_t foff = 0) {
+    if (!fstride) fstride = n;
+    return mode == 0 ? cck_miller_pl_g2(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, st)
+                     : cck_miller_pl_g1(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, st);
+}
+// the RLC fold's pseudo-credentials: one (Q, P) pair per lane pair, Q affine G2 and P in evaluation
+// form, both per lane (either group mode: the SigG2 instantiation reads exactly that)
+static int cck_miller_pairs(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
+                            size_t fstride, size_t foff, hipStream_t st) {
+    return cck_miller_pl_g2(0, 1, n, d_prep, d_flags, nullptr, d_f, fstride, foff, st);
 }
 static int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                     uint8_t* d_gt, hipStream_t st) {
@@ -239,6 +260,15 @@ cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
     }
     for (auto& e : c->ev) (void)hipEventCreate(&e);
     (void)hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+    {
+        // high priority: the pseudo-credential Miller launch (64 waves) must get its slots before the
+        // credentials' launch fills the chip (a Miller wave holds its slot for the whole loop)
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess) c->side = nullptr;
+    }
     *out = c;
     return CC_OK;
 }
@@ -260,11 +290,15 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag,
                       &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->pok_idx, &c->rlc_gath,
+                      &c->rlc_pts, &c->rlc_dig, &c->rlc_work, &c->rlc_prep2, &c->rlc_finf, &c->rlc_flags2,
                       &c->iss_ids, &c->iss_aff, &c->iss_inf, &c->iss_table, &c->agg_scratch};
     for (auto* b : bufs) b->release();
     for (auto& b : c->in_aux) b.release();
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+    if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+    if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->side) (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return CC_OK;
@@ -321,6 +355,7 @@ static cc_status rebuild_tables(cc_ctx* c) {
     size_t aw = aff_words(og);
     int nb = (int)c->q + 2;
     c->wbits = verkey_table_bits();
+    c->rlc_fixed_ok = false;
     if (c->table.ensure((size_t)nb * tab_words(og, c->wbits) * 4)) return CC_ERR_HIP;
     if (c->table_inf.ensure((size_t)nb * 4)) return CC_ERR_HIP;
     // [Y~..., g~, X~] are contiguous in vk_aff (X~ at 0, Y~ at 1..q, g~ at q+1, X~ again at q+2)
@@ -496,14 +531,22 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     }
     cc_status s = ensure_work(c, n);
     if (s) return s;
-    if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4)) return CC_ERR_HIP;
+    constexpr size_t NPS = 2048;  // fold pseudo-credentials (one per bucket, one pair each)
+    const size_t N = n + NPS;     // Miller values: n credentials, then the pseudo-credentials
+    if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4) || c->fbuf.ensure(N * 144 * 4) ||
+        c->scratch.ensure(((N + 1) / 2) * 144 * 4 + n * 12 * 4 * 72) || c->rlc_pts.ensure(n * 48 * 4) ||
+        c->rlc_dig.ensure(16 * n) || c->rlc_work.ensure(cck_fold_words(c->mode, n) * 4) ||
+        c->rlc_prep2.ensure((size_t)PREP_SLOTS * 12 * NPS * 4) || c->rlc_finf.ensure(2 * NPS) ||
+        c->rlc_flags2.ensure(NPS * 4))
+        return CC_ERR_HIP;
     memcpy(c->rlc_key_host, seed32, 32);
     HIPCK(hipMemcpyAsync(c->rlc_key.p, c->rlc_key_host, 32, hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_prep_rlc(c->mode, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
                      c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
-                     c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), st));
+                     c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), c->rlc_pts.as<uint32_t>(),
+                     c->rlc_dig.as<int8_t>(), st));
     if (!c->vk_subgroup) {
         // a verkey / g~ point outside the subgroup: the linear-combination argument does not hold,
         // so the batch is never accepted here and the caller verifies per credential (exact)
@@ -512,9 +555,29 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     }
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
-    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st, 1));
+    // the second pairs become 2,048 bucket pairs (fold.hip); their Miller launch (64 waves, latency
+    // bound alone) runs on the high-priority side stream concurrently with pair 0 of every credential
+    // on st; both write disjoint ranges of fbuf (stride N).  The fold's own short kernels run first,
+    // alone (behind a full Miller launch each would wait milliseconds for a free slot).
+    KCK(cck_fold(c->mode, n, c->rlc_dig.as<int8_t>(), c->rlc_pts.as<uint32_t>(), c->rlc_work.as<uint32_t>(),
+                 c->rlc_fixed_ok ? 1 : 0, (int)q, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(),
+                 c->rlc_prep2.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_flags2.as<uint32_t>(), st));
+    c->rlc_fixed_ok = true;
+    hipStream_t side = c->side ? c->side : st;
+    if (side != st) {
+        HIPCK(hipEventRecord(c->ev_fork, st));
+        HIPCK(hipStreamWaitEvent(side, c->ev_fork, 0));
+    }
+    KCK(cck_miller_pairs(NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(), c->fbuf.as<uint32_t>(), N, n,
+                         side));
+    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st, 1, N,
+                   0));
+    if (side != st) {
+        HIPCK(hipEventRecord(c->ev_join, side));
+        HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));
+    }
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
-    KCK(cck_rlc_reduce(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,
+    KCK(cck_rlc_reduce(N, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,
                        st));
     if (c->timing) {
         (void)hipEventRecord(c->ev[3], st);

@@ -1,0 +1,261 @@
+// The g~-side fold of the RLC batch mode (BASELINE config 3) for gfx950.
+//
+// RLC checks prod_i e(sigma_1,i, delta_i pr_i) e(-sigma_2,i, delta_i g~) == 1 (SigG2; SigG1 swaps the
+// pairing arguments, rlc.hip).  The second factors share g~, so
+//     prod_i e(-sigma_2,i, delta_i g~) = e(sum_i delta_i (-sigma_2,i), g~).
+// delta_i is drawn as 16 signed base-256 digits d_w,i in [-128, 127] (fr.h rlc_delta_signed), so
+//     sum_i delta_i X_i = sum_w sum_{d=1..128} (256^w d) B_w,d,   B_w,d = sum_{i: |d_w,i| = d} sign X_i
+// and instead of ONE sequential Horner combination (128 doublings of one point: ~2k dependent Fp
+// multiplications on one lane, milliseconds of latency) the scalars 256^w d move to the OTHER pairing
+// argument, whose points P_w,d = (256^w d) g~ are fixed per verkey:
+//     prod = prod_{w,d} e(B_w,d, P_w,d)       (2,048 one-pair pseudo-credentials)
+// The per-credential Miller loop keeps pair 0 only (NP = 1: ~40 % fewer multiplications); the fold
+// costs ~16 mixed additions per credential (one per window) and a 2,048-lane-pair Miller launch that
+// the host runs on a second stream, concurrently with the credentials' Miller launch (alone it
+// would be latency-bound: 64 waves on 1,024 SIMDs).
+//
+//   k_fold_count / k_fold_scan / k_fold_scatter : counting sort of the (w, i) digits into 2,048
+//                                                 bucket lists, each padded to FS-entry chunks
+//   k_fold_sum<F>                               : one lane per chunk: mixed additions of its points
+//   k_fold_reduce<F>                            : one wave per bucket: chunk partials, butterfly, affine
+//   k_fold_fixed<F>                             : the fixed points P_w,d (once per verkey)
+// X_i = -sigma_2,i (AoS affine, written by the RLC prep); B_w,d lands in the pseudo-credentials' prep
+// SoA (soa.h slots, stride FB; bucket b = pseudo-credential b, pair 0) as the Q side (SigG2: B in G2)
+// or the P side (SigG1: B in G1), P_w,d on the other side.
+#include "codec.h"
+#include "fixed.h"
+#include "soa.h"
+
+using namespace cc;
+
+namespace {
+
+constexpr int FW = 16;        // windows: signed base-256 digits of delta
+constexpr int FD = 128;       // |digit| values per window
+constexpr int FB = FW * FD;   // buckets
+constexpr int FS = 16;        // list entries per chunk (one lane)
+constexpr uint32_t PAD = 0xffffffffu;
+
+template <class F>
+DEV void ld_aff_aos(Aff<F>& a, const uint32_t* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4* d = reinterpret_cast<uint4*>(&a);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(Aff<F>) / 16); k++) d[k] = q[k];
+}
+template <class F>
+DEV void st_jac_aos(uint32_t* p, const Jac<F>& a) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    const uint4* s = reinterpret_cast<const uint4*>(&a);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(Jac<F>) / 16); k++) q[k] = s[k];
+}
+template <class F>
+DEV void ld_jac_aos(Jac<F>& a, const uint32_t* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4* d = reinterpret_cast<uint4*>(&a);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(Jac<F>) / 16); k++) d[k] = q[k];
+}
+
+// a point as the pair argument of a pseudo-credential: Q (affine G2, slots Q1) or P (G1, evaluation
+// form (x, y, 1), slots P1)
+DEV void st_as_q(const Soa& S, size_t j, const Aff<Fp2>& a) {
+    st_f2(S, S_Q1, j, a.x);
+    st_f2(S, S_Q1 + 2, j, a.y);
+}
+DEV void st_as_p(const Soa& S, size_t j, const Aff<Fp>& a) {
+    const int s = S_P1;
+    Fp one;
+    fp_one(one);
+    st_fp(S, s, j, a.x);
+    st_fp(S, s + 1, j, a.y);
+    st_fp(S, s + 2, j, one);
+}
+
+}  // namespace
+
+// per-window histograms of |digit| (LDS, then one global add per bucket and block)
+__global__ __launch_bounds__(256) void k_fold_count(size_t n, const int8_t* __restrict__ dig,
+                                                    uint32_t* __restrict__ cnt) {
+    __shared__ uint32_t h[FD];
+    const int w = blockIdx.y;
+    for (int t = threadIdx.x; t < FD; t += blockDim.x) h[t] = 0;
+    __syncthreads();
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int d = dig[(size_t)w * n + i];
+        if (d) atomicAdd(&h[(d < 0 ? -d : d) - 1], 1u);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < FD; t += blockDim.x)
+        if (h[t]) atomicAdd(&cnt[w * FD + t], h[t]);
+}
+
+// padded bucket offsets (off[FB] = total) and scatter cursors; one block
+__global__ __launch_bounds__(256) void k_fold_scan(const uint32_t* __restrict__ cnt, uint32_t* __restrict__ off,
+                                                   uint32_t* __restrict__ cur) {
+    constexpr int PT = FB / 256;
+    __shared__ uint32_t s[256];
+    const int t = threadIdx.x;
+    uint32_t loc[PT], pc[PT], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PT; k++) {
+        pc[k] = (cnt[t * PT + k] + FS - 1) / FS * FS;
+        loc[k] = sum;
+        sum += pc[k];
+    }
+    s[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const uint32_t v = t >= o ? s[t - o] : 0u;
+        __syncthreads();
+        s[t] += v;
+        __syncthreads();
+    }
+    const uint32_t base = t ? s[t - 1] : 0u;
+#pragma unroll
+    for (int k = 0; k < PT; k++) {
+        const int b = t * PT + k;
+        const uint32_t o = base + loc[k];
+        off[b] = o;
+        cur[b] = o;
+    }
+    if (t == 255) off[FB] = s[255];
+}
+
+// list[pos] = i | sign << 31 for every nonzero digit (order inside a bucket is irrelevant: sums)
+__global__ __launch_bounds__(256) void k_fold_scatter(size_t n, const int8_t* __restrict__ dig,
+                                                      uint32_t* __restrict__ cur, uint32_t* __restrict__ list) {
+    const int w = blockIdx.y;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int d = dig[(size_t)w * n + i];
+        if (!d) continue;
+        const uint32_t pos = atomicAdd(&cur[w * FD + (d < 0 ? -d : d) - 1], 1u);
+        list[pos] = (uint32_t)i | (d < 0 ? 0x80000000u : 0u);
+    }
+}
+
+// one lane per FS-entry chunk (all of one bucket): Jacobian partial sum of its signed points
+template <class F>
+__global__ __launch_bounds__(256) void k_fold_sum(size_t maxchunks, const uint32_t* __restrict__ off,
+                                                  const uint32_t* __restrict__ list, const uint32_t* __restrict__ pts,
+                                                  uint32_t* __restrict__ part) {
+    constexpr int AW = sizeof(Aff<F>) / 4, JW = sizeof(Jac<F>) / 4;
+    const size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (c >= maxchunks || c * FS >= off[FB]) return;
+    Jac<F> acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (int e = 0; e < FS; e++) {
+        const uint32_t v = list[c * FS + e];
+        if (v == PAD) continue;
+        Aff<F> a;
+        ld_aff_aos<F>(a, pts + (size_t)(v & 0x7fffffffu) * AW);
+        if (v >> 31) FT<F>::neg(a.y, a.y);
+        jac_add_aff(acc, acc, a);
+    }
+    st_jac_aos<F>(part + c * JW, acc);
+}
+
+// one wave per bucket: lane-strided sum of the bucket's chunk partials, butterfly across the wave,
+// affine; written as pseudo-credential b.  kBisQ: B is the Q side (SigG2).
+template <class F, bool kBisQ>
+__global__ __launch_bounds__(64) void k_fold_reduce(const uint32_t* __restrict__ off, const uint32_t* __restrict__ part,
+                                                    const uint8_t* __restrict__ fixed_inf, uint32_t* __restrict__ prep2,
+                                                    uint32_t* __restrict__ flags2) {
+    constexpr int JW = sizeof(Jac<F>) / 4;
+    const int b = blockIdx.x;
+    const uint32_t c0 = off[b] / FS, c1 = off[b + 1] / FS;
+    Jac<F> acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (uint32_t c = c0 + threadIdx.x; c < c1; c += 64) {
+        Jac<F> p;
+        ld_jac_aos<F>(p, part + (size_t)c * JW);
+        jac_add(acc, acc, p);
+    }
+    lane_group_sum<F, 64>(acc);
+    if (threadIdx.x != 0) return;
+    Aff<F> a;
+    const bool fin = jac_to_aff(a, acc);
+    const Soa S{prep2, FB};
+    if constexpr (kBisQ) st_as_q(S, b, a);
+    else st_as_p(S, b, a);
+    flags2[b] = (!fin || fixed_inf[b]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
+}
+
+// P_w,d = (256^w d) g~ from g~'s fixed-base table (base index q of the verkey tables); G is g~'s field
+template <class G>
+__global__ __launch_bounds__(256) void k_fold_fixed(int q, const uint32_t* __restrict__ table, int wbits,
+                                                    const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep2,
+                                                    uint8_t* __restrict__ fixed_inf) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= FB) return;
+    const int w = b / FD, d = b % FD + 1;
+    uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    s[w >> 2] = (uint32_t)d << (8 * (w & 3));
+    Jac<G> acc;
+    jac_set_inf(acc);
+    if (!binf[q]) ft_add<G>(acc, s, table, wbits, q, 0, ft_nwin(wbits));
+    Aff<G> a;
+    const bool fin = jac_to_aff(a, acc);
+    fixed_inf[b] = fin ? 0 : 1;
+    const Soa S{prep2, FB};
+    if constexpr (sizeof(G) == sizeof(Fp)) st_as_p(S, b, a);  // SigG2: g~ in G1
+    else st_as_q(S, b, a);                                     // SigG1: g~ in G2
+}
+
+static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// work-buffer layout (32-bit words): cnt FB | off FB+1 | cur FB (+3) | list maxchunks*FS |
+// part maxchunks*JW (16-byte aligned)
+static size_t fold_maxchunks(size_t n) { return (FW * n + (size_t)FB * (FS - 1)) / FS + 1; }
+
+extern "C" {
+
+size_t cck_fold_words(int mode, size_t n) {
+    const size_t jw = mode == 0 ? sizeof(Jac<Fp2>) / 4 : sizeof(Jac<Fp>) / 4;
+    const size_t mc = fold_maxchunks(n);
+    return 3 * (size_t)FB + 1 + 3 + mc * FS + mc * jw + 4;
+}
+
+// mode 0 (SigG2): X_i in G2 (AoS affine, 48 words), g~ in G1; mode 1: X_i in G1 (24 words), g~ in G2.
+// d_dig: [FW][n] int8 digits (0 for credentials to leave out).  fixed_ok = 0 recomputes P_w,d into
+// d_prep2 and their identity flags into d_finf (FB bytes); both persist between calls.
+// d_prep2: PREP_SLOTS x FB SoA; d_flags2: FB words (pair-0 skip flags of the pseudo-credentials).
+int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok, int q,
+             const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
+             uint32_t* d_flags2, hipStream_t st) {
+    if (!n) return -1;
+    const size_t mc = fold_maxchunks(n);
+    uint32_t* cnt = d_work;
+    uint32_t* off = cnt + FB;
+    uint32_t* cur = off + FB + 1;
+    uint8_t* finf = d_finf;
+    uint32_t* list = cur + FB + 3;
+    uint32_t* part = reinterpret_cast<uint32_t*>(((uintptr_t)(list + mc * FS) + 15) & ~(uintptr_t)15);
+    if (!fixed_ok) {
+        if (mode == 0)
+            hipLaunchKernelGGL(k_fold_fixed<Fp>, dim3(FB / 256), dim3(256), 0, st, q, d_table, wbits, d_binf, d_prep2,
+                               finf);
+        else
+            hipLaunchKernelGGL(k_fold_fixed<Fp2>, dim3(FB / 256), dim3(256), 0, st, q, d_table, wbits, d_binf,
+                               d_prep2, finf);
+    }
+    if (hipMemsetAsync(cnt, 0, FB * 4, st) != hipSuccess || hipMemsetAsync(list, 0xff, mc * FS * 4, st) != hipSuccess)
+        return -1;
+    const dim3 gw(nblocks(n, 256) < 64 ? nblocks(n, 256) : 64, FW);
+    hipLaunchKernelGGL(k_fold_count, gw, dim3(256), 0, st, n, d_dig, cnt);
+    hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(256), 0, st, cnt, off, cur);
+    hipLaunchKernelGGL(k_fold_scatter, gw, dim3(256), 0, st, n, d_dig, cur, list);
+    if (mode == 0) {
+        hipLaunchKernelGGL(k_fold_sum<Fp2>, dim3(nblocks(mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
+        hipLaunchKernelGGL((k_fold_reduce<Fp2, true>), dim3(FB), dim3(64), 0, st, off, part, finf, d_prep2, d_flags2);
+    } else {
+        hipLaunchKernelGGL(k_fold_sum<Fp>, dim3(nblocks(mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
+        hipLaunchKernelGGL((k_fold_reduce<Fp, false>), dim3(FB), dim3(64), 0, st, off, part, finf, d_prep2, d_flags2);
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // extern "C"

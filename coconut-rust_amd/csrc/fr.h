@@ -164,4 +164,32 @@ DEV void rlc_delta(uint32_t d[NR], const uint32_t key[8], uint64_t g) {
     d[4] = d[5] = d[6] = d[7] = 0u;
 }
 
+// RLC coefficient as 16 signed base-256 digits: the 16 ChaCha20 bytes b_w read as int8 d_w in
+// [-128, 127], delta = sum_w d_w 256^w (uniform over 2^128 consecutive integers around 0, so a
+// forged batch still passes with probability <= 2^-127).  The g~-side fold (fold.hip) buckets by
+// (w, |d_w|) with no carry digit.  d = delta mod r (canonical): with U = sum b_w 256^w and
+// H = sum [b_w >= 128] 256^w, delta = U - 256 H.  dig: the 16 digit bytes (= the key-stream bytes).
+DEV void rlc_delta_signed(uint32_t d[NR], uint32_t dig[4], const uint32_t key[8], uint64_t g) {
+    uint32_t blk[16];
+    chacha20_block(blk, key, (uint32_t)g, (uint32_t)(g >> 32), 0u, 0u);
+    uint32_t h[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        dig[k] = blk[k];
+        h[k] = (blk[k] >> 7) & 0x01010101u;
+    }
+    const uint32_t m[5] = {h[0] << 8, (h[1] << 8) | (h[0] >> 24), (h[2] << 8) | (h[1] >> 24),
+                           (h[3] << 8) | (h[2] >> 24), h[3] >> 24};
+    uint32_t br = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) d[k] = __builtin_subc(k < 4 ? blk[k] : 0u, m[k], br, &br);
+    const uint32_t ext = br ? 0xffffffffu : 0u;  // sign extension of U - 256 H
+    d[5] = d[6] = d[7] = ext;
+    if (br) {  // negative: + r
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < NR; k++) d[k] = __builtin_addc(d[k], rl(k), c, &c);
+    }
+}
+
 }  // namespace cc

@@ -15,9 +15,10 @@
 // the multiplication temporaries.  The 5 addition steps run out of line (rare; keeps code size down).
 //
 //   SigG2: pair 0 = (sigma_1, pr) with pr in Jacobian-evaluation form (XZ, Y, Z^3);
-//          pair 1 = (-sigma_2, g~): g~ affine constant, or per lane (RLC mode: delta_i g~).
-//   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2), where
-//          -sigma_2 is affine, or per-lane Jacobian-evaluation form (RLC mode: -delta_i sigma_2).
+//          pair 1 = (-sigma_2, g~): g~ affine constant, or per lane (lane2: the RLC fold's
+//          pseudo-credentials, two (bucket, fixed point) pairs each, fold.hip).
+//   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2).
+//   RLC mode runs pair 0 alone (NP = 1): its second pairs are folded (fold.hip).
 #ifndef CC_MILLER_SIG
 #define CC_MILLER_SIG 2
 #endif
@@ -126,11 +127,13 @@ static __device__ __noinline__ void miller_add(StepState* st, const uint32_t* qs
 // cst: SigG2 -> g~ affine (24 words, used when !kLane2); SigG1 -> g~ lines (68 x 72 words)
 // SIG is a template parameter (not only the macro) so the two objects' instantiations have distinct
 // symbol names: the same name in both would be merged by the linker as one weak definition.
-template <int SIG, bool kLane2>
+// NP = 1: pair 0 only (RLC mode, whose second pairs are folded into per-bucket pairs, fold.hip).
+// The Miller value of credential i goes to fout as SoA element foff + i of stride fstride.
+template <int SIG, bool kLane2, int NP>
 __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __restrict__ prep,
                                                const uint32_t* __restrict__ flags, const uint32_t* __restrict__ cst,
-                                               uint32_t* __restrict__ fout) {
-    __shared__ uint32_t lds[TW][MB];
+                                               uint32_t* __restrict__ fout, size_t fstride, size_t foff) {
+    __shared__ uint32_t lds[NP == 2 ? TW : 1][MB];
     const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
     if (i >= n) return;  // pair-uniform
     constexpr bool kSigG2 = SIG == 2;
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
     const uint32_t* q1 = prep + (size_t)S_Q2 * NL * n;
     const Soa S{const_cast<uint32_t*>(prep), n};
     G2Proj T;
-    if (kSigG2) {  // park pair 1's T = -sigma_2
+    if (kSigG2 && NP == 2) {  // park pair 1's T = -sigma_2
         ld_f2(T.x, S, S_Q2, i);
         ld_f2(T.y, S, S_Q2 + 2, i);
         f2_one(T.z);
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
     for (int b = 62; b >= 0; b--) {
         if (b != 62) f12_sqr(f, f);
 #pragma unroll 1
-        for (int k = 0; k < 2; k++) {
+        for (int k = 0; k < NP; k++) {
             Fp2 l0, l2, l3;
             if (!kSigG2 && k == 1) {
                 ld_line(l0, l2, l3, gl);
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
                 line_dbl(T, l0, l2, l3);
             }
             eval_mul(f, l0, l2, l3, k ? ps1 : ps0, i, k ? skip1 : skip0);
-            if (kSigG2) {  // swap T with the parked one
+            if (kSigG2 && NP == 2) {  // swap T with the parked one
                 G2Proj U;
                 unpark(U, lds);
                 park(lds, T);
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
         }
         if ((X_ABS >> b) & 1ull) {
 #pragma unroll 1
-            for (int k = 0; k < 2; k++) {
+            for (int k = 0; k < NP; k++) {
                 StepState st;
                 st.f = f;
                 st.T = T;
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
                 if (const_line) gl += 72;
                 f = st.f;
                 T = st.T;
-                if (kSigG2) {
+                if (kSigG2 && NP == 2) {
                     G2Proj U;
                     unpark(U, lds);
                     park(lds, T);
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
         }
     }
     f12_conj(f, f);
-    st_f12(Soa{fout, n}, i, f);
+    st_f12(Soa{fout, fstride}, foff + i, f);
 }
 
 }  // namespace pl
@@ -214,14 +217,22 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
 #define CC_MILLER_LAUNCH cck_miller_pl_g1
 #endif
 
-extern "C" int CC_MILLER_LAUNCH(int lane2, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
-                                const uint32_t* d_const, uint32_t* d_f, hipStream_t st) {
+// lane2: per-lane second-pair P (RLC pseudo-pairs); np: pairs per credential (1 or 2); the Miller
+// values go to SoA elements [foff, foff + n) of stride fstride (>= foff + n)
+extern "C" int CC_MILLER_LAUNCH(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+                                const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, hipStream_t st) {
     if (!n) return 0;
+    if (fstride < foff + n || (np != 1 && np != 2)) return -1;
     constexpr int MB = cc::pl::MB;
     dim3 g((unsigned)((2 * n + MB - 1) / MB)), b(MB);
-    if (lane2)
-        hipLaunchKernelGGL((cc::pl::k_miller<CC_MILLER_SIG, true>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f);
+    if (np == 1)
+        hipLaunchKernelGGL((cc::pl::k_miller<CC_MILLER_SIG, false, 1>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+                           fstride, foff);
+    else if (lane2)
+        hipLaunchKernelGGL((cc::pl::k_miller<CC_MILLER_SIG, true, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+                           fstride, foff);
     else
-        hipLaunchKernelGGL((cc::pl::k_miller<CC_MILLER_SIG, false>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f);
+        hipLaunchKernelGGL((cc::pl::k_miller<CC_MILLER_SIG, false, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+                           fstride, foff);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

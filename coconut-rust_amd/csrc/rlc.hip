@@ -6,20 +6,23 @@
 //     prod_i e(sigma_1,i, delta_i pr_i) * e(-sigma_2,i, delta_i g~) == 1        (SigG2)
 //     prod_i e(delta_i pr_i, sigma_1,i) * e(g~, -delta_i sigma_2,i) == 1        (SigG1)
 //
-// with independent 128-bit delta_i (ChaCha20 keyed by a fresh host seed): one Miller loop per
-// credential, the product of all Miller values, and ONE final exponentiation per batch (or, over
-// several GPUs, one per gathered set of per-GPU partial products).  A forged credential passes with
-// probability <= 2^-127.  If the batch fails, or any sigma is the identity (which the per-credential
+// with independent delta_i (ChaCha20 keyed by a fresh host seed, 16 signed base-256 digits: fr.h
+// rlc_delta_signed): the second pairs share g~ and are folded into 2,048 bucket pairs (fold.hip), so
+// each credential runs a ONE-pair Miller loop; then the product of all Miller values and ONE final
+// exponentiation per batch (or, over several GPUs, one per gathered set of per-GPU partial products).
+// A forged credential passes with probability <= 2^-127.  If the batch fails, or any sigma is the identity (which the per-credential
 // semantics reject), the caller falls back to per-credential verification, so verdicts always equal
 // the reference's.
 //
-//   k_prep_rlc_sigg2 / k_prep_rlc_sigg1 : decode, delta, delta-scaled fixed-base MSM (delta X + sum
-//                                         (delta m_j) Y_j) and the delta-scaled second pair, written
-//                                         in the Miller kernels' SoA operand layout (soa.h)
+//   k_rlc_check_* / k_rlc_msm_*        : decode, subgroup checks and the fold's inputs (-sigma_2,
+//                                         delta's digits); the delta-scaled fixed-base MSM
+//                                         (delta X + sum (delta m_j) Y_j) of pair 0 in the Miller
+//                                         kernels' SoA layout (soa.h)
 //   k_f12_reduce                        : one level of the pairwise product tree of Fp12 values
 //   k_rlc_partial_out / k_rlc_combine   : 145-word partial (Fp12 Montgomery words + identity flag),
 //                                         and the product of gathered partials ahead of k_fexp
 #include "codec.h"
+#include "curve_pl.h"
 #include "fixed.h"
 #include "fr.h"
 #include "pairing.h"
@@ -44,39 +47,88 @@ DEV void st_eval(const Soa& S, int slot, size_t i, const Jac<Fp>& P) {
 }  // namespace
 
 // Tables: bases [Y~_0 .. Y~_{q-1}, g~, X~] (indices 0..q-1, q, q+1) of cc_set_verkey.
-// flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 delta pr = O, bit4 second pair degenerate.
-__global__ __launch_bounds__(256) void k_prep_rlc_sigg2(size_t n, int q, uint64_t base_index,
-                                                        const uint32_t* __restrict__ key,
-                                                        const uint8_t* __restrict__ s1b,
-                                                        const uint8_t* __restrict__ s2b,
-                                                        const uint8_t* __restrict__ msgs,
-                                                        const uint32_t* __restrict__ table, int wbits,
-                                                        const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
-                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ any) {
+// flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 delta pr = O, bit5 sigma outside the subgroup.
+// Per credential: pair 0 of the Miller loop (sigma_1 with delta pr, SoA slots of soa.h), the fold
+// point X_i = -sigma_2,i (AoS affine, pts) and delta's 16 signed digits (dig[w * n + i]; all zero when
+// sigma_2 is the identity, which fails the batch anyway).  delta X~ runs over all windows: delta is
+// used mod r (fr.h rlc_delta_signed).
+
+template <class F>
+DEV void st_aff_aos(uint32_t* p, const Aff<F>& a) {
+    uint4* o = reinterpret_cast<uint4*>(p);
+    const uint4* w = reinterpret_cast<const uint4*>(&a);
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(Aff<F>) / 16); k++) o[k] = w[k];
+}
+
+// Two kernels per group mode (split so each keeps its registers within 2 waves/SIMD):
+//   k_rlc_check_* : decode sigma_1 / sigma_2, subgroup checks, the fold's inputs (-sigma_2 and
+//                   delta's digits), flags bits 0, 1, 5 and the batch's fall-back flag
+//   k_rlc_msm_*   : delta X~ + sum (delta m_j) Y~_j (delta recomputed from the key stream) as pair 0's
+//                   other argument, flag bit 2
+// one credential per lane PAIR: lane h decodes sigma_{h+1} and writes its outputs (h = 0: sigma_1 as
+// pair 0's Q; h = 1: the fold point -sigma_2); both subgroup checks run on the pair-lane Fp2
+// (curve_pl.h: 3 Fp a lane for a Jacobian G2 point); each lane writes 8 of delta's 16 digits.
+__global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t base_index,
+                                                            const uint32_t* __restrict__ key,
+                                                            const uint8_t* __restrict__ s1b,
+                                                            const uint8_t* __restrict__ s2b,
+                                                            uint32_t* __restrict__ prep, uint32_t* __restrict__ flags,
+                                                            uint32_t* __restrict__ any, uint32_t* __restrict__ pts,
+                                                            int8_t* __restrict__ dig) {
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t i = g >> 1;
+    const int h = (int)(g & 1);
+    if (i >= n) return;  // pair-uniform
+    const Soa S{prep, n};
+    uint32_t fl = 0;
+    Aff<Fp2> a;
+    if (!g2_decode(a, (h ? s2b : s1b) + i * 192)) fl |= h ? 2u : 1u;
+    if (!h) {
+        st_f2(S, S_Q1, i, a.x);
+        st_f2(S, S_Q1 + 2, i, a.y);
+    } else {
+        Aff<Fp2> m = a;
+        f2_neg(m.y, m.y);
+        st_aff_aos<Fp2>(pts + i * (sizeof(Aff<Fp2>) / 4), m);
+    }
+    fl |= pl::swp(fl);  // both decode flags on both lanes
+    Aff<pl::Fp2> p;
+    p.x = pl::f2_from_lane(a.x, 0);
+    p.y = pl::f2_from_lane(a.y, 0);
+    if (!(fl & 1u) && !pl::g2_in_subgroup(p)) fl |= 32u;
+    p.x = pl::f2_from_lane(a.x, 1);
+    p.y = pl::f2_from_lane(a.y, 1);
+    if (!(fl & 2u) && !pl::g2_in_subgroup(p)) fl |= 32u;
+    uint32_t kk[NR], d[NR], w4[4];
+    for (int k = 0; k < 8; k++) kk[k] = key[k];
+    rlc_delta_signed(d, w4, kk, base_index + i);
+    const bool on = (fl & 2u) == 0;
+#pragma unroll
+    for (int w = 8 * h; w < 8 * h + 8; w++)
+        dig[(size_t)w * n + i] = on ? (int8_t)((w4[w >> 2] >> (8 * (w & 3))) & 0xffu) : 0;
+    if (!h) {
+        flags[i] = fl;
+        if (fl & 35u) atomicOr(any, 1u);  // identity or non-subgroup sigma: the batch falls back
+    }
+}
+
+__global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, int q, uint64_t base_index,
+                                                          const uint32_t* __restrict__ key,
+                                                          const uint8_t* __restrict__ msgs,
+                                                          const uint32_t* __restrict__ table, int wbits,
+                                                          const uint32_t* __restrict__ binf,
+                                                          uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
     const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Soa S{prep, n};
-    uint32_t fl = 0;
-    {
-        Aff<Fp2> a;
-        if (!g2_decode(a, s1b + i * 192)) fl |= 1u;
-        else if (!g2_in_subgroup(a)) fl |= 32u;
-        st_f2(S, S_Q1, i, a.x);
-        st_f2(S, S_Q1 + 2, i, a.y);
-        if (!g2_decode(a, s2b + i * 192)) fl |= 2u;
-        else if (!g2_in_subgroup(a)) fl |= 32u;
-        f2_neg(a.y, a.y);
-        st_f2(S, S_Q2, i, a.x);
-        st_f2(S, S_Q2 + 2, i, a.y);
-    }
-    uint32_t kk[NR];
+    uint32_t kk[NR], d[NR], w4[4];
     for (int k = 0; k < 8; k++) kk[k] = key[k];
-    uint32_t d[NR];
-    rlc_delta(d, kk, base_index + i);
+    rlc_delta_signed(d, w4, kk, base_index + i);
     Jac<Fp> acc;
     jac_set_inf(acc);
     const int nwin = ft_nwin(wbits);
-    if (!binf[q + 1]) ft_add<Fp>(acc, d, table, wbits, q + 1, 0, nwin / 2);  // delta X~ (128-bit delta)
+    if (!binf[q + 1]) ft_add<Fp>(acc, d, table, wbits, q + 1, 0, nwin);  // delta X~
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
@@ -85,58 +137,64 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg2(size_t n, int q, uint64_
         fr_mul_canon(dm, d, m.v);
         ft_add<Fp>(acc, dm, table, wbits, j, 0, nwin);
     }
-    if (jac_is_inf(acc)) fl |= 4u;
+    if (jac_is_inf(acc)) flags[i] |= 4u;
     st_eval(S, S_P1, i, acc);
-    jac_set_inf(acc);
-    if (!binf[q]) ft_add<Fp>(acc, d, table, wbits, q, 0, nwin / 2);  // delta g~
-    if (jac_is_inf(acc)) fl |= 16u;
-    st_eval(S, S_P2, i, acc);
-    flags[i] = fl;
-    if (fl & 35u) atomicOr(any, 1u);  // identity or non-subgroup sigma: the batch falls back
 }
 
-__global__ __launch_bounds__(256) void k_prep_rlc_sigg1(size_t n, int q, uint64_t base_index,
-                                                        const uint32_t* __restrict__ key,
-                                                        const uint8_t* __restrict__ s1b,
-                                                        const uint8_t* __restrict__ s2b,
-                                                        const uint8_t* __restrict__ msgs,
-                                                        const uint32_t* __restrict__ table, int wbits,
-                                                        const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
-                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ any) {
+// one credential per lane pair: lane h decodes and subgroup-checks sigma_{h+1} (one-lane G1)
+__global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, uint64_t base_index,
+                                                            const uint32_t* __restrict__ key,
+                                                            const uint8_t* __restrict__ s1b,
+                                                            const uint8_t* __restrict__ s2b,
+                                                            uint32_t* __restrict__ prep, uint32_t* __restrict__ flags,
+                                                            uint32_t* __restrict__ any, uint32_t* __restrict__ pts,
+                                                            int8_t* __restrict__ dig) {
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t i = g >> 1;
+    const int h = (int)(g & 1);
+    if (i >= n) return;  // pair-uniform
+    const Soa S{prep, n};
+    uint32_t fl = 0;
+    Aff<Fp> a;
+    if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
+    else if (!g1_in_subgroup(a)) fl |= 32u;
+    if (!h) {
+        st_fp(S, S_P1, i, a.x);
+        st_fp(S, S_P1 + 1, i, a.y);
+    } else {
+        fp_neg(a.y, a.y);
+        st_aff_aos<Fp>(pts + i * (sizeof(Aff<Fp>) / 4), a);
+    }
+    fl |= pl::swp(fl);
+    uint32_t kk[NR], d[NR], w4[4];
+    for (int k = 0; k < 8; k++) kk[k] = key[k];
+    rlc_delta_signed(d, w4, kk, base_index + i);
+    const bool on = (fl & 2u) == 0;
+#pragma unroll
+    for (int w = 8 * h; w < 8 * h + 8; w++)
+        dig[(size_t)w * n + i] = on ? (int8_t)((w4[w >> 2] >> (8 * (w & 3))) & 0xffu) : 0;
+    if (!h) {
+        flags[i] = fl;
+        if (fl & 35u) atomicOr(any, 1u);  // identity or non-subgroup sigma: the batch falls back
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rlc_msm_sigg1(size_t n, int q, uint64_t base_index,
+                                                          const uint32_t* __restrict__ key,
+                                                          const uint8_t* __restrict__ msgs,
+                                                          const uint32_t* __restrict__ table, int wbits,
+                                                          const uint32_t* __restrict__ binf,
+                                                          uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
     const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Soa S{prep, n};
-    uint32_t fl = 0;
-    uint32_t kk[NR];
+    uint32_t kk[NR], d[NR], w4[4];
     for (int k = 0; k < 8; k++) kk[k] = key[k];
-    uint32_t d[NR];
-    rlc_delta(d, kk, base_index + i);
-    {
-        Aff<Fp> a;
-        if (!g1_decode(a, s1b + i * 97)) fl |= 1u;
-        else if (!g1_in_subgroup(a)) fl |= 32u;
-        st_fp(S, S_P1, i, a.x);
-        st_fp(S, S_P1 + 1, i, a.y);
-        // -delta sigma_2 (variable base, 128-bit double-and-add)
-        Jac<Fp> s;
-        jac_set_inf(s);
-        if (g1_decode(a, s2b + i * 97)) {
-            if (!g1_in_subgroup(a)) fl |= 32u;
-            for (int b = 127; b >= 0; b--) {
-                jac_dbl(s, s);
-                if ((d[b >> 5] >> (b & 31)) & 1u) jac_add_aff(s, s, a);
-            }
-            fp_neg(s.y, s.y);
-        } else {
-            fl |= 2u;
-        }
-        if (jac_is_inf(s)) fl |= 16u;
-        st_eval(S, S_P2, i, s);
-    }
+    rlc_delta_signed(d, w4, kk, base_index + i);
     Jac<Fp2> acc;
     jac_set_inf(acc);
     const int nwin = ft_nwin(wbits);
-    if (!binf[q + 1]) ft_add<Fp2>(acc, d, table, wbits, q + 1, 0, nwin / 2);
+    if (!binf[q + 1]) ft_add<Fp2>(acc, d, table, wbits, q + 1, 0, nwin);
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
@@ -146,11 +204,9 @@ __global__ __launch_bounds__(256) void k_prep_rlc_sigg1(size_t n, int q, uint64_
         ft_add<Fp2>(acc, dm, table, wbits, j, 0, nwin);
     }
     Aff<Fp2> a2;
-    if (!jac_to_aff(a2, acc)) fl |= 4u;
+    if (!jac_to_aff(a2, acc)) flags[i] |= 4u;
     st_f2(S, S_Q1, i, a2.x);
     st_f2(S, S_Q1 + 2, i, a2.y);
-    flags[i] = fl;
-    if (fl & 35u) atomicOr(any, 1u);  // identity or non-subgroup sigma: the batch falls back
 }
 
 // out[t] = in[2t] * in[2t+1] (in[2t] alone for an odd tail); SoA strides n_in / n_out
@@ -202,17 +258,24 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 
 extern "C" {
 
+// d_pts: n fold points (AoS affine: 48 words SigG2, 24 SigG1); d_dig: 16 x n digit bytes
 int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
                  const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
-                 uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, hipStream_t st) {
+                 uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, uint32_t* d_pts, int8_t* d_dig,
+                 hipStream_t st) {
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
-    if (mode == 0)
-        hipLaunchKernelGGL(k_prep_rlc_sigg2, g, b, 0, st, n, q, base_index, d_key, d_s1, d_s2, d_msgs, d_table,
-                           wbits, d_binf, d_prep, d_flags, d_any);
-    else
-        hipLaunchKernelGGL(k_prep_rlc_sigg1, g, b, 0, st, n, q, base_index, d_key, d_s1, d_s2, d_msgs, d_table,
-                           wbits, d_binf, d_prep, d_flags, d_any);
+    if (mode == 0) {
+        hipLaunchKernelGGL(k_rlc_check_sigg2, dim3(nblocks(2 * n, 256)), b, 0, st, n, base_index, d_key, d_s1, d_s2, d_prep, d_flags, d_any,
+                           d_pts, d_dig);
+        hipLaunchKernelGGL(k_rlc_msm_sigg2, g, b, 0, st, n, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
+                           d_prep, d_flags);
+    } else {
+        hipLaunchKernelGGL(k_rlc_check_sigg1, dim3(nblocks(2 * n, 256)), b, 0, st, n, base_index, d_key, d_s1, d_s2, d_prep, d_flags, d_any,
+                           d_pts, d_dig);
+        hipLaunchKernelGGL(k_rlc_msm_sigg1, g, b, 0, st, n, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
+                           d_prep, d_flags);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

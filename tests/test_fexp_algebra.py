@@ -135,3 +135,32 @@ def test_safegcd_inversion():
     for x in [0, 1, 2, P - 1, P - 2, (1 << 380) + 7] + [rnd.randrange(P) for _ in range(200)]:
         r = safegcd_inv(x)
         assert (x == 0 and r == 0) or r * x % P == 1
+
+
+# ---- RLC signed-digit coefficient (fr.h rlc_delta_signed) restated word by word
+R_ORDER = B.R
+
+
+def _delta_words(blk):
+    h = [(w >> 7) & 0x01010101 for w in blk]
+    m = [(h[0] << 8) & 0xFFFFFFFF, ((h[1] << 8) | (h[0] >> 24)) & 0xFFFFFFFF,
+         ((h[2] << 8) | (h[1] >> 24)) & 0xFFFFFFFF, ((h[3] << 8) | (h[2] >> 24)) & 0xFFFFFFFF, h[3] >> 24]
+    u = sum(blk[k] << (32 * k) for k in range(4))
+    mm = sum(m[k] << (32 * k) for k in range(5))
+    t = (u - mm) % (1 << 256)
+    if u < mm:
+        t = (t + R_ORDER) % (1 << 256)
+    return t
+
+
+def test_rlc_signed_digits():
+    """delta = sum int8(b_w) 256^w; the kernel's U - 256 H (+ r when negative) is delta mod r."""
+    rnd = random.Random(7)
+    cases = [[0, 0, 0, 0], [0xFFFFFFFF] * 4, [0x80808080] * 4, [0x7F7F7F7F] * 4]
+    cases += [[rnd.getrandbits(32) for _ in range(4)] for _ in range(500)]
+    for blk in cases:
+        b = b"".join(w.to_bytes(4, "little") for w in blk)
+        delta = sum((x - 256 if x >= 128 else x) << (8 * w) for w, x in enumerate(b))
+        S = ((1 << 128) - 1) // 255  # 2^128 consecutive values: [-128 S, 127 S]
+        assert -128 * S <= delta <= 127 * S
+        assert _delta_words(blk) == delta % R_ORDER
