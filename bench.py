@@ -430,6 +430,20 @@ def bench_rlc(args):
                          "reduce": round(phase_ms[2], 3)},
             "us_per_credential": round(elapsed / args.steps / n * 1e6, 4),
         }
+        counts = opcounts("rlc_sigg2_q16")
+        peak = peak_mad_per_s()
+        kt = {}
+        for k, ms in zip(("prep", "miller", "reduce"), phase_ms):
+            ach = counts[k] * MADS_PER_M * n / (ms * 1e-3) if ms > 0 else 0.0
+            kt[k] = {"ms": round(float(ms), 3), "achieved_Tmad_s": round(ach / 1e12, 3), "frac": round(ach / peak, 4)}
+        out["kernels"] = kt
+        out["roofline"] = {"bound": "valu-int", "kernel": "miller (fold + one-pair Miller + bucket pairs)",
+                           "achieved": kt["miller"]["achieved_Tmad_s"], "peak": round(peak / 1e12, 3),
+                           "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)", "frac": kt["miller"]["frac"],
+                           "traffic": None, "algorithmic_mads_per_credential": round(counts["miller"] * MADS_PER_M),
+                           "opcount_fixture": "tests/fixtures/opcount.json rlc_sigg2_q16",
+                           "note": "the batch's one final exponentiation (single element, latency-bound) and the "
+                                   "all-gather are outside the three phases but inside ms_per_step"}
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -209,21 +209,23 @@ __global__ __launch_bounds__(256) void k_rlc_msm_sigg1(size_t n, int q, uint64_t
     st_f2(S, S_Q1 + 2, i, a2.y);
 }
 
-// out[t] = in[2t] * in[2t+1] (in[2t] alone for an odd tail); SoA strides n_in / n_out
+// out[t] = in[2t] * in[2t+1] (in[2t] alone for an odd tail); SoA strides n_in / n_out.  One product
+// per lane PAIR (tower_pl.h): the tree's short levels are latency-bound, and the pair-lane Fp12
+// product has half the dependent multiplications of the one-lane one.
 __global__ __launch_bounds__(256) void k_f12_reduce(size_t n_in, const uint32_t* __restrict__ in,
                                                     uint32_t* __restrict__ out) {
-    const size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t t = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;
     const size_t n_out = (n_in + 1) / 2;
-    if (t >= n_out) return;
+    if (t >= n_out) return;  // pair-uniform
     const Soa I{const_cast<uint32_t*>(in), n_in}, O{out, n_out};
-    Fp12 a;
-    ld_f12(a, I, 2 * t);
+    pl::Fp12 a;
+    pl::ld_f12(a, I, 2 * t);
     if (2 * t + 1 < n_in) {
-        Fp12 b;
-        ld_f12(b, I, 2 * t + 1);
-        f12_mul(a, a, b);
+        pl::Fp12 b;
+        pl::ld_f12(b, I, 2 * t + 1);
+        pl::f12_mul(a, a, b);
     }
-    st_f12(O, t, a);
+    pl::st_f12(O, t, a);
 }
 
 // 145-word partial: the batch's Miller product (one element, Montgomery words in slot order) and
@@ -287,7 +289,7 @@ int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any
     uint32_t *src = d_a, *dst = d_b;
     while (n > 1) {
         const size_t n_out = (n + 1) / 2;
-        hipLaunchKernelGGL(k_f12_reduce, dim3(nblocks(n_out, 256)), dim3(256), 0, st, n, src, dst);
+        hipLaunchKernelGGL(k_f12_reduce, dim3(nblocks(2 * n_out, 256)), dim3(256), 0, st, n, src, dst);
         n = n_out;
         uint32_t* t = src;
         src = dst;
