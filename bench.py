@@ -437,7 +437,7 @@ def bench_rlc(args):
             ach = counts[k] * MADS_PER_M * n / (ms * 1e-3) if ms > 0 else 0.0
             kt[k] = {"ms": round(float(ms), 3), "achieved_Tmad_s": round(ach / 1e12, 3), "frac": round(ach / peak, 4)}
         out["kernels"] = kt
-        out["roofline"] = {"bound": "valu-int", "kernel": "miller (fold + one-pair Miller + bucket pairs)",
+        out["roofline"] = {"bound": "valu-int", "kernel": "miller (one-pair Miller + bucket pairs)",
                            "achieved": kt["miller"]["achieved_Tmad_s"], "peak": round(peak / 1e12, 3),
                            "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)", "frac": kt["miller"]["frac"],
                            "traffic": None, "algorithmic_mads_per_credential": round(counts["miller"] * MADS_PER_M),

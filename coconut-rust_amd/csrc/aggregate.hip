@@ -12,27 +12,15 @@
 //                    J' = X~ + J + sum_revealed Y~_i m_i, written in the verify kernels' Miller-loop
 //                    operand layout so k_miller_* / k_fexp finish the 2-pairing check.
 #include "codec.h"
+#include "curve_pl.h"
 #include "fixed.h"
 #include "fr.h"
 #include "pairing.h"
+#include "soa.h"
 
 using namespace cc;
 
 namespace {
-
-// ---------------------------------------------------------------- SoA helpers (local copies)
-struct Soa {
-    uint32_t* p;
-    size_t n;
-};
-DEV void st_fp(const Soa& s, size_t slot, size_t i, const Fp& x) {
-#pragma unroll
-    for (int k = 0; k < NL; k++) s.p[(slot * NL + k) * s.n + i] = x.v[k];
-}
-DEV void ld_fp(Fp& x, const Soa& s, size_t slot, size_t i) {
-#pragma unroll
-    for (int k = 0; k < NL; k++) x.v[k] = s.p[(slot * NL + k) * s.n + i];
-}
 
 template <class F>
 DEV bool decode_pt(Aff<F>& a, const uint8_t* p);
@@ -119,7 +107,7 @@ DEV void recode_w4(int8_t* d, const uint32_t k[8]) {
 // added across the lane group.  One lane per task would leave 10,000 tasks as 157 waves — a
 // latency-bound GPU (each lane doing ~146k serial Fp multiplications).
 template <class F, int L>
-__global__ __launch_bounds__(256) void k_msm_straus(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
+__global__ __launch_bounds__(256, 2) void k_msm_straus(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
                                                     size_t pt_stride, size_t pt_jstride, size_t pt_step,
                                                     const uint32_t* __restrict__ l, size_t l_div,
                                                     uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
@@ -224,6 +212,133 @@ __global__ __launch_bounds__(256) void k_msm_straus(size_t ntask, size_t t, cons
     }
 }
 
+// G2 bases on the pair-lane Fp2 (curve_pl.h): the same algorithm with ONE task lane per lane PAIR
+// (lane 2i + h holds half h of every Fp2 coordinate).  The one-lane G2 form of this kernel needs 512
+// VGPRs (1 wave/SIMD, spills) and runs a full doubling chain per lane; the pair form keeps a Jacobian
+// G2 point in 3 Fp a lane (2 waves/SIMD) and halves each lane's share of every Fp2 product.  L2 pairs
+// per task take the bases k = pair, pair + L2, ...; the scratch layout is straus_words<Fp2> with
+// each entry's two halves side by side ([entry][half][words]).
+template <int L2>
+__global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
+                                                           size_t pt_stride, size_t pt_jstride, size_t pt_step,
+                                                           const uint32_t* __restrict__ l, size_t l_div,
+                                                           uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
+    using F = pl::Fp2;
+    using T = FT<F>;
+    constexpr int L = 2 * L2;
+    constexpr int JW = 3 * NL, PW = NL;  // one lane's half of a Jacobian entry / of an Fp2
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t task = g / L;
+    const int pair = (int)((g % L) >> 1), h = (int)(g & 1);
+    if (task >= ntask) return;  // uniform over the lane group (L divides the block)
+    const size_t cred = task / l_div;
+    const uint8_t* base = pts + cred * pt_stride + (task % l_div) * pt_jstride;
+    const uint32_t* lk = l + cred * t * 8;
+    uint32_t* ent = scratch + task * straus_words<Fp2>(t);
+    uint32_t* pre = ent + t * 8 * (2 * JW);
+    int8_t* dig = reinterpret_cast<int8_t*>(pre + t * 8 * (2 * PW));
+    F acc_z;
+    T::one(acc_z);
+#pragma unroll 1
+    for (size_t k = pair; k < t; k += L2) {
+        cc::Aff<cc::Fp2> P1;
+        const bool ok = pl::pair_all(g2_decode(P1, base + k * pt_step));  // both lanes decode the point
+        recode_w4(dig + k * 65, lk + k * 8);                            // both write the same digits
+        cc::Aff<F> P;
+        P.x.c = h ? P1.x.b : P1.x.a;
+        P.y.c = h ? P1.y.b : P1.y.a;
+        cc::Jac<F> J;
+        if (ok) jac_from_aff(J, P);
+        else jac_set_inf(J);
+#pragma unroll 1
+        for (int d = 0; d < 8; d++) {
+            if (d == 1) jac_dbl(J, J);
+            else if (d > 1 && ok) jac_add_aff(J, J, P);
+            const size_t e = k * 8 + d;
+            uint32_t* w = ent + (e * 2 + h) * JW;
+            const uint32_t* jw = reinterpret_cast<const uint32_t*>(&J);
+            for (int c = 0; c < JW; c++) w[c] = jw[c];
+            for (int c = 0; c < PW; c++) pre[(e * 2 + h) * PW + c] = acc_z.c.v[c];
+            if (!jac_is_inf(J)) T::mul(acc_z, acc_z, J.z);
+        }
+    }
+    F inv;
+    T::inv(inv, acc_z);
+    if (t > (size_t)pair) {
+        const long long kmax = (long long)(((t - 1 - pair) / L2) * L2 + pair);
+#pragma unroll 1
+        for (long long kk = kmax; kk >= pair; kk -= L2) {
+            for (int d = 7; d >= 0; d--) {
+                const size_t e = (size_t)kk * 8 + d;
+                cc::Jac<F> J;
+                uint32_t* w = ent + (e * 2 + h) * JW;
+                uint32_t* jw = reinterpret_cast<uint32_t*>(&J);
+                for (int c = 0; c < JW; c++) jw[c] = w[c];
+                const bool inf = jac_is_inf(J);
+                if (!inf) {
+                    F pz, zi, zi2;
+                    for (int c = 0; c < PW; c++) pz.c.v[c] = pre[(e * 2 + h) * PW + c];
+                    T::mul(zi, inv, pz);
+                    T::mul(inv, inv, J.z);
+                    T::sqr(zi2, zi);
+                    T::mul(J.x, J.x, zi2);
+                    T::mul(zi2, zi2, zi);
+                    T::mul(J.y, J.y, zi2);
+                }
+                for (int c = 0; c < 2 * PW; c++) w[c] = jw[c];  // this half's affine x, y
+                w[2 * PW] = inf ? 1u : 0u;
+            }
+        }
+    }
+    cc::Jac<F> acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (int win = 64; win >= 0; win--) {
+        if (win != 64 && !jac_is_inf(acc))
+            for (int z = 0; z < 4; z++) jac_dbl(acc, acc);
+#pragma unroll 1
+        for (size_t k = pair; k < t; k += L2) {
+            const int d = dig[k * 65 + win];
+            if (!d) continue;
+            const uint32_t* w = ent + ((k * 8 + (d < 0 ? -d : d) - 1) * 2 + h) * JW;
+            if (w[2 * PW]) continue;  // identity multiple (pair-uniform: both halves carry the flag)
+            cc::Aff<F> e;
+            for (int c = 0; c < PW; c++) {
+                e.x.c.v[c] = w[c];
+                e.y.c.v[c] = w[PW + c];
+            }
+            if (d < 0) T::neg(e.y, e.y);
+            jac_add_aff(acc, acc, e);
+        }
+    }
+    // butterfly over the L2 pairs of the task (lane distances 2, 4, ..: halves stay with halves)
+    constexpr int JWF = sizeof(cc::Jac<F>) / 4;
+#pragma unroll 1
+    for (int m = L >> 1; m >= 2; m >>= 1) {
+        cc::Jac<F> o;
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(&acc);
+        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+        for (int c = 0; c < JWF; c++) ow[c] = (uint32_t)__shfl_xor((int)a[c], m);
+        if (threadIdx.x & m) {
+            cc::Jac<F> tmp = acc;
+            acc = o;
+            o = tmp;
+        }
+        jac_add(acc, acc, o);
+    }
+    if (pair == 0) {
+        cc::Aff<F> r;
+        const bool fin = jac_to_aff(r, acc);
+        const Fp xs = pl::swp(r.x.c), ys = pl::swp(r.y.c);
+        cc::Aff<cc::Fp2> o;
+        o.x.a = h ? xs : r.x.c;
+        o.x.b = h ? r.x.c : xs;
+        o.y.a = h ? ys : r.y.c;
+        o.y.b = h ? r.y.c : ys;
+        if (!h) g2_encode(out + task * 192, o, fin);
+    }
+}
+
 // ================================================================ issuer-table Verkey::aggregate
 // Verkey::aggregate (signature.rs:483-526) over a resident issuer table: the bases X~_k, Y~_k,j of
 // the n_iss issuers are FIXED, so cc_set_issuers gives each one an 8-bit window table (32 x 255
@@ -269,9 +384,8 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
 }
 
 // ================================================================ PoK verify prep
-// Prep layout and flag bits as kernels.hip (Q1 0..3 | Q2 4..7 | P1 8..10 | P2 11..12),
+// Prep layout (soa.h: Q1 0..3 | Q2 4..7 | P1 8..10 | P2 11..12) and flag bits as kernels.hip,
 // plus flag bit3 = Schnorr check failed.
-enum { S_Q1 = 0, S_Q2 = 4, S_P1 = 8, S_P2 = 11 };
 
 template <class FS_, class FO>  // FS_: SignatureGroup field, FO: OtherGroup field
 __global__ __launch_bounds__(256) void k_prep_pok(size_t n, int q, int r, const uint8_t* __restrict__ s1b,
@@ -425,8 +539,8 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
         hipLaunchKernelGGL((k_msm_straus<Fp, L>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l,
                            l_div, d_scratch, d_out);
     else
-        hipLaunchKernelGGL((k_msm_straus<Fp2, L>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l,
-                           l_div, d_scratch, d_out);
+        hipLaunchKernelGGL((k_msm_straus_g2pl<L / 2>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step,
+                           d_l, l_div, d_scratch, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

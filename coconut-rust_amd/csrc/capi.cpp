@@ -41,9 +41,11 @@ int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const ui
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
 int cck_miller_pl_g2(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
-                     const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, hipStream_t st);
+                     const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
+                     hipStream_t st);
 int cck_miller_pl_g1(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
-                     const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, hipStream_t st);
+                     const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
+                     hipStream_t st);
 size_t cck_fold_words(int mode, size_t n);
 int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok,
              int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
@@ -61,10 +63,10 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
                      uint8_t* d_outX, uint8_t* d_outY, hipStream_t st);
 int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
                   uint8_t* d_out, hipStream_t st);
-int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
-                 const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
-                 uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, uint32_t* d_pts, int8_t* d_dig,
-                 hipStream_t st);
+int cck_prep_rlc(int mode, int part, size_t n, int q, uint64_t base_index, const uint32_t* d_key,
+                 const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits,
+                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, uint32_t* d_pts,
+                 int8_t* d_dig, hipStream_t st);
 int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any, uint32_t* d_partial,
                    hipStream_t st);
 int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t* d_flag, hipStream_t st);
@@ -194,16 +196,17 @@ struct StreamOrder {
 // run one credential per lane pair (tower_pl.h).  Miller values go to SoA elements [foff, foff + n)
 // of stride fstride (default: n, 0).
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-                      uint32_t* d_f, hipStream_t st, int np = 2, size_t fstride = 0, size_t foff = 0) {
+                      uint32_t* d_f, hipStream_t st, int np = 2, size_t fstride = 0, size_t foff = 0,
+                      uint32_t* d_qcheck = nullptr) {
     if (!fstride) fstride = n;
-    return mode == 0 ? cck_miller_pl_g2(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, st)
-                     : cck_miller_pl_g1(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, st);
+    return mode == 0 ? cck_miller_pl_g2(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, d_qcheck, st)
+                     : cck_miller_pl_g1(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, nullptr, st);
 }
 // the RLC fold's pseudo-credentials: one (Q, P) pair per lane pair, Q affine G2 and P in evaluation
 // form, both per lane (either group mode: the SigG2 instantiation reads exactly that)
 static int cck_miller_pairs(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
                             size_t fstride, size_t foff, hipStream_t st) {
-    return cck_miller_pl_g2(0, 1, n, d_prep, d_flags, nullptr, d_f, fstride, foff, st);
+    return cck_miller_pl_g2(0, 1, n, d_prep, d_flags, nullptr, d_f, fstride, foff, nullptr, st);
 }
 static int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                     uint8_t* d_gt, hipStream_t st) {
@@ -543,22 +546,24 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     HIPCK(hipMemcpyAsync(c->rlc_key.p, c->rlc_key_host, 32, hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
-    KCK(cck_prep_rlc(c->mode, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
-                     c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
-                     c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), c->rlc_pts.as<uint32_t>(),
-                     c->rlc_dig.as<int8_t>(), st));
+    auto prep_part = [&](int part) {
+        return cck_prep_rlc(c->mode, part, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
+                            c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
+                            c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), c->rlc_pts.as<uint32_t>(),
+                            c->rlc_dig.as<int8_t>(), st);
+    };
+    KCK(prep_part(0));  // decode, subgroup checks, the fold's inputs
     if (!c->vk_subgroup) {
         // a verkey / g~ point outside the subgroup: the linear-combination argument does not hold,
         // so the batch is never accepted here and the caller verifies per credential (exact)
         static const uint32_t one = 1;
         HIPCK(hipMemcpyAsync(c->rlc_any.p, &one, 4, hipMemcpyHostToDevice, st));
     }
-    if (c->timing) (void)hipEventRecord(c->ev[1], st);
-    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
-    // the second pairs become 2,048 bucket pairs (fold.hip); their Miller launch (64 waves, latency
-    // bound alone) runs on the high-priority side stream concurrently with pair 0 of every credential
-    // on st; both write disjoint ranges of fbuf (stride N).  The fold's own short kernels run first,
-    // alone (behind a full Miller launch each would wait milliseconds for a free slot).
+    // The second pairs become 2,048 bucket pairs (fold.hip).  The fold's short kernels run alone
+    // (behind a full launch each would wait milliseconds for a free slot); the buckets' Miller launch
+    // (64 waves, latency bound alone) then runs on the high-priority side stream under the delta MSM
+    // and pair 0 of every credential on st.  Both Miller launches write disjoint ranges of fbuf
+    // (stride N).
     KCK(cck_fold(c->mode, n, c->rlc_dig.as<int8_t>(), c->rlc_pts.as<uint32_t>(), c->rlc_work.as<uint32_t>(),
                  c->rlc_fixed_ok ? 1 : 0, (int)q, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(),
                  c->rlc_prep2.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_flags2.as<uint32_t>(), st));
@@ -570,8 +575,12 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     }
     KCK(cck_miller_pairs(NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(), c->fbuf.as<uint32_t>(), N, n,
                          side));
+    KCK(prep_part(1));  // delta X~ + sum (delta m_j) Y~_j
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
+    // SigG2: sigma_1's subgroup test comes from this loop's T (a failure raises rlc_any: fallback)
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st, 1, N,
-                   0));
+                   0, c->mode == 0 ? c->rlc_any.as<uint32_t>() : nullptr));
     if (side != st) {
         HIPCK(hipEventRecord(c->ev_join, side));
         HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));

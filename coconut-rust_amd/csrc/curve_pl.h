@@ -7,6 +7,7 @@
 // than the 256 VGPRs of 2 waves/SIMD: the RLC batch mode's subgroup checks (rlc.hip).  As with
 // every pair-lane code path, control flow is pair-uniform (the predicates below agree on both lanes).
 #pragma once
+#include "fixed.h"
 #include "subgroup.h"
 #include "tower_pl.h"
 
@@ -32,8 +33,8 @@ struct FT<pl::Fp2> {
 
 namespace pl {
 
-// psi(Q) == [x] Q (subgroup.h g2_in_subgroup, same constants) for Q held as a lane-pair value
-DEV bool g2_in_subgroup(const Aff<Fp2>& q) {
+// psi(Q) for Q held as a lane-pair value (subgroup.h g2_in_subgroup's constants)
+DEV void g2_psi(Aff<Fp2>& r, const Aff<Fp2>& q) {
     constexpr uint32_t CXB[NL] = {0x954030c4u, 0x1ed59d62u, 0x026053a5u, 0xc81fdd18u, 0xb49e2e0fu, 0xcb785f67u,
                                   0x6a65e5c3u, 0x689a6956u, 0x21724249u, 0x14cec802u, 0x7aaa6c42u, 0x00ba917au};
     constexpr uint32_t CYA[NL] = {0x699d9feeu, 0xfb9f5730u, 0x791f82c1u, 0x573fc3f8u, 0xc260bc18u, 0x774659b7u,
@@ -41,21 +42,65 @@ DEV bool g2_in_subgroup(const Aff<Fp2>& q) {
     constexpr uint32_t CYB[NL] = {0x96620abdu, 0xbe5fa8cfu, 0x38347d3du, 0xc76c3c06u, 0x34503a0bu, 0xefea78e9u,
                                   0x8d8f9a7bu, 0x4ddb2a04u, 0x50dec50eu, 0x03a250e8u, 0xc4c0f858u, 0x00e14367u};
     const bool im = half_id() != 0;
-    Jac<Fp2> a, t;
-    jac_from_aff(a, q);
-    jac_mul_xabs(t, a);  // [|x|] Q = -[x] Q
-    Aff<Fp2> ps;
     Fp2 c, u;
 #pragma unroll
     for (int j = 0; j < NL; j++) c.c.v[j] = im ? CXB[j] : 0u;  // c_x = (0, CXB)
     f2_conj(u, q.x);
-    f2_mul(ps.x, u, c);
+    f2_mul(r.x, u, c);
 #pragma unroll
     for (int j = 0; j < NL; j++) c.c.v[j] = im ? CYB[j] : CYA[j];
     f2_conj(u, q.y);
-    f2_mul(ps.y, u, c);
+    f2_mul(r.y, u, c);
+}
+
+// psi(Q) == [x] Q (subgroup.h g2_in_subgroup, same constants) for Q held as a lane-pair value
+DEV bool g2_in_subgroup(const Aff<Fp2>& q) {
+    Jac<Fp2> a, t;
+    jac_from_aff(a, q);
+    jac_mul_xabs(t, a);  // [|x|] Q = -[x] Q
+    Aff<Fp2> ps;
+    g2_psi(ps, q);
     jac_add_aff(t, t, ps);  // [|x|] Q + psi(Q) == O  <=>  psi(Q) == [x] Q
     return jac_is_inf(t);
+}
+
+// The Miller loop's twist point ends as T = [|x|] Q (homogeneous projective: x = X/Z, y = Y/Z; the
+// loop walks |x|'s addition chain), so Q is in G2 iff psi(Q) == [x] Q = -T: X = psi_x Z, Y = -psi_y Z,
+// Z != 0 (eprint 2021/1130 §4, the test of g2_in_subgroup at the cost of two Fp2 multiplications).
+DEV bool miller_t_in_subgroup(const G2Proj& T, const Aff<Fp2>& q) {
+    Aff<Fp2> ps;
+    g2_psi(ps, q);
+    Fp2 a, b;
+    f2_mul(a, ps.x, T.z);
+    f2_mul(b, ps.y, T.z);
+    f2_neg(b, b);
+    return !f2_is_zero(T.z) && f2_eq(a, T.x) && f2_eq(b, T.y);
+}
+
+// fixed.h ft_add on the pair-lane Fp2: acc += (k over windows [w0, w1)) * B_j from a G2 window table
+// (AoS entries x.a | x.b | y.a | y.b, 12 words each): each lane loads its own halves.
+DEV void ft_add_g2(Jac<Fp2>& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j, int w0,
+                   int w1) {
+    constexpr int EW = sizeof(cc::Aff<cc::Fp2>) / 4;
+    const int h = (int)half_id();
+    const size_t went = ft_went(wbits);
+    const uint32_t* tj = table + (size_t)j * ft_base_words<cc::Fp2>(wbits);
+#pragma unroll 1
+    for (int w = w0; w < w1; w++) {
+        const uint32_t d = ft_digit(k, w, wbits);  // pair-uniform: both lanes hold the same scalar
+        if (!d) continue;
+        const uint32_t* e = tj + ((size_t)w * went + d - 1) * EW;
+        Aff<Fp2> a;
+        uint32_t o = 0;
+#pragma unroll
+        for (int c = 0; c < NL; c++) {
+            a.x.c.v[c] = e[NL * h + c];
+            a.y.c.v[c] = e[2 * NL + NL * h + c];
+            o |= a.x.c.v[c] | a.y.c.v[c];
+        }
+        if (pair_all(o == 0)) continue;  // (0, 0): an identity entry
+        jac_add_aff(acc, acc, a);
+    }
 }
 
 // the lane-pair form of a one-lane Fp2 value held by lane `src` of the pair (both lanes call it)

@@ -41,11 +41,12 @@ static __device__ __noinline__ void fx_inv(Soa src, Soa dst, size_t i) {
 }
 
 // dst <- src^3 (cyclotomic)
+template <bool W>
 static __device__ __noinline__ void fx_cube(Soa src, Soa dst, size_t i) {
     Fp12 f, r;
     ld_f12(f, src, i);
-    f12_cyc_sqr(r, f);
-    f12_mul(r, r, f);
+    cs12<W>(r, f);
+    m12<W>(r, r, f);
     st_f12(dst, i, r);
 }
 
@@ -53,16 +54,17 @@ static __device__ __noinline__ void fx_cube(Soa src, Soa dst, size_t i) {
 // each of the 5 multiplications instead of being held in registers across the 63 squarings.
 // Fallback of fx_pow_x below for the (never honestly reached) case of a zero decompression
 // denominator.
+template <bool W>
 static __device__ __noinline__ void fx_pow_x_gs(Soa src, Soa dst, size_t i) {
     Fp12 acc;
     ld_f12(acc, src, i);
     for (int b = 62; b >= 0; b--) {
-        f12_cyc_sqr(acc, acc);
+        cs12<W>(acc, acc);
         if ((X_ABS >> b) & 1ull) {
             asm volatile("" ::: "memory");  // keep the reload inside the loop
             Fp12 y;
             ld_f12(y, src, i);
-            f12_mul(acc, acc, y);
+            m12<W>(acc, acc, y);
         }
     }
     f12_conj(acc, acc);
@@ -158,6 +160,179 @@ DEV void cyc4_expand(Fp12& r, const Cyc4& x, const Fp2& n0, const Fp2& n1, const
     r.c.b = x.c1;
 }
 
+// ---------------------------------------------------------------- wide forms (k_fexp1: one element)
+// A single final exponentiation (the RLC batch mode's one per batch) runs on ONE wave: the 32 lane
+// pairs hold the same element, and the independent Fp2 products of a step are spread over them —
+// the 6 squarings of cyc4_sqr, the 18 products of f12_mul, the 6 of f12_cyc_sqr — as ONE call
+// (same instructions, different data), the results gathered with ds_bpermute shuffles and the
+// remaining additions done redundantly by every pair.  A step's latency then holds one product
+// instead of 6 or 18.
+DEV int pair_idx() { return (int)(threadIdx.x >> 1); }
+DEV Fp2 bcast_f2(const Fp2& v, int src_pair) {
+    const int lane = 2 * src_pair + (int)half_id();
+    Fp2 r;
+#pragma unroll
+    for (int k = 0; k < NL; k++) r.c.v[k] = (uint32_t)__shfl((int)v.c.v[k], lane);
+    return r;
+}
+DEV Fp2 f2_pick(int j, const Fp2* opts, int nopt) {
+    Fp2 r = opts[0];
+    for (int k = 1; k < nopt; k++) r.c = fp_sel(j == k, opts[k].c, r.c);
+    return r;
+}
+
+DEV void cyc4_sqr_wide(Cyc4& x) {
+    const int j = pair_idx() % 6;
+    Fp2 opt[6];
+    opt[0] = x.b0;
+    opt[1] = x.b1;
+    f2_add_lz(opt[2], x.b0, x.b1);
+    opt[3] = x.c0;
+    opt[4] = x.c1;
+    f2_add_lz(opt[5], x.c0, x.c1);
+    Fp2 in = f2_pick(j, opt, 6), sq;
+    f2_sqr(sq, in);
+    Fp2 s0 = bcast_f2(sq, 0), s1 = bcast_f2(sq, 1), Xb = bcast_f2(sq, 2);
+    Fp2 Tb, Tc, Xc;
+    f2_sub(Xb, Xb, s0);
+    f2_sub(Xb, Xb, s1);  // 2 b0 b1
+    f2_mul_xi(s1, s1);
+    f2_add(Tb, s0, s1);  // b0^2 + xi b1^2
+    s0 = bcast_f2(sq, 3);
+    s1 = bcast_f2(sq, 4);
+    Xc = bcast_f2(sq, 5);
+    f2_sub(Xc, Xc, s0);
+    f2_sub(Xc, Xc, s1);
+    f2_mul_xi(Xc, Xc);   // 2 xi c0 c1
+    f2_mul_xi(s1, s1);
+    f2_add(Tc, s0, s1);  // c0^2 + xi c1^2
+    f2_3u_p2v(x.b0, Xc, x.b0);
+    f2_3u_m2v(x.b1, Tc, x.b1);
+    f2_3u_m2v(x.c0, Tb, x.c0);
+    f2_3u_p2v(x.c1, Xb, x.c1);
+}
+
+// f4_mul's three products of operand set m, spread: pair 3m + p computes product p
+DEV void f4_from_products(Fp4& r, const Fp2& p0, const Fp2& p1, const Fp2& p2) {
+    Fp2 t;
+    f2_mul_xi(t, p1);
+    f2_add(r.a, p0, t);
+    f2_sub(t, p2, p0);
+    f2_sub(r.b, t, p1);
+}
+
+// = f12_mul (tower.inc): the six f4 products (t0, t1, t2 and the three cross terms) as 18 Fp2
+// products on pairs 0..17
+DEV void f12_mul_wide(Fp12& r, const Fp12& x, const Fp12& y) {
+    const int j = pair_idx() % 18;
+    const int m = j / 3, p = j % 3;
+    Fp4 U, V;
+    {
+        Fp4 u[6], v[6];
+        u[0] = x.a; u[1] = x.b; u[2] = x.c;
+        f4_add(u[3], x.b, x.c);
+        f4_add(u[4], x.a, x.b);
+        f4_add(u[5], x.a, x.c);
+        v[0] = y.a; v[1] = y.b; v[2] = y.c;
+        f4_add(v[3], y.b, y.c);
+        f4_add(v[4], y.a, y.b);
+        f4_add(v[5], y.a, y.c);
+        Fp2 ua[6], ub[6], va[6], vb[6];
+        for (int k = 0; k < 6; k++) {
+            ua[k] = u[k].a; ub[k] = u[k].b; va[k] = v[k].a; vb[k] = v[k].b;
+        }
+        U.a = f2_pick(m, ua, 6);
+        U.b = f2_pick(m, ub, 6);
+        V.a = f2_pick(m, va, 6);
+        V.b = f2_pick(m, vb, 6);
+    }
+    Fp2 o1 = U.a, o2 = V.a, s1, s2, prod;
+    f2_add_lz(s1, U.a, U.b);
+    f2_add_lz(s2, V.a, V.b);
+    o1.c = fp_sel(p == 1, U.b.c, o1.c);
+    o2.c = fp_sel(p == 1, V.b.c, o2.c);
+    o1.c = fp_sel(p == 2, s1.c, o1.c);
+    o2.c = fp_sel(p == 2, s2.c, o2.c);
+    f2_mul(prod, o1, o2);
+    Fp4 t0, t1, t2, s, w, ra, rb, rc;
+    f4_from_products(t0, bcast_f2(prod, 0), bcast_f2(prod, 1), bcast_f2(prod, 2));
+    f4_from_products(t1, bcast_f2(prod, 3), bcast_f2(prod, 4), bcast_f2(prod, 5));
+    f4_from_products(t2, bcast_f2(prod, 6), bcast_f2(prod, 7), bcast_f2(prod, 8));
+    f4_from_products(s, bcast_f2(prod, 9), bcast_f2(prod, 10), bcast_f2(prod, 11));  // (b + c)(b' + c')
+    f4_sub(s, s, t1);
+    f4_sub(s, s, t2);
+    f4_mul_s(s, s);
+    f4_add(ra, s, t0);
+    f4_from_products(s, bcast_f2(prod, 12), bcast_f2(prod, 13), bcast_f2(prod, 14));  // (a + b)(a' + b')
+    f4_sub(s, s, t0);
+    f4_sub(s, s, t1);
+    f4_mul_s(w, t2);
+    f4_add(rb, s, w);
+    f4_from_products(s, bcast_f2(prod, 15), bcast_f2(prod, 16), bcast_f2(prod, 17));  // (a + c)(a' + c')
+    f4_sub(s, s, t0);
+    f4_sub(s, s, t2);
+    f4_add(rc, s, t1);
+    r.a = ra;
+    r.b = rb;
+    r.c = rc;
+}
+
+// = f12_cyc_sqr (Granger-Scott): f4_sqr of a, b, c as 6 products on pairs 0..5 (pair 2m: ab,
+// pair 2m + 1: (a + b)(a + xi b) of operand m)
+DEV void f12_cyc_sqr_wide(Fp12& r, const Fp12& x) {
+    const int j = pair_idx() % 6;
+    const int m = j >> 1;
+    Fp2 oa[3] = {x.a.a, x.b.a, x.c.a}, ob[3] = {x.a.b, x.b.b, x.c.b};
+    const Fp2 a = f2_pick(m, oa, 3), b = f2_pick(m, ob, 3);
+    Fp2 o1 = a, o2 = b, s0, s1, prod;
+    f2_add_lz(s0, a, b);
+    f2_mul_xi(s1, b);
+    f2_add_lz(s1, s1, a);
+    o1.c = fp_sel(j & 1, s0.c, o1.c);
+    o2.c = fp_sel(j & 1, s1.c, o2.c);
+    f2_mul(prod, o1, o2);
+    Fp4 sq[3];
+    for (int k = 0; k < 3; k++) {  // f4_sqr from its two products
+        const Fp2 ab = bcast_f2(prod, 2 * k);
+        Fp2 t = bcast_f2(prod, 2 * k + 1), u;
+        f2_sub(t, t, ab);
+        f2_mul_xi(u, ab);
+        f2_sub(sq[k].a, t, u);
+        f2_dbl(sq[k].b, ab);
+    }
+    // a' = 3A - 2 conj(a), b' = 3 s C + 2 conj(b), c' = 3 B - 2 conj(c)  (A = a^2, B = b^2, C = c^2)
+    Fp4 t;
+    f4_sub_conj(t, sq[0], x.a);
+    f4_dbl(t, t);
+    f4_add(r.a, t, sq[0]);
+    Fp4 Bs;
+    f4_mul_s(Bs, sq[2]);
+    f4_add_conj(t, Bs, x.b);
+    f4_dbl(t, t);
+    Fp4 rb;
+    f4_add(rb, t, Bs);
+    f4_sub_conj(t, sq[1], x.c);
+    f4_dbl(t, t);
+    f4_add(r.c, t, sq[1]);
+    r.b = rb;
+}
+
+template <bool W>
+DEV void m12(Fp12& r, const Fp12& x, const Fp12& y) {
+    if (W) f12_mul_wide(r, x, y);
+    else f12_mul(r, x, y);
+}
+template <bool W>
+DEV void cs12(Fp12& r, const Fp12& x) {
+    if (W) f12_cyc_sqr_wide(r, x);
+    else f12_cyc_sqr(r, x);
+}
+template <bool W>
+DEV void c4s(Cyc4& x) {
+    if (W) cyc4_sqr_wide(x);
+    else cyc4_sqr(x);
+}
+
 // snapshot slots (Fp2 pairs) in the K region: per snapshot b0 b1 c0 c1 n0 n1
 DEV void st_cyc4(const Soa& K, int base, size_t i, const Cyc4& x) {
     st_f2(K, base + 0, i, x.b0);
@@ -178,6 +353,7 @@ DEV void ld_cyc4(Cyc4& x, const Soa& K, int base, size_t i) {
 // Granger-Scott squarings of g^(2^57) (cheaper than three more decompressions).  Five Fp12
 // multiplications as before.  A zero denominator (b = c = 0 pattern; never reached by honest inputs,
 // e.g. src = 1) sends the lane pair to the Granger-Scott ladder.
+template <bool W>
 static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i) {
     Cyc4 c;
     ld_f2(c.b0, src, 4, i);
@@ -185,7 +361,7 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i) 
     ld_f2(c.c0, src, 8, i);
     ld_f2(c.c1, src, 10, i);
     for (int k = 1; k <= 57; k++) {
-        cyc4_sqr(c);
+        c4s<W>(c);
         if (k == 16) st_cyc4(K, 0, i, c);
         if (k == 48) st_cyc4(K, 12, i, c);
     }
@@ -205,7 +381,7 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i) 
     f2_mul(p1, d16, d48);
     f2_mul(p2, p1, d57);
     if (f2_is_zero(p2)) {  // pair-uniform
-        fx_pow_x_gs(src, dst, i);
+        fx_pow_x_gs<W>(src, dst, i);
         return;
     }
     f2_inv(inv, p2);
@@ -230,59 +406,62 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i) 
         ld_f2(n1, K, 22, i);
         cyc4_expand(t, s, n0, n1, ik);    // g^(2^48)
     }
-    f12_mul(acc, acc, t);
-    f12_mul(acc, acc, y);
-    for (int k = 0; k < 3; k++) f12_cyc_sqr(y, y);
-    f12_mul(acc, acc, y);  // 2^60
-    for (int k = 0; k < 2; k++) f12_cyc_sqr(y, y);
-    f12_mul(acc, acc, y);  // 2^62
-    f12_cyc_sqr(y, y);
-    f12_mul(acc, acc, y);  // 2^63
+    m12<W>(acc, acc, t);
+    m12<W>(acc, acc, y);
+    for (int k = 0; k < 3; k++) cs12<W>(y, y);
+    m12<W>(acc, acc, y);  // 2^60
+    for (int k = 0; k < 2; k++) cs12<W>(y, y);
+    m12<W>(acc, acc, y);  // 2^62
+    cs12<W>(y, y);
+    m12<W>(acc, acc, y);  // 2^63
     f12_conj(acc, acc);
     st_f12(dst, i, acc);
 }
 
 // dst <- op_a(a) * op_b(b)
+template <bool W>
 static __device__ __noinline__ void fx_mul(Soa a, int opa, Soa b, int opb, Soa dst, size_t i) {
     Fp12 x, y;
     ld_f12(x, a, i);
     fx_apply(x, opa);
     ld_f12(y, b, i);
     fx_apply(y, opb);
-    f12_mul(x, x, y);
+    m12<W>(x, x, y);
     st_f12(dst, i, x);
 }
 
-// fbuf: Miller output f (12 slots); scratch: 4 x 12 slots (T, A, S, R) + 24 slots K (fx_pow_x snapshots)
-__global__ __launch_bounds__(256, 2) void k_fexp(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
-                                              const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
-                                              uint8_t* __restrict__ gt_out) {
-    const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
-    if (i >= n) return;  // pair-uniform
+// the chain (k_fexp: element i of n; k_fexp1: the one element, wide steps)
+template <bool W>
+DEV void fexp_chain(size_t n, size_t i, uint32_t* fbuf, uint32_t* scratch) {
     const Soa F{fbuf, n};
     const Soa T{scratch, n}, A{scratch + (size_t)12 * NL * n, n}, S{scratch + (size_t)24 * NL * n, n},
         R{scratch + (size_t)36 * NL * n, n}, K{scratch + (size_t)48 * NL * n, n};
     fx_inv(F, T, i);
-    fx_mul(F, OP_CONJ, T, OP_ID, F, i);  // f^(p^6 - 1)
-    fx_mul(F, OP_FROB2, F, OP_ID, F, i); // ^(p^2 + 1)
-    fx_cube(F, R, i);                    // res = f^3
-    fx_pow_x(F, T, K, i);
-    fx_mul(T, OP_ID, F, OP_CONJ, T, i);  // t = f^(x-1)
-    fx_pow_x(T, A, K, i);
-    fx_mul(A, OP_ID, T, OP_CONJ, A, i);  // a = f^((x-1)^2)
-    fx_mul(A, OP_FROB2, A, OP_CONJ, S, i);
-    fx_mul(S, OP_FROB, R, OP_ID, R, i);  // res *= (a^(p^2) a^-1)^p
-    fx_pow_x(A, T, K, i);                   // b = a^x
-    fx_mul(T, OP_FROB2, T, OP_CONJ, S, i);
-    fx_mul(S, OP_ID, R, OP_ID, R, i);    // res *= b^(p^2) b^-1
-    fx_pow_x(T, A, K, i);                   // c = b^x
-    fx_mul(A, OP_FROB, R, OP_ID, R, i);  // res *= c^p
-    fx_pow_x(A, T, K, i);                   // d = c^x
-    fx_mul(T, OP_ID, R, OP_ID, R, i);    // res *= d
+    fx_mul<W>(F, OP_CONJ, T, OP_ID, F, i);   // f^(p^6 - 1)
+    fx_mul<W>(F, OP_FROB2, F, OP_ID, F, i);  // ^(p^2 + 1)
+    fx_cube<W>(F, R, i);                     // res = f^3
+    fx_pow_x<W>(F, T, K, i);
+    fx_mul<W>(T, OP_ID, F, OP_CONJ, T, i);   // t = f^(x-1)
+    fx_pow_x<W>(T, A, K, i);
+    fx_mul<W>(A, OP_ID, T, OP_CONJ, A, i);   // a = f^((x-1)^2)
+    fx_mul<W>(A, OP_FROB2, A, OP_CONJ, S, i);
+    fx_mul<W>(S, OP_FROB, R, OP_ID, R, i);   // res *= (a^(p^2) a^-1)^p
+    fx_pow_x<W>(A, T, K, i);                 // b = a^x
+    fx_mul<W>(T, OP_FROB2, T, OP_CONJ, S, i);
+    fx_mul<W>(S, OP_ID, R, OP_ID, R, i);     // res *= b^(p^2) b^-1
+    fx_pow_x<W>(T, A, K, i);                 // c = b^x
+    fx_mul<W>(A, OP_FROB, R, OP_ID, R, i);   // res *= c^p
+    fx_pow_x<W>(A, T, K, i);                 // d = c^x
+    fx_mul<W>(T, OP_ID, R, OP_ID, R, i);     // res *= d
+}
+
+DEV void fexp_out(size_t n, size_t i, const uint32_t* scratch, const uint32_t* flags, uint8_t* verdicts,
+                  uint8_t* gt_out, bool writer) {
     Fp12 res;
-    ld_f12(res, R, i);
+    ld_f12(res, Soa{const_cast<uint32_t*>(scratch) + (size_t)36 * NL * n, n}, i);
     const uint32_t fl = flags ? flags[i] : 0u;
     const bool ok = f12_is_one(res) && (fl & 11u) == 0;  // sigma_1/sigma_2 = O or PoK Schnorr failure
+    if (!writer) return;
     if (!half_id()) verdicts[i] = ok ? 1 : 0;
     if (gt_out) {  // each lane writes its halves: Fp slots 2k + h of the AMCL FP12 order
         const Fp2* v = reinterpret_cast<const Fp2*>(&res);
@@ -295,6 +474,27 @@ __global__ __launch_bounds__(256, 2) void k_fexp(size_t n, uint32_t* __restrict_
     }
 }
 
+// fbuf: Miller output f (12 slots); scratch: 4 x 12 slots (T, A, S, R) + 24 slots K (fx_pow_x snapshots)
+__global__ __launch_bounds__(256, 2) void k_fexp(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
+                                              const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
+                                              uint8_t* __restrict__ gt_out) {
+    const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
+    if (i >= n) return;  // pair-uniform
+    fexp_chain<false>(n, i, fbuf, scratch);
+    fexp_out(n, i, scratch, flags, verdicts, gt_out, true);
+}
+
+// one element on one wave (64 lanes, all pairs holding the same values; pair 0 writes the outputs).
+// Bounds (64, 2) = k_fexp's register budget of 2 waves/SIMD (HIP's second bound is waves per SIMD):
+// the two kernels share out-of-line step functions, and a looser bound here would let those grow
+// past k_fexp's 256 VGPRs.
+__global__ __launch_bounds__(64, 2) void k_fexp1(uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
+                                              const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
+                                              uint8_t* __restrict__ gt_out) {
+    fexp_chain<true>(1, 0, fbuf, scratch);
+    fexp_out(1, 0, scratch, flags, verdicts, gt_out, threadIdx.x < 2);
+}
+
 }  // namespace pl
 }  // namespace cc
 
@@ -303,7 +503,10 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 extern "C" int cck_fexp_pl(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                         uint8_t* d_gt, hipStream_t st) {
     if (!n) return 0;
-    hipLaunchKernelGGL(cc::pl::k_fexp, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, d_f, d_scratch, d_flags, d_verdicts,
-                       d_gt);
+    if (n == 1)  // latency-bound: the wide one-wave form
+        hipLaunchKernelGGL(cc::pl::k_fexp1, dim3(1), dim3(64), 0, st, d_f, d_scratch, d_flags, d_verdicts, d_gt);
+    else
+        hipLaunchKernelGGL(cc::pl::k_fexp, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, d_f, d_scratch, d_flags,
+                           d_verdicts, d_gt);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -17,7 +17,7 @@
 #include "pairing.h"
 #include "soa.h"
 #include "subgroup.h"
-#include "tower_pl.h"  // pl::swp (lane-pair exchange)
+#include "curve_pl.h"  // pair-lane G2 (FT<pl::Fp2>), pl::swp
 
 using namespace cc;
 
@@ -443,6 +443,57 @@ __global__ __launch_bounds__(256) void k_prep_sigg1(size_t n, int q, const uint8
     flags[i] = fl;
 }
 
+// SigG1, shared verkey, one credential per lane PAIR: lane h decodes sigma_{h+1} (one-lane G1) and
+// the G2 verkey MSM X~ + sum m_j Y~_j runs on the pair-lane Fp2 (curve_pl.h): both lanes hold halves
+// of one Jacobian accumulator, each table entry is read as halves.  The one-lane form keeps a G2
+// accumulator and entry in ~150 words a lane (1 wave/SIMD, spills); here they take half, and every
+// Fp2 product costs half the mads a lane.
+__global__ __launch_bounds__(256, 2) void k_prep_sigg1_pair(size_t n, int q, const uint8_t* __restrict__ s1b,
+                                                            const uint8_t* __restrict__ s2b,
+                                                            const uint8_t* __restrict__ msgs,
+                                                            const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                            const uint32_t* __restrict__ table, int wbits,
+                                                            const uint32_t* __restrict__ binf_fixed,
+                                                            uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t i = g >> 1;
+    const int h = (int)(g & 1);
+    if (i >= n) return;  // pair-uniform
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp> a;
+        if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
+        if (h) fp_neg(a.y, a.y);  // -sigma_2
+        const int slot = h ? S_P2 : S_P1;
+        st_fp(S, slot, i, a.x);
+        st_fp(S, slot + 1, i, a.y);
+    }
+    fl |= pl::swp(fl);
+    Jac<pl::Fp2> acc;
+    if (Xinf) {
+        jac_set_inf(acc);
+    } else {
+        Aff<pl::Fp2> x;
+        for (int c = 0; c < NL; c++) {
+            x.x.c.v[c] = Xaff[NL * h + c];
+            x.y.c.v[c] = Xaff[2 * NL + NL * h + c];
+        }
+        jac_from_aff(acc, x);
+    }
+    for (int j = 0; j < q; j++) {
+        if (binf_fixed[j]) continue;  // uniform across the batch (shared verkey)
+        Fr m;
+        fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
+        pl::ft_add_g2(acc, m.v, table, wbits, j, 0, ft_nwin(wbits));
+    }
+    Aff<pl::Fp2> a;
+    if (!jac_to_aff(a, acc)) fl |= 4u;
+    pl::st_f2(S, S_Q1, i, a.x);
+    pl::st_f2(S, S_Q1 + 2, i, a.y);
+    if (!h) flags[i] = fl;
+}
+
 // Fixed-argument lines for the constant G2 point g~ (SigG1): per Miller step, (l0, l2c, l3c)
 // — 63 doubling + 5 addition steps, stored in loop order.  One thread computes them at setup.
 __global__ __launch_bounds__(64) void k_gtilde_lines(const uint32_t* __restrict__ gtilde, uint32_t* __restrict__ lines) {
@@ -560,8 +611,8 @@ int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const ui
                                wbits, d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
     } else {
         if (fixed)
-            hipLaunchKernelGGL(k_prep_sigg1<true>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
-                               wbits, d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
+            hipLaunchKernelGGL(k_prep_sigg1_pair, dim3(nblocks(2 * n, 256)), b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff,
+                               Xinf, d_table, wbits, d_binf_fixed, d_prep, d_flags);
         else
             hipLaunchKernelGGL(k_prep_sigg1<false>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
                                wbits, d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);

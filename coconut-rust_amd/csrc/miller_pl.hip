@@ -26,7 +26,7 @@
 #define CC_FP_INLINE 1
 #endif
 #include "codec.h"
-#include "tower_pl.h"
+#include "curve_pl.h"
 
 namespace cc {
 namespace pl {
@@ -129,10 +129,13 @@ static __device__ __noinline__ void miller_add(StepState* st, const uint32_t* qs
 // symbol names: the same name in both would be merged by the linker as one weak definition.
 // NP = 1: pair 0 only (RLC mode, whose second pairs are folded into per-bucket pairs, fold.hip).
 // The Miller value of credential i goes to fout as SoA element foff + i of stride fstride.
+// qcheck (NP = 1, SigG2): pair 0's Q (sigma_1) gets the G2 subgroup test from the loop's own T
+// (curve_pl.h miller_t_in_subgroup); a failure sets *qcheck (the RLC batch then falls back).
 template <int SIG, bool kLane2, int NP>
 __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __restrict__ prep,
                                                const uint32_t* __restrict__ flags, const uint32_t* __restrict__ cst,
-                                               uint32_t* __restrict__ fout, size_t fstride, size_t foff) {
+                                               uint32_t* __restrict__ fout, size_t fstride, size_t foff,
+                                               uint32_t* __restrict__ qcheck) {
     __shared__ uint32_t lds[NP == 2 ? TW : 1][MB];
     const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
     if (i >= n) return;  // pair-uniform
@@ -204,6 +207,12 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
             }
         }
     }
+    if (NP == 1 && kSigG2 && qcheck && !skip0) {
+        Aff<Fp2> q;
+        ld_f2(q.x, S, S_Q1, i);
+        ld_f2(q.y, S, S_Q1 + 2, i);
+        if (!miller_t_in_subgroup(T, q) && !half_id()) atomicOr(qcheck, 1u);
+    }
     f12_conj(f, f);
     st_f12(Soa{fout, fstride}, foff + i, f);
 }
@@ -217,22 +226,24 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
 #define CC_MILLER_LAUNCH cck_miller_pl_g1
 #endif
 
-// lane2: per-lane second-pair P (RLC pseudo-pairs); np: pairs per credential (1 or 2); the Miller
-// values go to SoA elements [foff, foff + n) of stride fstride (>= foff + n)
+// lane2: per-lane second-pair P; np: pairs per credential (1 or 2); the Miller values go to SoA
+// elements [foff, foff + n) of stride fstride (>= foff + n); d_qcheck (np = 1, SigG2, or null): the
+// sigma_1 subgroup test from the loop's T
 extern "C" int CC_MILLER_LAUNCH(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
-                                const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, hipStream_t st) {
+                                const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff,
+                                uint32_t* d_qcheck, hipStream_t st) {
     if (!n) return 0;
     if (fstride < foff + n || (np != 1 && np != 2)) return -1;
     constexpr int MB = cc::pl::MB;
     dim3 g((unsigned)((2 * n + MB - 1) / MB)), b(MB);
     if (np == 1)
         hipLaunchKernelGGL((cc::pl::k_miller<CC_MILLER_SIG, false, 1>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
-                           fstride, foff);
+                           fstride, foff, d_qcheck);
     else if (lane2)
         hipLaunchKernelGGL((cc::pl::k_miller<CC_MILLER_SIG, true, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
-                           fstride, foff);
+                           fstride, foff, d_qcheck);
     else
         hipLaunchKernelGGL((cc::pl::k_miller<CC_MILLER_SIG, false, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
-                           fstride, foff);
+                           fstride, foff, d_qcheck);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

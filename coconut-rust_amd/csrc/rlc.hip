@@ -67,8 +67,9 @@ DEV void st_aff_aos(uint32_t* p, const Aff<F>& a) {
 //   k_rlc_msm_*   : delta X~ + sum (delta m_j) Y~_j (delta recomputed from the key stream) as pair 0's
 //                   other argument, flag bit 2
 // one credential per lane PAIR: lane h decodes sigma_{h+1} and writes its outputs (h = 0: sigma_1 as
-// pair 0's Q; h = 1: the fold point -sigma_2); both subgroup checks run on the pair-lane Fp2
-// (curve_pl.h: 3 Fp a lane for a Jacobian G2 point); each lane writes 8 of delta's 16 digits.
+// pair 0's Q; h = 1: the fold point -sigma_2); sigma_2's subgroup test runs on the pair-lane Fp2
+// (curve_pl.h: 3 Fp a lane for a Jacobian G2 point) — sigma_1's comes free from the Miller loop's T;
+// each lane writes 8 of delta's 16 digits.
 __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t base_index,
                                                             const uint32_t* __restrict__ key,
                                                             const uint8_t* __restrict__ s1b,
@@ -93,10 +94,8 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t b
         st_aff_aos<Fp2>(pts + i * (sizeof(Aff<Fp2>) / 4), m);
     }
     fl |= pl::swp(fl);  // both decode flags on both lanes
+    // sigma_1's subgroup test runs in the Miller kernel, from its own T (miller_t_in_subgroup)
     Aff<pl::Fp2> p;
-    p.x = pl::f2_from_lane(a.x, 0);
-    p.y = pl::f2_from_lane(a.y, 0);
-    if (!(fl & 1u) && !pl::g2_in_subgroup(p)) fl |= 32u;
     p.x = pl::f2_from_lane(a.x, 1);
     p.y = pl::f2_from_lane(a.y, 1);
     if (!(fl & 2u) && !pl::g2_in_subgroup(p)) fl |= 32u;
@@ -179,34 +178,37 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, uint64_t b
     }
 }
 
-__global__ __launch_bounds__(256) void k_rlc_msm_sigg1(size_t n, int q, uint64_t base_index,
+// one credential per lane PAIR: the G2 MSM on the pair-lane Fp2 (curve_pl.h ft_add_g2)
+__global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg1(size_t n, int q, uint64_t base_index,
                                                           const uint32_t* __restrict__ key,
                                                           const uint8_t* __restrict__ msgs,
                                                           const uint32_t* __restrict__ table, int wbits,
                                                           const uint32_t* __restrict__ binf,
                                                           uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
-    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t i = g >> 1;
+    if (i >= n) return;  // pair-uniform
     const Soa S{prep, n};
     uint32_t kk[NR], d[NR], w4[4];
     for (int k = 0; k < 8; k++) kk[k] = key[k];
     rlc_delta_signed(d, w4, kk, base_index + i);
-    Jac<Fp2> acc;
+    Jac<pl::Fp2> acc;
     jac_set_inf(acc);
     const int nwin = ft_nwin(wbits);
-    if (!binf[q + 1]) ft_add<Fp2>(acc, d, table, wbits, q + 1, 0, nwin);
+    if (!binf[q + 1]) pl::ft_add_g2(acc, d, table, wbits, q + 1, 0, nwin);
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
         fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
         uint32_t dm[NR];
         fr_mul_canon(dm, d, m.v);
-        ft_add<Fp2>(acc, dm, table, wbits, j, 0, nwin);
+        pl::ft_add_g2(acc, dm, table, wbits, j, 0, nwin);
     }
-    Aff<Fp2> a2;
-    if (!jac_to_aff(a2, acc)) flags[i] |= 4u;
-    st_f2(S, S_Q1, i, a2.x);
-    st_f2(S, S_Q1 + 2, i, a2.y);
+    Aff<pl::Fp2> a2;
+    const bool fin = jac_to_aff(a2, acc);
+    pl::st_f2(S, S_Q1, i, a2.x);
+    pl::st_f2(S, S_Q1 + 2, i, a2.y);
+    if (!fin && !pl::half_id()) flags[i] |= 4u;
 }
 
 // out[t] = in[2t] * in[2t+1] (in[2t] alone for an odd tail); SoA strides n_in / n_out.  One product
@@ -260,23 +262,28 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 
 extern "C" {
 
-// d_pts: n fold points (AoS affine: 48 words SigG2, 24 SigG1); d_dig: 16 x n digit bytes
-int cck_prep_rlc(int mode, size_t n, int q, uint64_t base_index, const uint32_t* d_key, const uint8_t* d_s1,
-                 const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
-                 uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, uint32_t* d_pts, int8_t* d_dig,
-                 hipStream_t st) {
+// d_pts: n fold points (AoS affine: 48 words SigG2, 24 SigG1); d_dig: 16 x n digit bytes.
+// part 0: decode + subgroup checks + the fold's inputs; part 1: the delta-scaled MSM
+int cck_prep_rlc(int mode, int part, size_t n, int q, uint64_t base_index, const uint32_t* d_key,
+                 const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits,
+                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, uint32_t* d_pts,
+                 int8_t* d_dig, hipStream_t st) {
     if (!n) return 0;
-    dim3 g(nblocks(n, 256)), b(256);
-    if (mode == 0) {
-        hipLaunchKernelGGL(k_rlc_check_sigg2, dim3(nblocks(2 * n, 256)), b, 0, st, n, base_index, d_key, d_s1, d_s2, d_prep, d_flags, d_any,
-                           d_pts, d_dig);
-        hipLaunchKernelGGL(k_rlc_msm_sigg2, g, b, 0, st, n, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
-                           d_prep, d_flags);
+    const dim3 g2(nblocks(2 * n, 256)), g1(nblocks(n, 256)), b(256);
+    if (part == 0) {
+        if (mode == 0)
+            hipLaunchKernelGGL(k_rlc_check_sigg2, g2, b, 0, st, n, base_index, d_key, d_s1, d_s2, d_prep, d_flags,
+                               d_any, d_pts, d_dig);
+        else
+            hipLaunchKernelGGL(k_rlc_check_sigg1, g2, b, 0, st, n, base_index, d_key, d_s1, d_s2, d_prep, d_flags,
+                               d_any, d_pts, d_dig);
     } else {
-        hipLaunchKernelGGL(k_rlc_check_sigg1, dim3(nblocks(2 * n, 256)), b, 0, st, n, base_index, d_key, d_s1, d_s2, d_prep, d_flags, d_any,
-                           d_pts, d_dig);
-        hipLaunchKernelGGL(k_rlc_msm_sigg1, g, b, 0, st, n, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
-                           d_prep, d_flags);
+        if (mode == 0)
+            hipLaunchKernelGGL(k_rlc_msm_sigg2, g1, b, 0, st, n, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
+                               d_prep, d_flags);
+        else
+            hipLaunchKernelGGL(k_rlc_msm_sigg1, g2, b, 0, st, n, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
+                               d_prep, d_flags);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
