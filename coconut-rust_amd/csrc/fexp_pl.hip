@@ -32,7 +32,9 @@ DEV void fx_apply(Fp12& x, int op) {
     }
 }
 
-// dst <- src^-1
+// dst <- src^-1 (templated like every step: the one-wave kernel's looser register bound must not
+// reach k_fexp through a shared out-of-line function)
+template <bool W>
 static __device__ __noinline__ void fx_inv(Soa src, Soa dst, size_t i) {
     Fp12 f, t;
     ld_f12(f, src, i);
@@ -436,7 +438,7 @@ DEV void fexp_chain(size_t n, size_t i, uint32_t* fbuf, uint32_t* scratch) {
     const Soa F{fbuf, n};
     const Soa T{scratch, n}, A{scratch + (size_t)12 * NL * n, n}, S{scratch + (size_t)24 * NL * n, n},
         R{scratch + (size_t)36 * NL * n, n}, K{scratch + (size_t)48 * NL * n, n};
-    fx_inv(F, T, i);
+    fx_inv<W>(F, T, i);
     fx_mul<W>(F, OP_CONJ, T, OP_ID, F, i);   // f^(p^6 - 1)
     fx_mul<W>(F, OP_FROB2, F, OP_ID, F, i);  // ^(p^2 + 1)
     fx_cube<W>(F, R, i);                     // res = f^3
@@ -485,10 +487,9 @@ __global__ __launch_bounds__(256, 2) void k_fexp(size_t n, uint32_t* __restrict_
 }
 
 // one element on one wave (64 lanes, all pairs holding the same values; pair 0 writes the outputs).
-// Bounds (64, 2) = k_fexp's register budget of 2 waves/SIMD (HIP's second bound is waves per SIMD):
-// the two kernels share out-of-line step functions, and a looser bound here would let those grow
-// past k_fexp's 256 VGPRs.
-__global__ __launch_bounds__(64, 2) void k_fexp1(uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
+// One wave per SIMD (HIP's second bound): the whole register file; every step function is a W = true
+// instantiation of its own, so the bound does not reach k_fexp's 2 waves/SIMD budget.
+__global__ __launch_bounds__(64, 1) void k_fexp1(uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
                                               const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
                                               uint8_t* __restrict__ gt_out) {
     fexp_chain<true>(1, 0, fbuf, scratch);
