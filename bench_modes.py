@@ -285,7 +285,7 @@ def bench_pok(args):
         from bench import kernel_table, cpu_info
         peak = peak_mad_per_s()
         counts = opcounts("pok_sigg2_q32_r8")
-        kt = kernel_table(phase_ms, n, counts, 2 * 192 + 2 * 97 + (nresp + 1 + r) * 48, peak)
+        kt = kernel_table(phase_ms, n, counts, 2 * 192 + 2 * 97 + (nresp + 1 + r) * 48, peak, "k_prep_pok")
         dom = max(kt, key=lambda k: kt[k]["ms"])
         out = {
             "metric": "verified PoK-of-signature proofs/sec (msg_count=32, 8 revealed)",
