@@ -14,5 +14,5 @@ for k in 1 2; do
     COCONUT_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/verify_$v.$k.json" 2>&1 || exit 1
   done
 done
-timeout -k 10 300 python -u bench.py --mode rlc --steps 5 --warmup 1 > "$OUT/bench_rlc.json" 2>&1 || exit 1
+[ -n "$AB_RLC" ] && { timeout -k 10 300 python -u bench.py --mode rlc --steps 5 --warmup 1 > "$OUT/bench_rlc.json" 2>&1 || exit 1; }
 echo "[ab] done"
