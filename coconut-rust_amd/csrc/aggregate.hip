@@ -311,21 +311,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
             jac_add_aff(acc, acc, e);
         }
     }
-    // butterfly over the L2 pairs of the task (lane distances 2, 4, ..: halves stay with halves)
-    constexpr int JWF = sizeof(cc::Jac<F>) / 4;
-#pragma unroll 1
-    for (int m = L >> 1; m >= 2; m >>= 1) {
-        cc::Jac<F> o;
-        const uint32_t* a = reinterpret_cast<const uint32_t*>(&acc);
-        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
-        for (int c = 0; c < JWF; c++) ow[c] = (uint32_t)__shfl_xor((int)a[c], m);
-        if (threadIdx.x & m) {
-            cc::Jac<F> tmp = acc;
-            acc = o;
-            o = tmp;
-        }
-        jac_add(acc, acc, o);
-    }
+    pl::pair_group_sum<L>(acc);  // over the L2 pairs of the task
     if (pair == 0) {
         cc::Aff<F> r;
         const bool fin = jac_to_aff(r, acc);

@@ -103,6 +103,28 @@ DEV void ft_add_g2(Jac<Fp2>& acc, const uint32_t k[8], const uint32_t* __restric
     }
 }
 
+// curve.h lane_group_sum for lane-pair points: the sum over the L / 2 pairs of L consecutive lanes
+// (L a power of two <= 64), butterfly at lane distances L/2 .. 2 so halves stay with halves; every
+// pair ends with the same sum.
+template <int L>
+DEV void pair_group_sum(Jac<Fp2>& acc) {
+    constexpr int JW = sizeof(Jac<Fp2>) / 4;
+#pragma unroll 1
+    for (int m = L >> 1; m >= 2; m >>= 1) {
+        Jac<Fp2> o;
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(&acc);
+        uint32_t* w = reinterpret_cast<uint32_t*>(&o);
+        for (int c = 0; c < JW; c++) w[c] = (uint32_t)__shfl_xor((int)a[c], m);
+        // same operand order on both partners so they hold the same representation
+        if (threadIdx.x & m) {
+            Jac<Fp2> t = acc;
+            acc = o;
+            o = t;
+        }
+        jac_add(acc, acc, o);
+    }
+}
+
 // the lane-pair form of a one-lane Fp2 value held by lane `src` of the pair (both lanes call it)
 DEV Fp2 f2_from_lane(const cc::Fp2& v, int src) {
     const bool im = half_id() != 0;

@@ -18,11 +18,16 @@
 //                                                 bucket lists, each padded to FS-entry chunks
 //   k_fold_sum<F>                               : one lane per chunk: mixed additions of its points
 //   k_fold_reduce<F>                            : one wave per bucket: chunk partials, butterfly, affine
+//   k_fold_sum_g2pl / k_fold_reduce_g2pl        : the same for G2 buckets (SigG2) on the pair-lane
+//                                                 Fp2 (curve_pl.h): one LANE PAIR per chunk / 32 pairs
+//                                                 per bucket, 2 waves/SIMD where the one-lane G2
+//                                                 forms need 448-512 registers (1 wave/SIMD)
 //   k_fold_fixed<F>                             : the fixed points P_w,d (once per verkey)
 // X_i = -sigma_2,i (AoS affine, written by the RLC prep); B_w,d lands in the pseudo-credentials' prep
 // SoA (soa.h slots, stride FB; bucket b = pseudo-credential b, pair 0) as the Q side (SigG2: B in G2)
 // or the P side (SigG1: B in G1), P_w,d on the other side.
 #include "codec.h"
+#include "curve_pl.h"
 #include "fixed.h"
 #include "soa.h"
 
@@ -184,6 +189,59 @@ __global__ __launch_bounds__(64) void k_fold_reduce(const uint32_t* __restrict__
     flags2[b] = (!fin || fixed_inf[b]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
 }
 
+// k_fold_sum for G2 points on the pair-lane Fp2: one lane pair per chunk, each lane adds its halves.
+// part: chunk c's partial at c * 72 words, lane h's half (X, Y, Z halves: 36 words) at + 36 h.
+__global__ __launch_bounds__(256, 2) void k_fold_sum_g2pl(size_t maxchunks, const uint32_t* __restrict__ off,
+                                                          const uint32_t* __restrict__ list,
+                                                          const uint32_t* __restrict__ pts,
+                                                          uint32_t* __restrict__ part) {
+    constexpr int AW = sizeof(Aff<Fp2>) / 4, JW = sizeof(Jac<Fp2>) / 4, HW = sizeof(Jac<pl::Fp2>) / 4;
+    const size_t c = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // pair-uniform
+    const int h = (int)pl::half_id();
+    if (c >= maxchunks || c * FS >= off[FB]) return;
+    Jac<pl::Fp2> acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (int e = 0; e < FS; e++) {
+        const uint32_t v = list[c * FS + e];
+        if (v == PAD) continue;
+        const uint32_t* p = pts + (size_t)(v & 0x7fffffffu) * AW;
+        Aff<pl::Fp2> a;
+        pl::ld_f2_aos(a.x, p);
+        pl::ld_f2_aos(a.y, p + 2 * NL);
+        if (v >> 31) pl::f2_neg(a.y, a.y);
+        jac_add_aff(acc, acc, a);
+    }
+    st_jac_aos<pl::Fp2>(part + c * JW + h * HW, acc);
+}
+
+// k_fold_reduce<Fp2, true> on the pair-lane Fp2: one wave (32 lane pairs) per bucket
+__global__ __launch_bounds__(64, 2) void k_fold_reduce_g2pl(const uint32_t* __restrict__ off,
+                                                           const uint32_t* __restrict__ part,
+                                                           const uint8_t* __restrict__ fixed_inf,
+                                                           uint32_t* __restrict__ prep2, uint32_t* __restrict__ flags2) {
+    constexpr int JW = sizeof(Jac<Fp2>) / 4, HW = sizeof(Jac<pl::Fp2>) / 4;
+    const int b = blockIdx.x;
+    const int h = (int)pl::half_id();
+    const uint32_t c0 = off[b] / FS, c1 = off[b + 1] / FS;
+    Jac<pl::Fp2> acc;
+    jac_set_inf(acc);
+#pragma unroll 1
+    for (uint32_t c = c0 + (threadIdx.x >> 1); c < c1; c += 32) {
+        Jac<pl::Fp2> p;
+        ld_jac_aos<pl::Fp2>(p, part + (size_t)c * JW + h * HW);
+        jac_add(acc, acc, p);
+    }
+    pl::pair_group_sum<64>(acc);
+    if (threadIdx.x >= 2) return;
+    Aff<pl::Fp2> a;
+    const bool fin = jac_to_aff(a, acc);
+    const Soa S{prep2, FB};
+    pl::st_f2(S, S_Q1, b, a.x);
+    pl::st_f2(S, S_Q1 + 2, b, a.y);
+    if (!h) flags2[b] = (!fin || fixed_inf[b]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
+}
+
 // P_w,d = (256^w d) g~ from g~'s fixed-base table (base index q of the verkey tables); G is g~'s field
 template <class G>
 __global__ __launch_bounds__(256) void k_fold_fixed(int q, const uint32_t* __restrict__ table, int wbits,
@@ -249,8 +307,8 @@ int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uin
     hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(256), 0, st, cnt, off, cur);
     hipLaunchKernelGGL(k_fold_scatter, gw, dim3(256), 0, st, n, d_dig, cur, list);
     if (mode == 0) {
-        hipLaunchKernelGGL(k_fold_sum<Fp2>, dim3(nblocks(mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
-        hipLaunchKernelGGL((k_fold_reduce<Fp2, true>), dim3(FB), dim3(64), 0, st, off, part, finf, d_prep2, d_flags2);
+        hipLaunchKernelGGL(k_fold_sum_g2pl, dim3(nblocks(2 * mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
+        hipLaunchKernelGGL(k_fold_reduce_g2pl, dim3(FB), dim3(64), 0, st, off, part, finf, d_prep2, d_flags2);
     } else {
         hipLaunchKernelGGL(k_fold_sum<Fp>, dim3(nblocks(mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
         hipLaunchKernelGGL((k_fold_reduce<Fp, false>), dim3(FB), dim3(64), 0, st, off, part, finf, d_prep2, d_flags2);
