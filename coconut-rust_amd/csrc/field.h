@@ -490,8 +490,9 @@ DEV void fp_from_s30(Fp& r, const S30& a) {
     }
 }
 
-// r = a^-1 in Montgomery form (a in Montgomery form); 0 -> 0 like Fermat's a^(p-2).
-DEV void fp_inv(Fp& r, const Fp& a) {
+// r = a^-1 mod p as a plain integer (a < p; 0 -> 0).  fp_inv below and the lazy layer (lazy.h) put
+// it back into their own Montgomery forms.
+DEV void fp_inv_int(Fp& r, const Fp& a) {
     S30 d, e, f, g;
 #pragma unroll
     for (int i = 0; i < S30N; i++) {
@@ -524,8 +525,13 @@ DEV void fp_inv(Fp& r, const Fp& a) {
     S30 t = d;
     s30_add_kp(t, -1);
     if (t.v[S30N - 1] >= 0) d = t;
+    fp_from_s30(r, d);
+}
+
+// r = a^-1 in Montgomery form (a in Montgomery form); 0 -> 0 like Fermat's a^(p-2).
+DEV void fp_inv(Fp& r, const Fp& a) {
     Fp x, r3;
-    fp_from_s30(x, d);
+    fp_inv_int(x, a);
     constexpr uint32_t R3[NL] = {CC_R3_LIMBS};
 #pragma unroll
     for (int j = 0; j < NL; j++) r3.v[j] = R3[j];

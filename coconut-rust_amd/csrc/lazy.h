@@ -1,0 +1,501 @@
+// Lazy-reduced pair-lane field layer for the pairing kernels (Miller loop, final exponentiation) on
+// gfx950 — device code (the product path).  Same field, tower and lane-pair layout as tower_pl.h
+// (AMCL's BLS12-381 tower, reached by the reference through amcl_wrapper 0.1.7; SURVEY.md §8a rows
+// T3, V6); different number representation:
+//
+//   Fq   14 SIGNED 28-bit-radix limbs, V = sum v_k 2^(28k), Montgomery radix R' = 2^392.  Values are
+//        neither reduced mod p nor limb-normalised: additions, subtractions and negations are 14
+//        carry-free v_add/v_sub (no borrow chains, no conditional subtraction of p), and the
+//        multiplication takes the limbs as they are (signed v_mad_i64_i32 product scanning, one
+//        accumulator chain per column) and returns normalised limbs with V < 1.13 p.  Nothing is
+//        converted per multiplication (tower_pl.h converts 12 x 32 <-> 14 x 29 at each one and
+//        subtracts p).
+//
+// Correctness rests on two bounds carried in the TYPE of every value, checked at compile time:
+//   A  limb magnitude, units of 2^20:   |v_k| < A 2^20 for every limb (normalised: A = 256)
+//   B  value magnitude, units of p/16:  |V| < B p / 16          (canonical: 16; product: >= 18)
+// * multiplication: every column of sum a_i b_j (+ c_i d_j) + m_i p_j + carry must fit a signed 64-bit
+//   accumulator: 14 (sum A_a A_b) 2^40 + 14 2^56 + 2^36 < 2^63  <=>  sum A_a A_b <= 533,000.
+//   Its result is (ab + cd + m p) / R' with 0 <= m < R', so |V| < (sum B_a B_b / 256) p^2 / R' + p,
+//   i.e. B_out = 16 + ceil(sum B_a B_b / 40,304)  (p / R' < 1 / 2,520).
+// * squeeze (parallel carry, 3 ops a limb): limbs back to A = 257, value unchanged; valid while the top
+//   limb (V / 2^364) stays below 2^28, i.e. B <= 32,768.
+// * limbs are int32: A <= 2,047.
+// A formula that breaks a bound does not compile (static_assert), so overflow cannot happen at run
+// time whatever the inputs; the squeezes in tower_lz.h are exactly the ones the bounds demand.
+//
+// Boundary: kernels keep their SoA inputs/outputs in the storage form of field.h (12 x 32 canonical,
+// R = 2^406).  in_r() moves a value to R' form (x R * 2^378 / R' = x R'), out_r() back (x R' * R /
+// R' = x R), each one Montgomery multiplication; canon() gives the canonical residue (rare: outputs,
+// equality tests, inversion inputs).
+#pragma once
+#include "tower_pl.h"
+
+namespace cc {
+namespace lz {
+
+constexpr int LN = 14;
+constexpr int32_t LM = 0x0fffffff;
+constexpr int AN = 256;  // normalised limbs (product output)
+constexpr int AS = 257;  // squeezed limbs
+constexpr int BC = 16;   // canonical value (< p)
+constexpr long long AMAX = 533000;
+constexpr int bprod(long long s) { return 16 + (int)((s + 40303) / 40304); }
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
+
+#define LZ_P_LIMBS 0xfffaaab, 0xfefffff, 0x3ffffb9, 0xfffeb15, 0x6241eab, 0xa0f6b0f, 0xf6730d2, 0xf38512b, 0x4774b84, \
+    0x4bacd76, 0xba7b643, 0xe69a4b1, 0x1ea397f, 0x001a011
+constexpr uint32_t LZ_N0 = 0xffcfffdu;  // -p^-1 mod 2^28
+// 2^406 mod p (= R mod p): R' form -> R form, and the line scaling of miller_lz.hip
+#define LZ_C_OUT_LIMBS 0x3a9fb84, 0x7400d20, 0xc4a23c5, 0xacde629, 0x6cb6147, 0x0b7e6d2, 0x16b0f4b, 0xc2b7d6e, 0x1ecbde7, \
+    0xdd80b89, 0xa23c34f, 0xd636d56, 0xc30f3a0, 0x0013317
+// R'^3 mod p: inversion
+#define LZ_R3_LIMBS 0x1f7b890, 0x294cc4d, 0x9f3af22, 0xb5ba56c, 0xcb5c0cc, 0xc0d975c, 0xc89a8c5, 0x6c968b4, 0x22672ea, \
+    0x91de8c9, 0x35652a6, 0x84977c8, 0x424bbb9, 0x00141ab
+// R' mod p (one)
+#define LZ_ONE_LIMBS 0x347fcb8, 0xd800000, 0x002b119, 0x0cde6d2, 0xc7212e0, 0x83a2090, 0x037669f, 0xda0f73e, 0x9b09b42, \
+    0x1297bb0, 0x515d98f, 0x012ca7c, 0x659fcfa, 0x000577a
+constexpr double LZ_PH = 28591897852287.902;  // p / 2^336
+
+DEV int32_t lz_p(int k) {
+    constexpr int32_t P[LN] = {LZ_P_LIMBS};
+    return P[k];
+}
+
+template <int A, int B>
+struct Fq {
+    static_assert(A <= 2047, "limbs must fit int32");
+    static constexpr int AV = A, BV = B;
+    int32_t v[LN];
+};
+struct W14 {
+    int32_t v[LN];
+};
+
+template <int A2, int B2, int A, int B>
+DEV Fq<A2, B2> fit(const Fq<A, B>& x) {
+    static_assert(A <= A2 && B <= B2, "fit: bound exceeds the target type");
+    Fq<A2, B2> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = x.v[k];
+    return r;
+}
+
+// ---------------------------------------------------------------- Montgomery product scanning
+// Column k: the caller's products are in acc; add m_i p_j, derive m_k (k < 14) or emit limb k - 14,
+// shift.  All signed 64-bit (arithmetic shift): inputs may be negative, m and p are in [0, 2^28).
+DEV void lz_redc_col(int k, int64_t& acc, int32_t m[LN], int32_t r[LN]) {
+#pragma unroll
+    for (int i = 0; i < LN; i++) {
+        const int j = k - i;
+        if (i >= k || j < 0 || j >= LN) continue;
+        acc += (int64_t)m[i] * lz_p(j);
+    }
+    if (k < LN) {
+        m[k] = (int32_t)(((uint32_t)acc * LZ_N0) & (uint32_t)LM);
+        acc += (int64_t)m[k] * lz_p(0);
+    } else {
+        r[k - LN] = (int32_t)acc & LM;
+    }
+    acc >>= 28;
+}
+
+// (a b + c d) / R' mod p (NP = 2) or a b / R' (NP = 1); limbs 0..12 of the result in [0, 2^28)
+template <int NP>
+DEV W14 lz_mont(const int32_t a[LN], const int32_t b[LN], const int32_t c[LN], const int32_t d[LN]) {
+    int32_t m[LN];
+    W14 r;
+    int64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * LN - 1; k++) {
+        int64_t acc2 = 0;
+#pragma unroll
+        for (int i = 0; i < LN; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= LN) continue;
+            acc += (int64_t)a[i] * b[j];
+            if (NP == 2) acc2 += (int64_t)c[i] * d[j];
+        }
+        if (NP == 2) acc += acc2;
+        lz_redc_col(k, acc, m, r.v);
+    }
+    r.v[LN - 1] = (int32_t)acc;
+    return r;
+}
+
+DEV int32_t swp(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true); }
+using pl::half_id;
+
+// own half of x * y for pair-lane Fp2 values x, y: re  x y + xs (-ys),  im  x ys + xs y
+DEV W14 lz_f2_mul_v(const W14& x, const W14& y) {
+    const bool im = half_id() != 0;
+    int32_t xs[LN], b[LN], d[LN];
+#pragma unroll
+    for (int k = 0; k < LN; k++) {
+        xs[k] = swp(x.v[k]);
+        const int32_t ys = swp(y.v[k]);
+        b[k] = im ? ys : y.v[k];
+        d[k] = im ? y.v[k] : -ys;
+    }
+    return lz_mont<2>(x.v, b, xs, d);
+}
+// own half of x^2: re (x + xs)(x - xs),  im xs (2 x)
+DEV W14 lz_f2_sqr_v(const W14& x) {
+    const bool im = half_id() != 0;
+    int32_t u[LN], w[LN];
+#pragma unroll
+    for (int k = 0; k < LN; k++) {
+        const int32_t xs = swp(x.v[k]);
+        u[k] = im ? xs : x.v[k] + xs;
+        w[k] = im ? x.v[k] + x.v[k] : x.v[k] - xs;
+    }
+    return lz_mont<1>(u, w, u, w);
+}
+DEV W14 lz_mul_v(const W14& x, const W14& y) { return lz_mont<1>(x.v, y.v, x.v, y.v); }
+
+#define LZ_L14(x) int32_t x##0, int32_t x##1, int32_t x##2, int32_t x##3, int32_t x##4, int32_t x##5, int32_t x##6, \
+    int32_t x##7, int32_t x##8, int32_t x##9, int32_t x##10, int32_t x##11, int32_t x##12, int32_t x##13
+#define LZ_V14(x) x##0, x##1, x##2, x##3, x##4, x##5, x##6, x##7, x##8, x##9, x##10, x##11, x##12, x##13
+#define LZ_E14(x) x.v[0], x.v[1], x.v[2], x.v[3], x.v[4], x.v[5], x.v[6], x.v[7], x.v[8], x.v[9], x.v[10], x.v[11], \
+    x.v[12], x.v[13]
+#ifdef CC_FP_INLINE
+DEV void lz_opaque(W14& x) {
+#pragma unroll
+    for (int k = 0; k < LN; k++) asm volatile("" : "+v"(x.v[k]));
+}
+DEV W14 lz_f2_mul_c(W14 x, W14 y) {
+    W14 r;
+    do {
+        lz_opaque(x);
+        lz_opaque(y);
+        r = lz_f2_mul_v(x, y);
+    } while (cc_opaque_false());
+    return r;
+}
+DEV W14 lz_f2_sqr_c(W14 x) {
+    W14 r;
+    do {
+        lz_opaque(x);
+        r = lz_f2_sqr_v(x);
+    } while (cc_opaque_false());
+    return r;
+}
+DEV W14 lz_mul_c(W14 x, W14 y) {
+    W14 r;
+    do {
+        lz_opaque(x);
+        lz_opaque(y);
+        r = lz_mul_v(x, y);
+    } while (cc_opaque_false());
+    return r;
+}
+#else
+static __device__ __noinline__ W14 lz_f2_mul_call(LZ_L14(a), LZ_L14(b)) {
+    const W14 A = {{LZ_V14(a)}}, B = {{LZ_V14(b)}};
+    return lz_f2_mul_v(A, B);
+}
+static __device__ __noinline__ W14 lz_f2_sqr_call(LZ_L14(a)) {
+    const W14 A = {{LZ_V14(a)}};
+    return lz_f2_sqr_v(A);
+}
+static __device__ __noinline__ W14 lz_mul_call(LZ_L14(a), LZ_L14(b)) {
+    const W14 A = {{LZ_V14(a)}}, B = {{LZ_V14(b)}};
+    return lz_mul_v(A, B);
+}
+DEV W14 lz_f2_mul_c(const W14& x, const W14& y) { return lz_f2_mul_call(LZ_E14(x), LZ_E14(y)); }
+DEV W14 lz_f2_sqr_c(const W14& x) { return lz_f2_sqr_call(LZ_E14(x)); }
+DEV W14 lz_mul_c(const W14& x, const W14& y) { return lz_mul_call(LZ_E14(x), LZ_E14(y)); }
+#endif
+
+template <int A, int B>
+DEV W14 w14(const Fq<A, B>& x) {
+    W14 r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = x.v[k];
+    return r;
+}
+template <int B>
+DEV Fq<AN, B> fq(const W14& x) {
+    Fq<AN, B> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = x.v[k];
+    return r;
+}
+
+// ---------------------------------------------------------------- canonical residue (rare)
+// the residue of x in [0, p) as 12 x 32-bit limbs (the integer V mod p; still R' form)
+static __device__ __noinline__ Fp lz_canon_call(LZ_L14(a)) {
+    int32_t u[LN] = {LZ_V14(a)};
+    int32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < LN - 1; k++) {
+        const int32_t t = u[k] + c;
+        u[k] = t & LM;
+        c = t >> 28;
+    }
+    u[LN - 1] += c;
+    // V = sum u_k 2^(28k), u_0..12 in [0, 2^28): subtract floor(V / p) p, estimated from the top
+    // 56 bits (off by at most one), then fix up
+    const int64_t h = ((int64_t)u[LN - 1] << 28) + u[LN - 2];
+    const int32_t q = (int32_t)floor((double)h / LZ_PH);
+    {
+        int64_t cc = 0;
+#pragma unroll
+        for (int k = 0; k < LN; k++) {
+            const int64_t t = (int64_t)u[k] - (int64_t)q * lz_p(k) + cc;
+            if (k < LN - 1) {
+                u[k] = (int32_t)(t & LM);
+                cc = t >> 28;
+            } else {
+                u[k] = (int32_t)t;
+            }
+        }
+    }
+    for (int it = 0; it < 2; it++) {  // V < 0: add p
+        if (u[LN - 1] >= 0) break;
+        int32_t cc = 0;
+#pragma unroll
+        for (int k = 0; k < LN; k++) {
+            const int32_t t = u[k] + lz_p(k) + cc;
+            if (k < LN - 1) {
+                u[k] = t & LM;
+                cc = t >> 28;
+            } else {
+                u[k] = t;
+            }
+        }
+    }
+    for (int it = 0; it < 2; it++) {  // V >= p: subtract p
+        int32_t w[LN], cc = 0;
+#pragma unroll
+        for (int k = 0; k < LN; k++) {
+            const int32_t t = u[k] - lz_p(k) + cc;
+            if (k < LN - 1) {
+                w[k] = t & LM;
+                cc = t >> 28;
+            } else {
+                w[k] = t;
+            }
+        }
+        if (w[LN - 1] < 0) break;
+#pragma unroll
+        for (int k = 0; k < LN; k++) u[k] = w[k];
+    }
+    Fp r;
+#pragma unroll
+    for (int w = 0; w < NL; w++) {
+        const int bit = 32 * w, k = bit / 28, s = bit % 28;
+        uint32_t x = (uint32_t)u[k] >> s;
+        if (k + 1 < LN) x |= (uint32_t)u[k + 1] << (28 - s);
+        if (s > 24 && k + 2 < LN) x |= (uint32_t)u[k + 2] << (56 - s);
+        r.v[w] = x;
+    }
+    return r;
+}
+template <int A, int B>
+DEV Fp canon(const Fq<A, B>& x) {
+    static_assert(B <= 32768, "canon: value bound");
+    return lz_canon_call(LZ_E14(x));
+}
+
+// ---------------------------------------------------------------- storage-form conversions
+// the integer of a 12 x 32 value (< 2^384) as normalised limbs; B is the caller's value bound
+template <int B = BC>
+DEV Fq<AN, B> from_fp(const Fp& x) {
+    Fq<AN, B> r;
+    r.v[0] = (int32_t)(x.v[0] & (uint32_t)LM);
+#pragma unroll
+    for (int k = 1; k < LN - 1; k++) {
+        const int bit = 28 * k, w = bit >> 5, s = bit & 31;
+        r.v[k] = (int32_t)((s ? __builtin_amdgcn_alignbit(x.v[w + 1], x.v[w], s) : x.v[w]) & (uint32_t)LM);
+    }
+    r.v[LN - 1] = (int32_t)(x.v[NL - 1] >> 12);
+    return r;
+}
+DEV Fq<AN, BC> fq_const(const int32_t (&c)[LN]) {
+    Fq<AN, BC> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = c[k];
+    return r;
+}
+
+// ---------------------------------------------------------------- lane-local linear operations
+template <int A1, int B1, int A2, int B2>
+DEV Fq<A1 + A2, B1 + B2> add(const Fq<A1, B1>& x, const Fq<A2, B2>& y) {
+    Fq<A1 + A2, B1 + B2> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = x.v[k] + y.v[k];
+    return r;
+}
+template <int A1, int B1, int A2, int B2>
+DEV Fq<A1 + A2, B1 + B2> sub(const Fq<A1, B1>& x, const Fq<A2, B2>& y) {
+    Fq<A1 + A2, B1 + B2> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = x.v[k] - y.v[k];
+    return r;
+}
+template <int A, int B>
+DEV Fq<A, B> neg(const Fq<A, B>& x) {
+    Fq<A, B> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = -x.v[k];
+    return r;
+}
+template <int K, int A, int B>
+DEV Fq<K * A, K * B> smul(const Fq<A, B>& x) {  // x * K for a small constant K
+    Fq<K * A, K * B> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = x.v[k] * K;
+    return r;
+}
+// limbs back to [-A/256 - 1, 2^28 + A/256]: one parallel carry step, value unchanged
+template <int A, int B>
+DEV Fq<AS, B> squeeze(const Fq<A, B>& x) {
+    static_assert(B <= 32768, "squeeze: the top limb must stay below 2^28");
+    Fq<AS, B> r;
+    int32_t hi = 0;
+#pragma unroll
+    for (int k = 0; k < LN - 1; k++) {
+        const int32_t h = x.v[k] >> 28;
+        r.v[k] = (x.v[k] & LM) + hi;
+        hi = h;
+    }
+    r.v[LN - 1] = x.v[LN - 1] + hi;
+    return r;
+}
+template <int A, int B>
+DEV Fq<A, B> sel(bool c, const Fq<A, B>& x, const Fq<A, B>& y) {
+    Fq<A, B> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.v[k] = c ? x.v[k] : y.v[k];
+    return r;
+}
+
+// ---------------------------------------------------------------- pair-lane Fp2
+template <int A, int B>
+struct F2 {
+    static constexpr int AV = A, BV = B;
+    Fq<A, B> c;  // this lane's half: real part on even lanes, imaginary part on odd lanes
+};
+template <int A2, int B2, int A, int B>
+DEV F2<A2, B2> fit(const F2<A, B>& x) { return {fit<A2, B2>(x.c)}; }
+
+template <int A1, int B1, int A2, int B2>
+DEV F2<A1 + A2, B1 + B2> add(const F2<A1, B1>& x, const F2<A2, B2>& y) { return {add(x.c, y.c)}; }
+template <int A1, int B1, int A2, int B2>
+DEV F2<A1 + A2, B1 + B2> sub(const F2<A1, B1>& x, const F2<A2, B2>& y) { return {sub(x.c, y.c)}; }
+template <int A, int B>
+DEV F2<A, B> neg(const F2<A, B>& x) { return {neg(x.c)}; }
+template <int K, int A, int B>
+DEV F2<K * A, K * B> smul(const F2<A, B>& x) { return {smul<K>(x.c)}; }
+template <int A, int B>
+DEV F2<2 * A, 2 * B> dbl(const F2<A, B>& x) { return {add(x.c, x.c)}; }
+template <int A, int B>
+DEV F2<AS, B> squeeze(const F2<A, B>& x) { return {squeeze(x.c)}; }
+
+// x (1 + i) = (a - b) + (a + b) i: own + (im ? partner : -partner)
+template <int A, int B>
+DEV F2<2 * A, 2 * B> xi(const F2<A, B>& x) {
+    const bool im = half_id() != 0;
+    F2<2 * A, 2 * B> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) {
+        const int32_t s = swp(x.c.v[k]);
+        r.c.v[k] = x.c.v[k] + (im ? s : -s);
+    }
+    return r;
+}
+// conj: the imaginary half negated
+template <int A, int B>
+DEV F2<A, B> conj(const F2<A, B>& x) {
+    const bool im = half_id() != 0;
+    F2<A, B> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.c.v[k] = im ? -x.c.v[k] : x.c.v[k];
+    return r;
+}
+
+template <int A1, int B1, int A2, int B2>
+DEV F2<AN, bprod(2LL * B1 * B2)> mul(const F2<A1, B1>& x, const F2<A2, B2>& y) {
+    static_assert(2LL * A1 * A2 <= AMAX, "f2 mul: limb bound");
+    return {fq<bprod(2LL * B1 * B2)>(lz_f2_mul_c(w14(x.c), w14(y.c)))};
+}
+template <int A, int B>
+DEV F2<AN, bprod(4LL * B * B)> sqr(const F2<A, B>& x) {
+    static_assert(4LL * A * A <= AMAX, "f2 sqr: limb bound");
+    return {fq<bprod(4LL * B * B)>(lz_f2_sqr_c(w14(x.c)))};
+}
+// Fp2 x Fp (k held on both lanes)
+template <int A1, int B1, int A2, int B2>
+DEV F2<AN, bprod((long long)B1 * B2)> mul_fp(const F2<A1, B1>& x, const Fq<A2, B2>& k) {
+    static_assert((long long)A1 * A2 <= AMAX, "mul_fp: limb bound");
+    return {fq<bprod((long long)B1 * B2)>(lz_mul_c(w14(x.c), w14(k)))};
+}
+template <int A1, int B1, int A2, int B2>
+DEV Fq<AN, bprod((long long)B1 * B2)> mul(const Fq<A1, B1>& x, const Fq<A2, B2>& y) {
+    static_assert((long long)A1 * A2 <= AMAX, "fp mul: limb bound");
+    return fq<bprod((long long)B1 * B2)>(lz_mul_c(w14(x), w14(y)));
+}
+
+// pair-uniform predicates (both halves agree)
+DEV bool pair_all(bool own) { return pl::pair_all(own); }
+template <int A, int B>
+DEV bool is_zero(const F2<A, B>& x) { return pair_all(fp_is_zero(canon(x.c))); }
+template <int A1, int B1, int A2, int B2>
+DEV bool eq(const F2<A1, B1>& x, const F2<A2, B2>& y) { return pair_all(fp_eq(canon(x.c), canon(y.c))); }
+
+// storage form (12 x 32 canonical, R = 2^406) <-> R' form
+DEV auto in_r(const Fp& x) {
+    constexpr int32_t C[LN] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x4000};  // 2^378
+    return mul(from_fp(x), fq_const(C));
+}
+template <int A, int B>
+DEV Fp out_r(const Fq<A, B>& x) {
+    constexpr int32_t C[LN] = {LZ_C_OUT_LIMBS};
+    return canon(mul(x, fq_const(C)));
+}
+DEV auto in_r2(const pl::Fp2& x) {
+    const auto c = in_r(x.c);
+    return F2<AN, decltype(c)::BV>{c};
+}
+template <int A, int B>
+DEV pl::Fp2 out_r2(const F2<A, B>& x) { return {out_r(x.c)}; }
+
+// x^-1 (x on both lanes of the pair)
+template <int A, int B>
+DEV auto inv(const Fq<A, B>& x) {
+    constexpr int32_t C[LN] = {LZ_R3_LIMBS};
+    Fp a = canon(x), ai;
+    fp_inv_int(ai, a);  // (x R')^-1
+    return mul(from_fp(ai), fq_const(C));
+}
+// (a + b i)^-1 = conj(x) / (a^2 + b^2)
+template <int A, int B>
+DEV auto inv(const F2<A, B>& x) {
+    static_assert(2LL * A * A <= AMAX, "f2 inv: limb bound");
+    int32_t xs[LN];
+#pragma unroll
+    for (int k = 0; k < LN; k++) xs[k] = swp(x.c.v[k]);
+    const W14 n = lz_mont<2>(x.c.v, x.c.v, xs, xs);  // a^2 + b^2 on both lanes
+    const auto ni = inv(fq<bprod(2LL * B * B)>(n));
+    const auto r = mul(x.c, ni);
+    return conj(F2<AN, decltype(r)::BV>{r});
+}
+
+DEV F2<AN, BC> f2_zero() {
+    F2<AN, BC> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.c.v[k] = 0;
+    return r;
+}
+DEV F2<AN, BC> f2_one() {
+    constexpr int32_t O[LN] = {LZ_ONE_LIMBS};
+    const bool im = half_id() != 0;
+    F2<AN, BC> r;
+#pragma unroll
+    for (int k = 0; k < LN; k++) r.c.v[k] = im ? 0 : O[k];
+    return r;
+}
+
+}  // namespace lz
+}  // namespace cc

@@ -1,0 +1,307 @@
+// Miller-loop kernels for gfx950 on the lazy radix-2^28 field (lazy.h, tower_lz.h) — the
+// shared-squaring 2-pair loop of ate_2_pairing (ps_sig `ate_2_pairing` -> AMCL `pair::ate2`,
+// reference src/lib.rs:13).  Replaces miller_pl.hip (same launchers, same SoA
+// inputs and outputs); one credential per PAIR of adjacent lanes as there.
+//
+//   SigG2: pair 0 = (sigma_1, pr) with pr in Jacobian-evaluation form (XZ, Y, Z^3);
+//          pair 1 = (-sigma_2, g~): g~ affine constant, or per lane (lane2: the RLC fold's
+//          pseudo-credentials, fold.hip).
+//   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2).
+//   RLC mode runs pair 0 alone (NP = 1).
+//
+// Representation boundary: the prep SoA holds canonical 12 x 32 values in R = 2^406 form.  The twist
+// points are moved to R' form once (in_r: T's start and the addition steps' Q).  The G1 evaluation
+// coordinates are NOT converted: multiplied in R form straight into the R'-form line, every
+// coefficient of a line comes out scaled by the same 2^14 (R / R'), and affine points use the constant
+// R mod p as their Z; a line scaled by an Fp constant leaves the pairing unchanged (the final
+// exponentiation's easy part kills Fp^*), as does the doubling step's 4x scale of T (lines are
+// homogeneous of degree 2 in T).  The Miller value leaves in R form, canonical (out_r), for k_fexp.
+#ifndef CC_MILLER_SIG
+#define CC_MILLER_SIG 2
+#endif
+#ifdef CC_HOT_INLINE  // build option (Makefile HOT_INLINE=1): inline every Fp multiplication
+#define CC_FP_INLINE 1
+#endif
+#include "codec.h"
+#include "curve_pl.h"
+#include "tower_lz.h"
+
+namespace cc {
+namespace lz {
+namespace {
+
+constexpr int MB = 256;  // lanes per block
+// loop-carried value bounds (units of p/16; lazy.h): the step functions fit their results into
+// these, so a bound that does not hold is a compile error
+// f: after a line multiplication (BF), after the squaring (BS)
+constexpr int BX = 128, BY = 1024, BZ = 128, BF = 512, BS = 2048, BL = 2048;
+using Tw = G2P<BX, BY, BZ>;
+using F12S = F12<AS, BF>;
+using F2L = F2<AS, BL>;
+using LineS = Line<F2L, F2L, F2L>;
+constexpr int TW = 3 * LN;  // words of a parked Tw (this lane's halves)
+
+template <class L>
+DEV LineS fit_line(const L& l) { return {fit<AS, BL>(l.l0), fit<AS, BL>(l.l2), fit<AS, BL>(l.l3)}; }
+
+// where a pair's G1 evaluation point lives: word (slot * NL + limb) * n + i * is
+struct PSrc {
+    const uint32_t* p;
+    size_t n, is;
+    bool jac;  // (XZ, Y, Z^3) form; affine (x, y) [z = 1] otherwise
+};
+
+DEV Fq<AN, BC> ld_Pc(const PSrc& s, int slot, size_t i) {
+    Fp x;
+#pragma unroll
+    for (int k = 0; k < NL; k++) x.v[k] = s.p[(size_t)(slot * NL + k) * s.n + i * s.is];
+    return from_fp(x);
+}
+
+// f * line(P), the line scaled by 2^14 (header).  A skipped pair (identity argument: e(O, Q) =
+// e(P, O) = 1) multiplies by the unit line (1, 0, 0) instead of returning early: the product's type
+// bound then holds on every path (f's value bound only shrinks through a multiplication), and the
+// lanes of a mixed wave would wait for the others anyway.
+template <int B>
+DEV F12S eval_mul(const F12<AS, B>& f, const LineS& ln, const PSrc& ps, size_t i, bool skip) {
+    constexpr int32_t ONE_R[LN] = {LZ_C_OUT_LIMBS};
+    const auto a0 = mul_fpr(ln.l0, ps.jac ? ld_Pc(ps, 2, i) : fq_const(ONE_R));
+    const auto a2 = mul_fpr(ln.l2, ld_Pc(ps, 0, i));
+    const auto a3 = mul_fpr(ln.l3, ld_Pc(ps, 1, i));
+    using L = decltype(a0);
+    const L one = fit<AN, L::BV>(f2_one()), zero = fit<AN, L::BV>(f2_zero());
+    return fit<AS, BF>(f12_mul_line(f, L{sel(skip, one.c, a0.c)}, L{sel(skip, zero.c, fit<AN, L::BV>(a2).c)},
+                                    L{sel(skip, zero.c, fit<AN, L::BV>(a3).c)}));
+}
+
+// Two-pair loop: both twist points are parked in LDS while f is multiplied by their lines (the values
+// live across the out-of-line multiplications must fit the callee-saved registers; f, a line and a T
+// (84 + 42 + 42 words a lane) do not).  A T is packed for it: limbs carry-normalised to [0, 2^28),
+// 13 limbs in 12 words + the signed top limb = 39 words, so both T's of the 512 lanes a CU holds fit
+// its 160 KiB (78 x 4 B x 512).
+constexpr int PW = 13;      // packed words per Fq
+constexpr int TP = 3 * PW;  // packed words per T
+template <int A, int B>
+DEV void pack_fq(int32_t (*lds)[MB], int row, const Fq<A, B>& x) {
+    int32_t u[LN], c = 0;
+#pragma unroll
+    for (int k = 0; k < LN - 1; k++) {
+        const int32_t t = x.v[k] + c;
+        u[k] = t & LM;
+        c = t >> 28;
+    }
+    u[LN - 1] = x.v[LN - 1] + c;
+#pragma unroll
+    for (int w = 0; w < PW - 1; w++) {
+        const int bit = 32 * w, k = bit / 28, s = bit % 28;
+        uint32_t v = (uint32_t)u[k] >> s;
+        if (k + 1 < LN - 1) v |= (uint32_t)u[k + 1] << (28 - s);
+        if (s > 24 && k + 2 < LN - 1) v |= (uint32_t)u[k + 2] << (56 - s);
+        lds[row + w][threadIdx.x] = (int32_t)v;
+    }
+    lds[row + PW - 1][threadIdx.x] = u[LN - 1];
+}
+template <int B>
+DEV Fq<AN, B> unpack_fq(int32_t (*lds)[MB], int row) {
+    uint32_t w[PW];
+#pragma unroll
+    for (int j = 0; j < PW; j++) w[j] = (uint32_t)lds[row + j][threadIdx.x];
+    Fq<AN, B> r;
+    r.v[0] = (int32_t)(w[0] & (uint32_t)LM);
+#pragma unroll
+    for (int k = 1; k < LN - 1; k++) {
+        const int bit = 28 * k, j = bit >> 5, s = bit & 31;
+        r.v[k] = (int32_t)((s ? __builtin_amdgcn_alignbit(w[j + 1], w[j], s) : w[j]) & (uint32_t)LM);
+    }
+    r.v[LN - 1] = (int32_t)w[PW - 1];
+    return r;
+}
+DEV void park(int32_t (*lds)[MB], int k, const Tw& T) {
+    pack_fq(lds, TP * k, T.x.c);
+    pack_fq(lds, TP * k + PW, T.y.c);
+    pack_fq(lds, TP * k + 2 * PW, T.z.c);
+}
+DEV Tw unpark(int32_t (*lds)[MB], int k) {
+    return {fit<AS, BX>(F2<AN, BX>{unpack_fq<BX>(lds, TP * k)}), fit<AS, BY>(F2<AN, BY>{unpack_fq<BY>(lds, TP * k + PW)}),
+            fit<AS, BZ>(F2<AN, BZ>{unpack_fq<BZ>(lds, TP * k + 2 * PW)})};
+}
+
+// a precomputed g~ line (SigG1): AoS l0 | l2 | l3, (a, b) halves of 12 words, R form
+DEV LineS ld_line(const uint32_t* L) {
+    const int h = (int)half_id();
+    Fp c[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int k = 0; k < NL; k++) c[j].v[k] = L[24 * j + NL * h + k];
+    return {fit<AS, BL>(F2<AN, BC>{from_fp(c[0])}), fit<AS, BL>(F2<AN, BC>{from_fp(c[1])}),
+            fit<AS, BL>(F2<AN, BC>{from_fp(c[2])})};
+}
+
+// an affine twist point from the prep SoA, in R' form
+DEV void ld_q(F2<AN, 17>& x, F2<AN, 17>& y, const Soa& S, int slot, size_t i) {
+    pl::Fp2 a, b;
+    pl::ld_f2(a, S, slot, i);
+    pl::ld_f2(b, S, slot + 2, i);
+    x = in_r2(a);
+    y = in_r2(b);
+}
+DEV Tw t_from(const F2<AN, 17>& x, const F2<AN, 17>& y) {
+    return {fit<AS, BX>(x), fit<AS, BY>(y), fit<AS, BZ>(f2_one())};
+}
+
+// g's value came from eval_mul (F12S), stored in a wider variable: back to F12S
+template <int B2, int B>
+DEV F12<AS, B2> narrow_to(const F12<AS, B>& g) {
+    static_assert(B2 == BF, "narrow_to: only for eval_mul results");
+    F12<AS, B2> r;
+    static_assert(sizeof(r) == sizeof(g), "same layout");
+    __builtin_memcpy(&r, &g, sizeof(r));
+    return r;
+}
+
+struct StepState {
+    F12S f;
+    Tw T;
+};
+
+// addition step of one pair: T <- T + Q, f *= line; or (line != nullptr) f *= precomputed line
+static __device__ __noinline__ void miller_add(StepState* st, const uint32_t* prep, size_t n, int qslot, size_t i,
+                                               const uint32_t* line, PSrc ps, bool skip) {
+    F12S f = st->f;
+    LineS ln;
+    if (line) {
+        ln = ld_line(line);
+    } else {
+        Tw T = st->T;
+        F2<AN, 17> qx, qy;
+        ld_q(qx, qy, Soa{const_cast<uint32_t*>(prep), n}, qslot, i);
+        ln = fit_line(line_add(T, qx, qy));
+        st->T = T;
+    }
+    st->f = eval_mul(f, ln, ps, i, skip);
+}
+
+}  // namespace
+
+// prep: SoA slots of soa.h; flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 pr = O, bit4 pair-1 P = O
+// cst: SigG2 -> g~ affine (24 words, used when !kLane2); SigG1 -> g~ lines (68 x 72 words)
+// NP = 1: pair 0 only (RLC mode).  The Miller value of credential i goes to fout as SoA element
+// foff + i of stride fstride.  qcheck (NP = 1, SigG2): pair 0's Q (sigma_1) gets the G2 subgroup test
+// from the loop's own T (curve_pl.h miller_t_in_subgroup); a failure sets *qcheck.
+template <int SIG, bool kLane2, int NP>
+__global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __restrict__ prep,
+                                               const uint32_t* __restrict__ flags, const uint32_t* __restrict__ cst,
+                                               uint32_t* __restrict__ fout, size_t fstride, size_t foff,
+                                               uint32_t* __restrict__ qcheck) {
+    __shared__ int32_t lds[NP == 2 ? 2 * TP : 1][MB];
+    const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
+    if (i >= n) return;  // pair-uniform
+    constexpr bool kSigG2 = SIG == 2;
+    const uint32_t fl = flags[i];
+    const bool skip0 = (fl & 5u) != 0, skip1 = (fl & 18u) != 0;
+    PSrc ps0, ps1;
+    if (kSigG2) {
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, true};
+        ps1 = kLane2 ? PSrc{prep + (size_t)S_P2 * NL * n, n, 1, true} : PSrc{cst, 1, 0, false};
+    } else {
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, false};
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kLane2};
+    }
+    const Soa S{const_cast<uint32_t*>(prep), n};
+    // NP = 1: T stays in registers; NP = 2: both T's parked in LDS between their uses
+    Tw T;
+    {
+        F2<AN, 17> qx, qy;
+        if (kSigG2 && NP == 2) {  // pair 1's T = -sigma_2
+            ld_q(qx, qy, S, S_Q2, i);
+            park(lds, 1, t_from(qx, qy));
+        }
+        ld_q(qx, qy, S, S_Q1, i);
+        T = t_from(qx, qy);
+        if (NP == 2) park(lds, 0, T);
+    }
+    F12S f = fit<AS, BF>(f12_one());
+    const uint32_t* gl = cst;  // SigG1: next precomputed g~ line
+#pragma unroll 1
+    for (int b = 62; b >= 0; b--) {
+        // g: the squared f, then f times each pair's line; one eval_mul instantiation serves both pairs
+        F12<AS, BS> g = b != 62 ? fit<AS, BS>(f12_sqr(f)) : fit<AS, BS>(f);
+#pragma unroll 1
+        for (int k = 0; k < NP; k++) {
+            LineS ln;
+            if (!kSigG2 && k == 1) {
+                ln = ld_line(gl);
+                gl += 72;
+            } else {
+                if (NP == 2) T = unpark(lds, k);
+                ln = fit_line(line_dbl(T));
+                if (NP == 2) park(lds, k, T);
+            }
+            g = fit<AS, BS>(eval_mul(g, ln, k ? ps1 : ps0, i, k ? skip1 : skip0));
+        }
+        // NP >= 1 passes ran, so g holds an eval_mul result, whose type bound is BF
+        f = narrow_to<BF>(g);
+        if ((X_ABS >> b) & 1ull) {
+#pragma unroll 1
+            for (int k = 0; k < NP; k++) {
+                const bool const_line = !kSigG2 && k == 1;
+                StepState st;
+                st.f = f;
+                if (!const_line) st.T = NP == 2 ? unpark(lds, k) : T;
+                miller_add(&st, prep, n, k ? S_Q2 : S_Q1, i, const_line ? gl : nullptr, k ? ps1 : ps0,
+                           k ? skip1 : skip0);
+                if (const_line) gl += 72;
+                else if (NP == 2) park(lds, k, st.T);
+                else T = st.T;
+                f = st.f;
+            }
+        }
+    }
+    if (NP == 1 && kSigG2 && qcheck && !skip0) {
+        pl::G2Proj Tp;
+        Tp.x = out_r2(T.x);
+        Tp.y = out_r2(T.y);
+        Tp.z = out_r2(T.z);
+        Aff<pl::Fp2> q;
+        pl::ld_f2(q.x, S, S_Q1, i);
+        pl::ld_f2(q.y, S, S_Q1 + 2, i);
+        if (!pl::miller_t_in_subgroup(Tp, q) && !half_id()) atomicOr(qcheck, 1u);
+    }
+    f = f12_conj(f);
+    const Soa O{fout, fstride};
+    const F2<AS, BF>* v = reinterpret_cast<const F2<AS, BF>*>(&f);
+#pragma unroll
+    for (int k = 0; k < 6; k++) st_fp(O, 2 * k + (int)half_id(), foff + i, out_r(v[k].c));
+}
+
+}  // namespace lz
+}  // namespace cc
+
+#if CC_MILLER_SIG == 2
+#define CC_MILLER_LAUNCH cck_miller_lz_g2
+#else
+#define CC_MILLER_LAUNCH cck_miller_lz_g1
+#endif
+
+// lane2: per-lane second-pair P; np: pairs per credential (1 or 2); the Miller values go to SoA
+// elements [foff, foff + n) of stride fstride (>= foff + n); d_qcheck (np = 1, SigG2, or null): the
+// sigma_1 subgroup test from the loop's T
+extern "C" int CC_MILLER_LAUNCH(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+                                const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff,
+                                uint32_t* d_qcheck, hipStream_t st) {
+    if (!n) return 0;
+    if (fstride < foff + n || (np != 1 && np != 2)) return -1;
+    constexpr int MB = cc::lz::MB;
+    dim3 g((unsigned)((2 * n + MB - 1) / MB)), b(MB);
+    if (np == 1)
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, false, 1>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+                           fstride, foff, d_qcheck);
+    else if (lane2)
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, true, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+                           fstride, foff, d_qcheck);
+    else
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, false, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+                           fstride, foff, d_qcheck);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
