@@ -454,8 +454,9 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
 
 static cc_status ensure_work(cc_ctx* c, size_t n) {
     size_t words = n * 12;  // one Fp slot
+    // fexp scratch: 84 lazy Fp slots of 14 words (fexp_lz.hip) >= 72 slots of 12 (fexp_pl.hip)
     if (c->prep.ensure(words * 4 * PREP_SLOTS) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
-        c->scratch.ensure(words * 4 * 72) || c->verdicts.ensure(n))
+        c->scratch.ensure(n * 14 * 84 * 4) || c->verdicts.ensure(n))
         return CC_ERR_HIP;
     return CC_OK;
 }

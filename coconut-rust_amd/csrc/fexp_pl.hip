@@ -8,6 +8,8 @@
 #ifdef CC_HOT_INLINE  // build option (Makefile HOT_INLINE=1): inline every Fp multiplication
 #define CC_FP_INLINE 1
 #endif
+#include <cstdlib>
+#include <cstring>
 #include "codec.h"
 #include "tower_pl.h"
 
@@ -501,9 +503,19 @@ __global__ __launch_bounds__(64, 1) void k_fexp1(uint32_t* __restrict__ fbuf, ui
 
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
+// the lazy-field kernel (fexp_lz.hip), same arguments; its scratch is 84 x 14 words per element
+extern "C" int cck_fexp_lz(size_t n, const uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags,
+                           uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st);
+
 extern "C" int cck_fexp_pl(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                         uint8_t* d_gt, hipStream_t st) {
     if (!n) return 0;
+    // batches: the lazy-field kernel unless CC_FEXP=pl (A/B runs)
+    static const bool lz = [] {
+        const char* e = getenv("CC_FEXP");
+        return !(e && !strcmp(e, "pl"));
+    }();
+    if (n > 1 && lz) return cck_fexp_lz(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st);
     if (n == 1)  // latency-bound: the wide one-wave form
         hipLaunchKernelGGL(cc::pl::k_fexp1, dim3(1), dim3(64), 0, st, d_f, d_scratch, d_flags, d_verdicts, d_gt);
     else

@@ -363,6 +363,31 @@ DEV Fq<AS, B> squeeze(const Fq<A, B>& x) {
     r.v[LN - 1] = x.v[LN - 1] + hi;
     return r;
 }
+// value reduction: x - q p with q = round(V / p) taken from the top limb (V / 2^364 / (p / 2^364); the
+// lower limbs move V / p by < A 2^-24.7 and the float estimate by < 2^-11), carried limb by limb into
+// normalised limbs: |result| < 0.5002 p (B = 9; tests/test_lazy_algebra.py).  For values that only grow through additions (the
+// cyclotomic squarings' 3u +- 2v): ~70 simple ops against 392 mads for a product by one.
+constexpr float LZ_INV_P13 = 1.0f / 106513.12f;  // 2^364 / p
+template <int A, int B>
+DEV Fq<AN, 9> reduce(const Fq<A, B>& x) {
+    static_assert(B <= 32768, "reduce: |q| must stay small");
+    const int32_t q = (int32_t)__builtin_rintf((float)x.v[LN - 1] * LZ_INV_P13);
+    Fq<AN, 9> r;
+    int64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < LN - 1; k++) {
+        // one v_mad_i64_i32 into the running carry: the opaque step keeps the compiler from hoisting
+        // the 13 products as parallel 64-bit temporaries (they spilled in the squaring loop)
+        c += x.v[k];
+        asm volatile("" : "+v"(c));
+        c += (int64_t)q * -lz_p(k);
+        r.v[k] = (int32_t)c & LM;
+        c >>= 28;
+    }
+    r.v[LN - 1] = x.v[LN - 1] - q * lz_p(LN - 1) + (int32_t)c;
+    return r;
+}
+
 template <int A, int B>
 DEV Fq<A, B> sel(bool c, const Fq<A, B>& x, const Fq<A, B>& y) {
     Fq<A, B> r;
@@ -392,6 +417,8 @@ template <int A, int B>
 DEV F2<2 * A, 2 * B> dbl(const F2<A, B>& x) { return {add(x.c, x.c)}; }
 template <int A, int B>
 DEV F2<AS, B> squeeze(const F2<A, B>& x) { return {squeeze(x.c)}; }
+template <int A, int B>
+DEV F2<AN, 9> reduce(const F2<A, B>& x) { return {reduce(x.c)}; }
 
 // x (1 + i) = (a - b) + (a + b) i: own + (im ? partner : -partner)
 template <int A, int B>
@@ -424,6 +451,25 @@ template <int A, int B>
 DEV F2<AN, bprod(4LL * B * B)> sqr(const F2<A, B>& x) {
     static_assert(4LL * A * A <= AMAX, "f2 sqr: limb bound");
     return {fq<bprod(4LL * B * B)>(lz_f2_sqr_c(w14(x.c)))};
+}
+// a wave-uniform false the compiler cannot see through (field.h cc_opaque_false)
+DEV bool lz_opaque_false() {
+    uint32_t x;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(x));
+    return x != 0;
+}
+// x^2 with the multiplication inlined (its own basic block): for small hot loops whose whole body then
+// runs without call boundaries (no values saved around calls; fexp_lz.hip's compressed squarings)
+template <int A, int B>
+DEV F2<AN, bprod(4LL * B * B)> sqr_in(const F2<A, B>& x) {
+    static_assert(4LL * A * A <= AMAX, "f2 sqr: limb bound");
+    W14 r, a = w14(x.c);
+    do {
+#pragma unroll
+        for (int k = 0; k < LN; k++) asm volatile("" : "+v"(a.v[k]));
+        r = lz_f2_sqr_v(a);
+    } while (lz_opaque_false());
+    return {fq<bprod(4LL * B * B)>(r)};
 }
 // Fp2 x Fp (k held on both lanes)
 template <int A1, int B1, int A2, int B2>

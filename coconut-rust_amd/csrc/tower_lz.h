@@ -32,6 +32,11 @@ DEV auto sqrr(const F2<A, B>& x) {
     if constexpr (4LL * A * A <= AMAX) return sqr(x);
     else return sqr(squeeze(x));
 }
+template <int A, int B>
+DEV auto sqrr_in(const F2<A, B>& x) {
+    if constexpr (4LL * A * A <= AMAX) return sqr_in(x);
+    else return sqr_in(squeeze(x));
+}
 template <int A1, int B1, int A2, int B2>
 DEV auto mul_fpr(const F2<A1, B1>& x, const Fq<A2, B2>& k) {
     if constexpr ((long long)A1 * A2 <= AMAX) return mul_fp(x, k);

@@ -142,3 +142,29 @@ def test_canon_range():
     for _ in range(200):
         x = rand_lz(1500, 4000, rng, extreme=False)
         assert canon(x) == value(x) % P
+
+
+def reduce(v):
+    """lazy.h reduce: q = round(top limb * (2^364 / p)) in float32, V - q p carried into normalised limbs."""
+    import numpy as np
+    q = int(np.rint(np.float32(v[LN - 1]) * (np.float32(1.0) / np.float32(106513.12))))
+    r, c = [], 0
+    for k in range(LN - 1):
+        c += v[k] - q * PL[k]
+        r.append(c & M28)
+        c >>= 28
+    r.append(v[LN - 1] - q * PL[LN - 1] + c)
+    return r
+
+
+def test_reduce_bound():
+    """Any input the types allow (A <= 2047, |V| < 2048 p) comes back below 0.5625 p (B = 9)."""
+    rng = random.Random(13)
+    worst = 0.0
+    for _ in range(3000):
+        x = rand_lz(2047, 32768, rng, extreme=rng.random() < 0.5)
+        r = reduce(x)
+        assert value(r) % P == value(x) % P
+        assert all(0 <= t <= M28 for t in r[:-1]) and -(1 << 31) <= r[-1] < (1 << 31)
+        worst = max(worst, abs(value(r)) / P)
+    assert worst < 9 / 16
