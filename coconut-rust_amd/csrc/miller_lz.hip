@@ -48,8 +48,7 @@ DEV LineS fit_line(const L& l) { return {fit<AS, BL>(l.l0), fit<AS, BL>(l.l2), f
 struct PSrc {
     const uint32_t* p;
     size_t n, is;
-    bool jac;          // (XZ, Y, Z^3) form; affine (x, y) [z = 1] otherwise
-    const int32_t* cz;  // a constant affine point already in R' form (LDS, x then y), or null
+    bool jac;  // (XZ, Y, Z^3) form; affine (x, y) [z = 1] otherwise
 };
 
 DEV Fq<AN, BC> ld_Pc(const PSrc& s, int slot, size_t i) {
@@ -66,26 +65,13 @@ DEV Fq<AN, BC> ld_Pc(const PSrc& s, int slot, size_t i) {
 template <int B>
 DEV F12S eval_mul(const F12<AS, B>& f, const LineS& ln, const PSrc& ps, size_t i, bool skip) {
     constexpr int32_t ONE_R[LN] = {LZ_C_OUT_LIMBS};
-    using L = decltype(mul_fpr(ln.l0, fq_const(ONE_R)));
-    L a0, a2, a3;
-    if (ps.cz) {  // constant affine P in R' form: the line unscaled, l0 needs no product (reduce only)
-        Fq<AN, BC> px, py;
-#pragma unroll
-        for (int k = 0; k < LN; k++) {
-            px.v[k] = ps.cz[k];
-            py.v[k] = ps.cz[LN + k];
-        }
-        a0 = fit<AN, L::BV>(reduce(ln.l0));
-        a2 = fit<AN, L::BV>(mul_fpr(ln.l2, px));
-        a3 = fit<AN, L::BV>(mul_fpr(ln.l3, py));
-    } else {
-        a0 = mul_fpr(ln.l0, ps.jac ? ld_Pc(ps, 2, i) : fq_const(ONE_R));
-        a2 = fit<AN, L::BV>(mul_fpr(ln.l2, ld_Pc(ps, 0, i)));
-        a3 = fit<AN, L::BV>(mul_fpr(ln.l3, ld_Pc(ps, 1, i)));
-    }
+    const auto a0 = mul_fpr(ln.l0, ps.jac ? ld_Pc(ps, 2, i) : fq_const(ONE_R));
+    const auto a2 = mul_fpr(ln.l2, ld_Pc(ps, 0, i));
+    const auto a3 = mul_fpr(ln.l3, ld_Pc(ps, 1, i));
+    using L = decltype(a0);
     const L one = fit<AN, L::BV>(f2_one()), zero = fit<AN, L::BV>(f2_zero());
-    return fit<AS, BF>(f12_mul_line(f, L{sel(skip, one.c, a0.c)}, L{sel(skip, zero.c, a2.c)},
-                                    L{sel(skip, zero.c, a3.c)}));
+    return fit<AS, BF>(f12_mul_line(f, L{sel(skip, one.c, a0.c)}, L{sel(skip, zero.c, fit<AN, L::BV>(a2).c)},
+                                    L{sel(skip, zero.c, fit<AN, L::BV>(a3).c)}));
 }
 
 // Two-pair loop: both twist points are parked in LDS while f is multiplied by their lines (the values
@@ -209,33 +195,18 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
                                                uint32_t* __restrict__ fout, size_t fstride, size_t foff,
                                                uint32_t* __restrict__ qcheck) {
     __shared__ int32_t lds[NP == 2 ? 2 * TP : 1][MB];
-    constexpr bool kSigG2 = SIG == 2;
-    // SigG2's constant g~ (pair 1 without lane2): moved to R' form once per block (lanes 0, 1: x, y)
-    constexpr bool kConstP = kSigG2 && !kLane2 && NP == 2;
-    __shared__ int32_t gz[kConstP ? 2 * LN : 1];
-    if (kConstP) {
-        if (threadIdx.x < 2) {
-            Fp c;
-#pragma unroll
-            for (int k = 0; k < NL; k++) c.v[k] = cst[NL * threadIdx.x + k];
-            const auto z = in_r(c);
-#pragma unroll
-            for (int k = 0; k < LN; k++) gz[LN * threadIdx.x + k] = z.v[k];
-        }
-        __syncthreads();
-    }
     const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
     if (i >= n) return;  // pair-uniform
+    constexpr bool kSigG2 = SIG == 2;
     const uint32_t fl = flags[i];
     const bool skip0 = (fl & 5u) != 0, skip1 = (fl & 18u) != 0;
     PSrc ps0, ps1;
     if (kSigG2) {
-        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, true, nullptr};
-        ps1 = kLane2 ? PSrc{prep + (size_t)S_P2 * NL * n, n, 1, true, nullptr}
-                     : PSrc{cst, 1, 0, false, kConstP ? &gz[0] : nullptr};
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, true};
+        ps1 = kLane2 ? PSrc{prep + (size_t)S_P2 * NL * n, n, 1, true} : PSrc{cst, 1, 0, false};
     } else {
-        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, false, nullptr};
-        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kLane2, nullptr};
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, false};
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kLane2};
     }
     const Soa S{const_cast<uint32_t*>(prep), n};
     // NP = 1: T stays in registers; NP = 2: both T's parked in LDS between their uses

@@ -3,7 +3,7 @@
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
-OUT=$R/gpurun_out/pmc
+OUT=${PMC_OUT:-$R/gpurun_out/pmc}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
