@@ -373,8 +373,10 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
 // Prep layout (soa.h: Q1 0..3 | Q2 4..7 | P1 8..10 | P2 11..12) and flag bits as kernels.hip,
 // plus flag bit3 = Schnorr check failed.
 
-template <class FS_, class FO>  // FS_: SignatureGroup field, FO: OtherGroup field
-__global__ __launch_bounds__(256) void k_prep_pok(size_t n, int q, int r, const uint8_t* __restrict__ s1b,
+// FS_: SignatureGroup field, FO: OtherGroup field; MINB blocks a CU (2 for SigG2: its G1 Schnorr MSM
+// fits 2 waves/SIMD, ~10 registers over the bound otherwise ran it at one wave/SIMD)
+template <class FS_, class FO, int MINB>
+__global__ __launch_bounds__(256, MINB) void k_prep_pok(size_t n, int q, int r, const uint8_t* __restrict__ s1b,
                                                   const uint8_t* __restrict__ s2b, const uint8_t* __restrict__ Jb,
                                                   const uint8_t* __restrict__ Tb, const uint8_t* __restrict__ resp,
                                                   const uint8_t* __restrict__ chal,
@@ -553,10 +555,10 @@ int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const ui
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
     if (mode == 0)
-        hipLaunchKernelGGL((k_prep_pok<Fp2, Fp>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
+        hipLaunchKernelGGL((k_prep_pok<Fp2, Fp, 2>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
                            d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags);
     else
-        hipLaunchKernelGGL((k_prep_pok<Fp, Fp2>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
+        hipLaunchKernelGGL((k_prep_pok<Fp, Fp2, 1>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
                            d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
