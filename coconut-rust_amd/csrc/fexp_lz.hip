@@ -77,7 +77,7 @@ static __device__ __noinline__ void zx_in(const uint32_t* fbuf, size_t n, Zs dst
 }
 static __device__ __noinline__ void zx_inv(Zs src, Zs dst, size_t i) { st12(dst, i, rest(f12_inv(ld12(src, i)))); }
 // dst <- op_a(a) * op_b(b)
-static __device__ __noinline__ void zx_mul(Zs a, int opa, Zs b, int opb, Zs dst, size_t i) {
+DEV void zx_mul(Zs a, int opa, Zs b, int opb, Zs dst, size_t i) {
     const FR x = zapply(ld12(a, i), opa);
     const FR y = zapply(ld12(b, i), opb);
     st12(dst, i, rest(f12_mul(x, y)));
@@ -148,7 +148,7 @@ DEV Z4 ld_z4(const Zs& K, int base, size_t i) {
 
 // dst <- src^x (fexp_pl.hip fx_pow_x): 57 compressed squarings with snapshots g^(2^16), g^(2^48) in K,
 // one inversion for the three decompressions, 6 Granger-Scott squarings, 5 Fp12 products, conj.
-static __device__ __noinline__ void zx_pow_x(Zs src, Zs dst, Zs K, size_t i) {
+DEV void zx_pow_x(Zs src, Zs dst, Zs K, size_t i) {
     Z4 c{ld_z(src, 4, i), ld_z(src, 6, i), ld_z(src, 8, i), ld_z(src, 10, i)};
     // three loops, the snapshot stores between them (a store inside the loop body gets its address
     // arithmetic spilled and reloaded at every iteration)
@@ -218,6 +218,29 @@ DEV void zexp_out(size_t i, const FR& res, const uint32_t* flags, uint8_t* verdi
     }
 }
 
+// the chain after the easy part's inversion (fexp_pl.hip fexp_chain); regions F 0, T 1, A 2, S 3, R 4
+struct ZStep {
+    uint8_t kind, a, opa, b, opb, d;  // kind 0: d = op_a(a) op_b(b); 1: d = a^x; 2: d = a^3
+};
+__constant__ static const ZStep kChain[16] = {
+    {0, 0, OP_CONJ, 1, OP_ID, 0},    // f^(p^6 - 1)
+    {0, 0, OP_FROB2, 0, OP_ID, 0},   // ^(p^2 + 1)
+    {2, 0, 0, 0, 0, 4},              // res = f^3
+    {1, 0, 0, 0, 0, 1},              // t = f^x
+    {0, 1, OP_ID, 0, OP_CONJ, 1},    // t = f^(x-1)
+    {1, 1, 0, 0, 0, 2},              // a = t^x
+    {0, 2, OP_ID, 1, OP_CONJ, 2},    // a = f^((x-1)^2)
+    {0, 2, OP_FROB2, 2, OP_CONJ, 3},
+    {0, 3, OP_FROB, 4, OP_ID, 4},    // res *= (a^(p^2) a^-1)^p
+    {1, 2, 0, 0, 0, 1},              // b = a^x
+    {0, 1, OP_FROB2, 1, OP_CONJ, 3},
+    {0, 3, OP_ID, 4, OP_ID, 4},      // res *= b^(p^2) b^-1
+    {1, 1, 0, 0, 0, 2},              // c = b^x
+    {0, 2, OP_FROB, 4, OP_ID, 4},    // res *= c^p
+    {1, 2, 0, 0, 0, 1},              // d = c^x
+    {0, 1, OP_ID, 4, OP_ID, 4},      // res *= d
+};
+
 }  // namespace
 
 // fbuf: Miller output f (12 x 32 SoA, 12 slots); scratch: 84 lazy Fp slots (F, T, A, S, R, K)
@@ -231,22 +254,17 @@ __global__ __launch_bounds__(256, 2) void k_fexp_lz(size_t n, const uint32_t* __
         R{scratch + 48 * sl, n}, K{scratch + 60 * sl, n};
     zx_in(fbuf, n, F, i);
     zx_inv(F, T, i);
-    zx_mul(F, OP_CONJ, T, OP_ID, F, i);   // f^(p^6 - 1)
-    zx_mul(F, OP_FROB2, F, OP_ID, F, i);  // ^(p^2 + 1)
-    zx_cube(F, R, i);                     // res = f^3
-    zx_pow_x(F, T, K, i);
-    zx_mul(T, OP_ID, F, OP_CONJ, T, i);   // t = f^(x-1)
-    zx_pow_x(T, A, K, i);
-    zx_mul(A, OP_ID, T, OP_CONJ, A, i);   // a = f^((x-1)^2)
-    zx_mul(A, OP_FROB2, A, OP_CONJ, S, i);
-    zx_mul(S, OP_FROB, R, OP_ID, R, i);   // res *= (a^(p^2) a^-1)^p
-    zx_pow_x(A, T, K, i);                 // b = a^x
-    zx_mul(T, OP_FROB2, T, OP_CONJ, S, i);
-    zx_mul(S, OP_ID, R, OP_ID, R, i);     // res *= b^(p^2) b^-1
-    zx_pow_x(T, A, K, i);                 // c = b^x
-    zx_mul(A, OP_FROB, R, OP_ID, R, i);   // res *= c^p
-    zx_pow_x(A, T, K, i);                 // d = c^x
-    zx_mul(T, OP_ID, R, OP_ID, R, i);     // res *= d
+    // The rest of the chain as ONE loop over its steps with the product and the pow-by-x inlined once
+    // each: an out-of-line step function saves and restores every callee-saved register it touches
+    // (~330 scratch instructions a call, ~20 calls a lane pair).
+#pragma unroll 1
+    for (int s = 0; s < 16; s++) {
+        const ZStep z = kChain[s];
+        const Zs a{scratch + z.a * 12 * sl, n}, b{scratch + z.b * 12 * sl, n}, d{scratch + z.d * 12 * sl, n};
+        if (z.kind == 0) zx_mul(a, z.opa, b, z.opb, d, i);
+        else if (z.kind == 1) zx_pow_x(a, d, K, i);
+        else zx_cube(a, d, i);
+    }
     zexp_out(i, ld12(R, i), flags, verdicts, gt_out);
 }
 
