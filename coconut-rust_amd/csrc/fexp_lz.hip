@@ -22,6 +22,10 @@ using F2R = F2<AN, 9>;
 using FR = F12<AN, 9>;  // at rest: reduced
 
 template <int A, int B>
+DEV F4<AN, 9> rest4(const F4<A, B>& x) {
+    return {reduce(x.a), reduce(x.b)};
+}
+template <int A, int B>
 DEV FR rest(const F12<A, B>& x) {
     return {{reduce(x.a.a), reduce(x.a.b)}, {reduce(x.b.a), reduce(x.b.b)}, {reduce(x.c.a), reduce(x.c.b)}};
 }
@@ -65,6 +69,38 @@ DEV FR zapply(const FR& x, int op) {
     return x;
 }
 
+// ---------------------------------------------------------------- Fp12 products with one operand in LDS
+// The multiplier waits in LDS, packed (78 words a lane: the 512 lanes a CU holds fill its 160 KiB),
+// and its coefficients are unpacked right before each use: x, the Karatsuba terms and the results
+// are then what lives across the out-of-line products (with both operands in registers every call
+// site spilled to scratch).  The memory clobber forces the re-read at each use.
+constexpr int FB = 256;  // lanes per block
+using Park = int32_t (*)[FB];
+DEV void park12(Park lds, const FR& y) {
+    const F2R* v = reinterpret_cast<const F2R*>(&y);
+#pragma unroll
+    for (int k = 0; k < 6; k++) pack_fq<FB>(lds, PW * k, v[k].c);
+}
+DEV F2R unp(Park lds, int k) {
+    asm volatile("" ::: "memory");
+    return {unpack_fq<FB, 9>(lds, PW * k)};
+}
+DEV F4<AN, 9> unp4(Park lds, int j) { return {unp(lds, 2 * j), unp(lds, 2 * j + 1)}; }
+DEV FR unpark12(Park lds) {
+    return {{unp(lds, 0), unp(lds, 1)}, {unp(lds, 2), unp(lds, 3)}, {unp(lds, 4), unp(lds, 5)}};
+}
+// x * y, y parked (tower.inc f12_mul)
+template <int A, int B>
+DEV FR f12_mul_lds(const F12<A, B>& x, Park y) {
+    const auto t0 = norm(mul(x.a, unp4(y, 0)));
+    const auto t1 = norm(mul(x.b, unp4(y, 1)));
+    const auto t2 = norm(mul(x.c, unp4(y, 2)));
+    const auto rb = rest4(add(sub(sub(mul(norm(add(x.a, x.b)), norm(add(unp4(y, 0), unp4(y, 1)))), t0), t1), mul_s(t2)));
+    const auto rc = rest4(add(sub(sub(mul(norm(add(x.a, x.c)), norm(add(unp4(y, 0), unp4(y, 2)))), t0), t2), t1));
+    const auto ra = rest4(add(mul_s(norm(sub(sub(mul(norm(add(x.b, x.c)), norm(add(unp4(y, 1), unp4(y, 2)))), t1), t2))), t0));
+    return {ra, rb, rc};
+}
+
 // F <- the Miller values (fexp_pl.hip's input: 12 x 32 SoA, R form), in R' form
 static __device__ __noinline__ void zx_in(const uint32_t* fbuf, size_t n, Zs dst, size_t i) {
     const Soa F{const_cast<uint32_t*>(fbuf), n};
@@ -77,10 +113,10 @@ static __device__ __noinline__ void zx_in(const uint32_t* fbuf, size_t n, Zs dst
 }
 static __device__ __noinline__ void zx_inv(Zs src, Zs dst, size_t i) { st12(dst, i, rest(f12_inv(ld12(src, i)))); }
 // dst <- op_a(a) * op_b(b)
-DEV void zx_mul(Zs a, int opa, Zs b, int opb, Zs dst, size_t i) {
+DEV void zx_mul(Zs a, int opa, Zs b, int opb, Zs dst, Park lds, size_t i) {
+    park12(lds, zapply(ld12(b, i), opb));
     const FR x = zapply(ld12(a, i), opa);
-    const FR y = zapply(ld12(b, i), opb);
-    st12(dst, i, rest(f12_mul(x, y)));
+    st12(dst, i, f12_mul_lds(x, lds));
 }
 // dst <- src^3 (cyclotomic)
 static __device__ __noinline__ void zx_cube(Zs src, Zs dst, size_t i) {
@@ -148,7 +184,7 @@ DEV Z4 ld_z4(const Zs& K, int base, size_t i) {
 
 // dst <- src^x (fexp_pl.hip fx_pow_x): 57 compressed squarings with snapshots g^(2^16), g^(2^48) in K,
 // one inversion for the three decompressions, 6 Granger-Scott squarings, 5 Fp12 products, conj.
-DEV void zx_pow_x(Zs src, Zs dst, Zs K, size_t i) {
+DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i) {
     Z4 c{ld_z(src, 4, i), ld_z(src, 6, i), ld_z(src, 8, i), ld_z(src, 10, i)};
     // three loops, the snapshot stores between them (a store inside the loop body gets its address
     // arithmetic spilled and reloaded at every iteration)
@@ -179,23 +215,23 @@ DEV void zx_pow_x(Zs src, Zs dst, Zs K, size_t i) {
         return;
     }
     const auto iv = inv(p2);
-    FR y = z4_expand(c, n0, n1, mulr(iv, p1));  // g^(2^57)
-    const auto iv2 = mulr(iv, d57);             // (d16 d48)^-1
-    FR acc = z4_expand(ld_z4(K, 0, i), ld_z(K, 8, i), ld_z(K, 10, i), mulr(iv2, d48));  // g^(2^16)
+    st12(dst, i, z4_expand(c, n0, n1, mulr(iv, p1)));  // y = g^(2^57), waits in dst
+    const auto iv2 = mulr(iv, d57);                   // (d16 d48)^-1
+    park12(lds, z4_expand(ld_z4(K, 12, i), ld_z(K, 20, i), ld_z(K, 22, i), mulr(iv2, d16)));  // g^(2^48)
     {
-        const FR t = z4_expand(ld_z4(K, 12, i), ld_z(K, 20, i), ld_z(K, 22, i), mulr(iv2, d16));  // g^(2^48)
-        acc = rest(f12_mul(acc, t));
+        const FR acc = f12_mul_lds(z4_expand(ld_z4(K, 0, i), ld_z(K, 8, i), ld_z(K, 10, i), mulr(iv2, d48)),
+                                   lds);  // g^(2^16) g^(2^48)
+        park12(lds, ld12(dst, i));        // y
+        st12(K, i, f12_mul_lds(acc, lds));  // acc waits in K while y squares in LDS
     }
-    acc = rest(f12_mul(acc, y));
+    // then y^2 three times, acc *= y (2^60), y^2 twice, acc *= y (2^62), y^2, acc *= y (2^63)
+    constexpr uint32_t kSq = 0b010110111u;  // from bit 0: S S S M S S M S M  (1 = square)
 #pragma unroll 1
-    for (int k = 0; k < 3; k++) y = rest(f12_cyc_sqr(y));
-    acc = rest(f12_mul(acc, y));  // 2^60
-#pragma unroll 1
-    for (int k = 0; k < 2; k++) y = rest(f12_cyc_sqr(y));
-    acc = rest(f12_mul(acc, y));  // 2^62
-    y = rest(f12_cyc_sqr(y));
-    acc = rest(f12_mul(acc, y));  // 2^63
-    st12(dst, i, f12_conj(acc));
+    for (int st = 0; st < 9; st++) {
+        if ((kSq >> st) & 1u) park12(lds, rest(f12_cyc_sqr(unpark12(lds))));
+        else st12(K, i, f12_mul_lds(ld12(K, i), lds));
+    }
+    st12(dst, i, f12_conj(ld12(K, i)));
 }
 
 // verdict and GT bytes of the result (fexp_pl.hip fexp_out), through the storage form
@@ -247,6 +283,7 @@ __constant__ static const ZStep kChain[16] = {
 __global__ __launch_bounds__(256, 2) void k_fexp_lz(size_t n, const uint32_t* __restrict__ fbuf,
                                                  int32_t* __restrict__ scratch, const uint32_t* __restrict__ flags,
                                                  uint8_t* __restrict__ verdicts, uint8_t* __restrict__ gt_out) {
+    __shared__ int32_t lds[6 * PW][FB];
     const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
     if (i >= n) return;  // pair-uniform
     const size_t sl = (size_t)LN * n;
@@ -261,8 +298,8 @@ __global__ __launch_bounds__(256, 2) void k_fexp_lz(size_t n, const uint32_t* __
     for (int s = 0; s < 16; s++) {
         const ZStep z = kChain[s];
         const Zs a{scratch + z.a * 12 * sl, n}, b{scratch + z.b * 12 * sl, n}, d{scratch + z.d * 12 * sl, n};
-        if (z.kind == 0) zx_mul(a, z.opa, b, z.opb, d, i);
-        else if (z.kind == 1) zx_pow_x(a, d, K, i);
+        if (z.kind == 0) zx_mul(a, z.opa, b, z.opb, d, lds, i);
+        else if (z.kind == 1) zx_pow_x(a, d, K, lds, i);
         else zx_cube(a, d, i);
     }
     zexp_out(i, ld12(R, i), flags, verdicts, gt_out);

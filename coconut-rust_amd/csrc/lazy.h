@@ -396,6 +396,46 @@ DEV Fq<A, B> sel(bool c, const Fq<A, B>& x, const Fq<A, B>& y) {
     return r;
 }
 
+// ---------------------------------------------------------------- packed LDS parking
+// A lazy value parked in LDS column threadIdx.x of a [rows][MB] array: limbs carry-normalised to
+// [0, 2^28) (value unchanged), limbs 0..12 packed into 12 words, the signed top limb in a 13th.
+constexpr int PW = 13;  // packed words per Fq
+template <int MB, int A, int B>
+DEV void pack_fq(int32_t (*lds)[MB], int row, const Fq<A, B>& x) {
+    int32_t u[LN], c = 0;
+#pragma unroll
+    for (int k = 0; k < LN - 1; k++) {
+        const int32_t t = x.v[k] + c;
+        u[k] = t & LM;
+        c = t >> 28;
+    }
+    u[LN - 1] = x.v[LN - 1] + c;
+#pragma unroll
+    for (int w = 0; w < PW - 1; w++) {
+        const int bit = 32 * w, k = bit / 28, s = bit % 28;
+        uint32_t v = (uint32_t)u[k] >> s;
+        if (k + 1 < LN - 1) v |= (uint32_t)u[k + 1] << (28 - s);
+        if (s > 24 && k + 2 < LN - 1) v |= (uint32_t)u[k + 2] << (56 - s);
+        lds[row + w][threadIdx.x] = (int32_t)v;
+    }
+    lds[row + PW - 1][threadIdx.x] = u[LN - 1];
+}
+template <int MB, int B>
+DEV Fq<AN, B> unpack_fq(int32_t (*lds)[MB], int row) {
+    uint32_t w[PW];
+#pragma unroll
+    for (int j = 0; j < PW; j++) w[j] = (uint32_t)lds[row + j][threadIdx.x];
+    Fq<AN, B> r;
+    r.v[0] = (int32_t)(w[0] & (uint32_t)LM);
+#pragma unroll
+    for (int k = 1; k < LN - 1; k++) {
+        const int bit = 28 * k, j = bit >> 5, s = bit & 31;
+        r.v[k] = (int32_t)((s ? __builtin_amdgcn_alignbit(w[j + 1], w[j], s) : w[j]) & (uint32_t)LM);
+    }
+    r.v[LN - 1] = (int32_t)w[PW - 1];
+    return r;
+}
+
 // ---------------------------------------------------------------- pair-lane Fp2
 template <int A, int B>
 struct F2 {

@@ -79,51 +79,15 @@ DEV F12S eval_mul(const F12<AS, B>& f, const LineS& ln, const PSrc& ps, size_t i
 // (84 + 42 + 42 words a lane) do not).  A T is packed for it: limbs carry-normalised to [0, 2^28),
 // 13 limbs in 12 words + the signed top limb = 39 words, so both T's of the 512 lanes a CU holds fit
 // its 160 KiB (78 x 4 B x 512).
-constexpr int PW = 13;      // packed words per Fq
 constexpr int TP = 3 * PW;  // packed words per T
-template <int A, int B>
-DEV void pack_fq(int32_t (*lds)[MB], int row, const Fq<A, B>& x) {
-    int32_t u[LN], c = 0;
-#pragma unroll
-    for (int k = 0; k < LN - 1; k++) {
-        const int32_t t = x.v[k] + c;
-        u[k] = t & LM;
-        c = t >> 28;
-    }
-    u[LN - 1] = x.v[LN - 1] + c;
-#pragma unroll
-    for (int w = 0; w < PW - 1; w++) {
-        const int bit = 32 * w, k = bit / 28, s = bit % 28;
-        uint32_t v = (uint32_t)u[k] >> s;
-        if (k + 1 < LN - 1) v |= (uint32_t)u[k + 1] << (28 - s);
-        if (s > 24 && k + 2 < LN - 1) v |= (uint32_t)u[k + 2] << (56 - s);
-        lds[row + w][threadIdx.x] = (int32_t)v;
-    }
-    lds[row + PW - 1][threadIdx.x] = u[LN - 1];
-}
-template <int B>
-DEV Fq<AN, B> unpack_fq(int32_t (*lds)[MB], int row) {
-    uint32_t w[PW];
-#pragma unroll
-    for (int j = 0; j < PW; j++) w[j] = (uint32_t)lds[row + j][threadIdx.x];
-    Fq<AN, B> r;
-    r.v[0] = (int32_t)(w[0] & (uint32_t)LM);
-#pragma unroll
-    for (int k = 1; k < LN - 1; k++) {
-        const int bit = 28 * k, j = bit >> 5, s = bit & 31;
-        r.v[k] = (int32_t)((s ? __builtin_amdgcn_alignbit(w[j + 1], w[j], s) : w[j]) & (uint32_t)LM);
-    }
-    r.v[LN - 1] = (int32_t)w[PW - 1];
-    return r;
-}
 DEV void park(int32_t (*lds)[MB], int k, const Tw& T) {
-    pack_fq(lds, TP * k, T.x.c);
-    pack_fq(lds, TP * k + PW, T.y.c);
-    pack_fq(lds, TP * k + 2 * PW, T.z.c);
+    pack_fq<MB>(lds, TP * k, T.x.c);
+    pack_fq<MB>(lds, TP * k + PW, T.y.c);
+    pack_fq<MB>(lds, TP * k + 2 * PW, T.z.c);
 }
 DEV Tw unpark(int32_t (*lds)[MB], int k) {
-    return {fit<AS, BX>(F2<AN, BX>{unpack_fq<BX>(lds, TP * k)}), fit<AS, BY>(F2<AN, BY>{unpack_fq<BY>(lds, TP * k + PW)}),
-            fit<AS, BZ>(F2<AN, BZ>{unpack_fq<BZ>(lds, TP * k + 2 * PW)})};
+    return {fit<AS, BX>(F2<AN, BX>{unpack_fq<MB, BX>(lds, TP * k)}), fit<AS, BY>(F2<AN, BY>{unpack_fq<MB, BY>(lds, TP * k + PW)}),
+            fit<AS, BZ>(F2<AN, BZ>{unpack_fq<MB, BZ>(lds, TP * k + 2 * PW)})};
 }
 
 // a precomputed g~ line (SigG1): AoS l0 | l2 | l3, (a, b) halves of 12 words, R form
