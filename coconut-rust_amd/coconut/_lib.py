@@ -54,6 +54,7 @@ _SIGS = {
     "cc_last_timing": (c_int, [c_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),
                                ctypes.POINTER(ctypes.c_float)]),
     "cc_set_timing": (c_int, [c_p, c_int]),
+    "cc_selftest_lazy": (c_int, [c_int, c_sz, c_p, c_p, c_p, c_p, c_p]),
 }
 
 for _name, (_res, _args) in _SIGS.items():

@@ -230,6 +230,15 @@ cc_status cc_fixed_base_mul(cc_ctx* ctx, int group, const uint8_t* base, size_t 
 cc_status cc_last_timing(const cc_ctx* ctx, float* prep_ms, float* miller_ms, float* fexp_ms);
 cc_status cc_set_timing(cc_ctx* ctx, int enabled);
 
+/* Device self-test of the lazy radix-2^28 field core the pairing kernels use (csrc/lazy.h): op 0
+ * (a b + c d) / 2^392, op 1 a b / 2^392 (signed product scanning with Montgomery reduction), op 2 the
+ * value reduction, op 3 the limb squeeze, on n elements of 14 signed 28-bit-radix limbs (host
+ * arrays, n x 14 int32; b, c, d may be NULL for ops 1-3).  Test infrastructure: the tests drive it
+ * at the limits of the compile-time bounds and compare with big-integer arithmetic.  Returns 0, or
+ * -1 on a HIP error or an unknown op.  No context needed (current device). */
+int cc_selftest_lazy(int op, size_t n, const int32_t* a, const int32_t* b, const int32_t* c, const int32_t* d,
+                     int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif
