@@ -385,7 +385,7 @@ __global__ __launch_bounds__(256, MINB) void k_prep_pok(size_t n, int q, int r, 
                                                   const uint32_t* __restrict__ Xaff, uint32_t Xinf,
                                                   const uint32_t* __restrict__ table, int wbits,
                                                   const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
-                                                  uint32_t* __restrict__ flags) {
+                                                  uint32_t* __restrict__ flags, uint32_t* __restrict__ jtab) {
     size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     constexpr bool kSigG2 = sizeof(FS_) == sizeof(Fp2);
@@ -430,14 +430,33 @@ __global__ __launch_bounds__(256, MINB) void k_prep_pok(size_t n, int q, int r, 
             slot++;
             if (!binf[h]) ft_add<FO>(acc, k.v, table, wbits, h, 0, nwin);
         }
-        // J * chal (variable base)
+        // J * chal (variable base), fixed 4-bit windows: a per-lane table d J (d = 1..15, Jacobian, SoA
+        // in jtab) and 64 windows of 4 doublings + one addition.  The bitwise double-and-add it
+        // replaces ran an addition at nearly every bit in SIMT (some lane of the wave has the bit set):
+        // 255 + 255 group operations against 255 + 64 + 14 here.
         fr_from_be48(k, chal + i * 48);
         if (Jok) {
+            constexpr int JW = sizeof(Jac<FO>) / 4;
+            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * JW + w) * n + i]; };
+            Jac<FO> t;
+            jac_from_aff(t, Ja);
+#pragma unroll 1
+            for (int d = 1; d <= 15; d++) {
+                if (d > 1) jac_add_aff(t, t, Ja);
+                const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
+                for (int w = 0; w < JW; w++) tab(d, w) = tw[w];
+            }
             Jac<FO> s;
             jac_set_inf(s);
-            for (int b = 254; b >= 0; b--) {
-                jac_dbl(s, s);
-                if ((k.v[b >> 5] >> (b & 31)) & 1u) jac_add_aff(s, s, Ja);
+#pragma unroll 1
+            for (int win = 63; win >= 0; win--) {
+                for (int b = 0; b < 4; b++) jac_dbl(s, s);
+                const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
+                if (d) {
+                    uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
+                    for (int w = 0; w < JW; w++) tw[w] = tab((int)d, w);
+                    jac_add(s, s, t);
+                }
             }
             jac_add(acc, acc, s);
         }
@@ -551,15 +570,16 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
                  const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
-                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st) {
+                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_jtab, hipStream_t st) {
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
+    // d_jtab: 15 Jacobian points of the other group per element (<= 15 x 72 words a proof)
     if (mode == 0)
         hipLaunchKernelGGL((k_prep_pok<Fp2, Fp, 2>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
-                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags);
+                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags, d_jtab);
     else
         hipLaunchKernelGGL((k_prep_pok<Fp, Fp2, 1>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
-                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags);
+                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags, d_jtab);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -73,7 +73,7 @@ int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t*
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
                  const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
-                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
+                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_jtab, hipStream_t st);
 }
 
 namespace {
@@ -1137,7 +1137,8 @@ static cc_status launch_pok(cc_ctx* c, size_t n, size_t q, size_t r, const uint8
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_prep_pok(c->mode, n, (int)q, (int)r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_idx,
                      c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(), c->wbits,
-                     c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
+                     c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(),
+                     c->scratch.as<uint32_t>(), st));  // J*chal window table: the fexp scratch, free until fexp
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
