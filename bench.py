@@ -334,7 +334,7 @@ def bench_verify(args, mode):
             "value": round(value, 1), "unit": "credentials/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
-            "dtype": "u32 (Fp 12x32-bit Montgomery limbs, integer-only)",
+            "dtype": "int32/u32 (pairing kernels: 14 signed 28-bit-radix limbs, lazy; elsewhere 12x32-bit Montgomery; integer-only)",
             "data": "synthetic (seeded; sigma = k*G, k*(x+sum y m)*G built on the GPU; 1/16 corrupted)",
             "config": {"workload": f"config2: batch of {n:,} Signature::verify per GPU, msg_count=6, shared "
                                    f"aggregated verkey, {layout}",
@@ -423,7 +423,7 @@ def bench_rlc(args):
             "metric": "verified credentials/sec, RLC batch mode (msg_count=16)",
             "value": round(value, 1), "unit": "credentials/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 12x32-bit storage, integer-only)",
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32/u32 (pairing kernels: 14 signed 28-bit-radix limbs, lazy; elsewhere 12x32-bit Montgomery; integer-only)",
             "data": "synthetic (seeded; all valid, reject path checked after timing)",
             "config": {"workload": "config3: RLC batch verify, msg_count=16, shared verkey, SigG2",
                        "credentials_per_gpu": n, "msg_count": q,

@@ -291,7 +291,7 @@ def bench_pok(args):
             "metric": "verified PoK-of-signature proofs/sec (msg_count=32, 8 revealed)",
             "value": round(value, 1), "unit": "proofs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 12x32-bit Montgomery limbs, integer-only)",
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32/u32 (pairing kernels: 14 signed 28-bit-radix limbs, lazy; elsewhere 12x32-bit Montgomery; integer-only)",
             "data": "synthetic (seeded; proofs with known discrete logs built on the GPU; 1/16 bad response)",
             "config": {"workload": f"config5: {n:,} PoKOfSignatureProof::verify per GPU, q=32, revealed "
                                    f"{b['revealed']}, SigG2", "proofs_per_gpu": n,
