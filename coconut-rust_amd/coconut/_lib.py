@@ -12,6 +12,15 @@ if not os.path.exists(LIB_PATH):
     raise ImportError(f"libcoconut_hip.so not built at {LIB_PATH}: run `make -C coconut-rust_amd` "
                       "(or __graft_entry__.build()); there is no CPU fallback")
 
+# torch ships its own libamdhip64.so.7 (built for an older ROCm) with the same SONAME as
+# /opt/rocm's. Whichever is loaded first serves both, and torch's own device init fails against
+# the newer one ("No HIP GPUs are available"). Load torch first so that this library binds to
+# torch's runtime. Tensors handed across the ABI then live in the same HIP context.
+try:
+    import torch  # noqa: F401
+except ImportError:  # the C ABI itself needs no torch
+    pass
+
 lib = ctypes.CDLL(LIB_PATH)
 
 c_sz = ctypes.c_size_t
