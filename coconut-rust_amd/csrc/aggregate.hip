@@ -11,6 +11,8 @@
 //                    Schnorr check MSM(g~, Y~_hidden.., J; responses.., chal) == T, then
 //                    J' = X~ + J + sum_revealed Y~_i m_i, written in the verify kernels' Miller-loop
 //                    operand layout so k_miller_* / k_fexp finish the 2-pairing check.
+#include <cstdlib>
+
 #include "codec.h"
 #include "curve_pl.h"
 #include "fixed.h"
@@ -49,29 +51,72 @@ DEV void ld_aff_aos(Aff<F>& a, const uint32_t* p) {
 
 // ================================================================ Lagrange coefficients
 // l[(cred * t + i) * 8 ..]: canonical l_i(0) for the i-th of the first t ids of credential `cred`.
+// LT tasks (credential, i) per lane.
+// - The factors enter as raw integers, not Montgomery images: num and den both take one factor per
+//   other id, so the R^-1 each product picks up cancels in num / den (no conversion multiply).
+// - The tasks' denominators share ONE Fermat inversion (Montgomery's trick: with
+//   P_q = den_0 ... den_{q-1}, l_q = (num_q P_q) / P_{q+1}, walking q down from 1 / P_cnt and
+//   multiplying den_q back in).
+// - The O(t^2) duplicate scan (HashSet semantics) runs once per credential a lane touches; a
+//   credential without repeated ids takes the plain product loop.
+template <int LT>
 __global__ void k_lagrange(size_t n, size_t len, size_t t, const uint64_t* __restrict__ ids, uint32_t* __restrict__ l) {
-    size_t task = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (task >= n * t) return;
-    size_t cred = task / t, i = task % t;
-    const uint64_t* id = ids + cred * len;
-    const uint64_t xi = id[i];
-    Fm num = fm_one(), den = fm_one();
-    const Fm fxi = fm_from_u64(xi);
-    for (size_t j = 0; j < t; j++) {
-        const uint64_t xj = id[j];
-        if (xj == xi) continue;
-        bool dup = false;
-        for (size_t k = 0; k < j; k++)
-            if (id[k] == xj) { dup = true; break; }
-        if (dup) continue;  // HashSet semantics
-        Fm fxj = fm_from_u64(xj), d;
-        num = fm_mul_v(num, fxj);
-        fm_sub(d, fxj, fxi);
-        den = fm_mul_v(den, d);
+    const size_t first = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) * LT;
+    if (first >= n * t) return;
+    const int cnt = (int)((n * t - first) < (size_t)LT ? (n * t - first) : (size_t)LT);
+    Fm nump[LT], den[LT];
+    Fm pre = fm_one();  // P_q (a Montgomery 1: the raw factors' R^-k cancel between num and den)
+    size_t have = ~(size_t)0;
+    bool dups = false;
+#pragma unroll
+    for (int q = 0; q < LT; q++) {
+        if (q >= cnt) break;
+        const size_t task = first + q, cred = task / t, i = task % t;
+        const uint64_t* id = ids + cred * len;
+        if (cred != have) {
+            have = cred;
+            dups = false;
+            for (size_t j = 1; j < t && !dups; j++)
+                for (size_t k = 0; k < j; k++)
+                    if (id[k] == id[j]) { dups = true; break; }
+        }
+        const uint64_t xi = id[i];
+        Fm nm = fm_one(), dn = fm_one(), fxi;
+#pragma unroll
+        for (int k = 0; k < NR; k++) fxi.v[k] = 0;
+        fxi.v[0] = (uint32_t)xi;
+        fxi.v[1] = (uint32_t)(xi >> 32);
+        for (size_t j = 0; j < t; j++) {
+            const uint64_t xj = id[j];
+            if (xj == xi) continue;
+            if (dups) {
+                bool seen = false;
+                for (size_t k = 0; k < j; k++)
+                    if (id[k] == xj) { seen = true; break; }
+                if (seen) continue;
+            }
+            Fm fxj, d;
+#pragma unroll
+            for (int k = 0; k < NR; k++) fxj.v[k] = 0;
+            fxj.v[0] = (uint32_t)xj;
+            fxj.v[1] = (uint32_t)(xj >> 32);
+            nm = fm_mul_v(nm, fxj);
+            fm_sub(d, fxj, fxi);
+            dn = fm_mul_v(dn, d);
+        }
+        nump[q] = fm_mul_v(nm, pre);
+        den[q] = dn;
+        pre = fm_mul_v(pre, dn);
     }
-    Fm li = fm_to_canon(fm_mul_v(num, fm_inv(den)));
-    uint32_t* o = l + task * 8;
-    for (int k = 0; k < 8; k++) o[k] = li.v[k];
+    Fm inv = fm_inv(pre);  // 1 / P_cnt
+#pragma unroll
+    for (int q = LT - 1; q >= 0; q--) {
+        if (q >= cnt) continue;
+        const Fm li = fm_to_canon(fm_mul_v(nump[q], inv));  // num_q P_q / P_{q+1}
+        uint32_t* o = l + (first + q) * 8;
+        for (int k = 0; k < 8; k++) o[k] = li.v[k];
+        inv = fm_mul_v(inv, den[q]);  // 1 / P_q
+    }
 }
 
 // ================================================================ windowed Straus MSM (variable bases)
@@ -530,7 +575,16 @@ extern "C" {
 
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st) {
     if (!n || !t) return 0;
-    hipLaunchKernelGGL(k_lagrange, dim3(nblocks(n * t, 64)), dim3(64), 0, st, n, len, t, d_ids, d_l);
+    static const int lt = [] {
+        const char* e = getenv("CC_LAG_LT");
+        return e ? atoi(e) : 4;
+    }();
+    if (lt == 8)
+        hipLaunchKernelGGL(k_lagrange<8>, dim3(nblocks((n * t + 7) / 8, 64)), dim3(64), 0, st, n, len, t, d_ids, d_l);
+    else if (lt == 2)
+        hipLaunchKernelGGL(k_lagrange<2>, dim3(nblocks((n * t + 1) / 2, 64)), dim3(64), 0, st, n, len, t, d_ids, d_l);
+    else
+        hipLaunchKernelGGL(k_lagrange<4>, dim3(nblocks((n * t + 3) / 4, 64)), dim3(64), 0, st, n, len, t, d_ids, d_l);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
