@@ -596,9 +596,19 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
     if (!ntask) return 0;
     constexpr int L = 16;
     dim3 g(nblocks(ntask * L, 256)), b(256);
+    static const int l2 = [] {
+        const char* e = getenv("CC_STRAUS_L2");
+        return e ? atoi(e) : L / 2;
+    }();
     if (group == 1)
         hipLaunchKernelGGL((k_msm_straus<Fp, L>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l,
                            l_div, d_scratch, d_out);
+    else if (l2 == 4)
+        hipLaunchKernelGGL((k_msm_straus_g2pl<4>), dim3(nblocks(ntask * 8, 256)), b, 0, st, ntask, t, d_pts, pt_stride,
+                           pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
+    else if (l2 == 16)
+        hipLaunchKernelGGL((k_msm_straus_g2pl<16>), dim3(nblocks(ntask * 32, 256)), b, 0, st, ntask, t, d_pts,
+                           pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
     else
         hipLaunchKernelGGL((k_msm_straus_g2pl<L / 2>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step,
                            d_l, l_div, d_scratch, d_out);
@@ -609,15 +619,22 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
                      const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, const uint32_t* d_binf,
                      uint8_t* d_outX, uint8_t* d_outY, hipStream_t st) {
     if (!n) return 0;
-    constexpr int L = 4;
+    constexpr int L = 8;  // 8 lanes per (credential, key) task: 34.1 ms vs 35.8 (4) and 43.3 (2) at config 4
     const size_t ntask = n * (size_t)(q + 1);
     dim3 g(nblocks(ntask * L, 256)), b(256);
-    if (group == 1)
+    static const int vl = [] {
+        const char* e = getenv("CC_VKF_L");
+        return e ? atoi(e) : L;
+    }();
+    if (group == 1 && vl == 4)
+        hipLaunchKernelGGL((k_vk_agg_fixed<Fp, 4>), dim3(nblocks(ntask * 4, 256)), b, 0, st, n, len, t, q, d_ids, d_l,
+                           d_iss_ids, n_iss, d_table, d_binf, d_outX, d_outY);
+    else if (group == 1)
         hipLaunchKernelGGL((k_vk_agg_fixed<Fp, L>), g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
                            d_binf, d_outX, d_outY);
     else
-        hipLaunchKernelGGL((k_vk_agg_fixed<Fp2, L>), g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
-                           d_binf, d_outX, d_outY);
+        hipLaunchKernelGGL((k_vk_agg_fixed<Fp2, 4>), dim3(nblocks(ntask * 4, 256)), b, 0, st, n, len, t, q, d_ids,
+                           d_l, d_iss_ids, n_iss, d_table, d_binf, d_outX, d_outY);  // G2 keys: not re-measured
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
