@@ -263,11 +263,18 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus(size_t ntask, size_t t, c
 // G2 point in 3 Fp a lane (2 waves/SIMD) and halves each lane's share of every Fp2 product.  L2 pairs
 // per task take the bases k = pair, pair + L2, ...; the scratch layout is straus_words<Fp2> with
 // each entry's two halves side by side ([entry][half][words]).
-template <int L2>
+//
+// kLds: the task's digits live in LDS (t x 65 bytes a task, dynamic shared memory), and a digit whose
+// multiple is the identity is zeroed there after normalisation, so the only global load an addition
+// waits on is its table entry (the digit byte and the identity flag were two more dependent global
+// round trips; the out-of-line Fp2 products begin with s_waitcnt vmcnt(0), so a load cannot be
+// prefetched across them).
+template <int L2, bool kLds>
 __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
                                                            size_t pt_stride, size_t pt_jstride, size_t pt_step,
                                                            const uint32_t* __restrict__ l, size_t l_div,
                                                            uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
+    extern __shared__ int8_t sdig[];
     using F = pl::Fp2;
     using T = FT<F>;
     constexpr int L = 2 * L2;
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
     const uint32_t* lk = l + cred * t * 8;
     uint32_t* ent = scratch + task * straus_words<Fp2>(t);
     uint32_t* pre = ent + t * 8 * (2 * JW);
-    int8_t* dig = reinterpret_cast<int8_t*>(pre + t * 8 * (2 * PW));
+    int8_t* dig = kLds ? sdig + (threadIdx.x / L) * t * 65 : reinterpret_cast<int8_t*>(pre + t * 8 * (2 * PW));
     F acc_z;
     T::one(acc_z);
 #pragma unroll 1
@@ -313,6 +320,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
         const long long kmax = (long long)(((t - 1 - pair) / L2) * L2 + pair);
 #pragma unroll 1
         for (long long kk = kmax; kk >= pair; kk -= L2) {
+            unsigned infm = 0;  // identity multiples of base kk (pair-uniform)
             for (int d = 7; d >= 0; d--) {
                 const size_t e = (size_t)kk * 8 + d;
                 cc::Jac<F> J;
@@ -320,6 +328,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
                 uint32_t* jw = reinterpret_cast<uint32_t*>(&J);
                 for (int c = 0; c < JW; c++) jw[c] = w[c];
                 const bool inf = jac_is_inf(J);
+                infm |= (inf ? 1u : 0u) << d;
                 if (!inf) {
                     F pz, zi, zi2;
                     for (int c = 0; c < PW; c++) pz.c.v[c] = pre[(e * 2 + h) * PW + c];
@@ -332,6 +341,13 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
                 }
                 for (int c = 0; c < 2 * PW; c++) w[c] = jw[c];  // this half's affine x, y
                 w[2 * PW] = inf ? 1u : 0u;
+            }
+            if (kLds && infm) {
+                int8_t* dk = dig + kk * 65;
+                for (int win = 0; win < 65; win++) {
+                    const int d = dk[win];
+                    if (d && ((infm >> ((d < 0 ? -d : d) - 1)) & 1u)) dk[win] = 0;
+                }
             }
         }
     }
@@ -346,7 +362,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
             const int d = dig[k * 65 + win];
             if (!d) continue;
             const uint32_t* w = ent + ((k * 8 + (d < 0 ? -d : d) - 1) * 2 + h) * JW;
-            if (w[2 * PW]) continue;  // identity multiple (pair-uniform: both halves carry the flag)
+            if (!kLds && w[2 * PW]) continue;  // identity multiple (pair-uniform: both halves carry the flag)
             cc::Aff<F> e;
             for (int c = 0; c < PW; c++) {
                 e.x.c.v[c] = w[c];
@@ -600,18 +616,30 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
         const char* e = getenv("CC_STRAUS_L2");
         return e ? atoi(e) : L / 2;
     }();
+    static const bool lds_ok = [] {
+        const char* e = getenv("CC_STRAUS_LDS");
+        return !(e && e[0] == '0');
+    }();
+    const size_t lds = (256 / L) * t * 65;  // digits of the block's 16 tasks
     if (group == 1)
         hipLaunchKernelGGL((k_msm_straus<Fp, L>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l,
                            l_div, d_scratch, d_out);
     else if (l2 == 4)
-        hipLaunchKernelGGL((k_msm_straus_g2pl<4>), dim3(nblocks(ntask * 8, 256)), b, 0, st, ntask, t, d_pts, pt_stride,
-                           pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
-    else if (l2 == 16)
-        hipLaunchKernelGGL((k_msm_straus_g2pl<16>), dim3(nblocks(ntask * 32, 256)), b, 0, st, ntask, t, d_pts,
+        hipLaunchKernelGGL((k_msm_straus_g2pl<4, false>), dim3(nblocks(ntask * 8, 256)), b, 0, st, ntask, t, d_pts,
                            pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
-    else
-        hipLaunchKernelGGL((k_msm_straus_g2pl<L / 2>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step,
-                           d_l, l_div, d_scratch, d_out);
+    else if (l2 == 16)
+        hipLaunchKernelGGL((k_msm_straus_g2pl<16, false>), dim3(nblocks(ntask * 32, 256)), b, 0, st, ntask, t, d_pts,
+                           pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
+    else if (lds_ok && lds <= 80 * 1024) {  // two blocks a CU (the 2 waves/SIMD the registers allow)
+        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msm_straus_g2pl<L / 2, true>),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     80 * 1024) == hipSuccess;
+        if (!attr) return -1;
+        hipLaunchKernelGGL((k_msm_straus_g2pl<L / 2, true>), g, b, lds, st, ntask, t, d_pts, pt_stride, pt_jstride,
+                           pt_step, d_l, l_div, d_scratch, d_out);
+    } else
+        hipLaunchKernelGGL((k_msm_straus_g2pl<L / 2, false>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride,
+                           pt_step, d_l, l_div, d_scratch, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
