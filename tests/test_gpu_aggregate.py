@@ -131,3 +131,51 @@ def test_signature_aggregate_threshold_zero_and_small_order_safe(ctxs):
     o1, o2 = signature_aggregate_batch(ctx, 1, 3, 0, [case["ids"]], _cat(case["sigma1"]), _cat(case["sigma2"]))
     assert o1.hex() == case["sigma1"][0]
     assert o2 == bytes(96) + (1).to_bytes(48, "big") + bytes(48)
+
+
+@pytest.mark.parametrize("mode_name", ["aggregate_g2_t67_subsets.json", "aggregate_g1_t67_subsets.json"])
+@pytest.mark.parametrize("t", [1, 2, 3, 5, 9])
+def test_lagrange_batching_ragged_against_oracle(ctxs, oc, mode_name, t):
+    """k_lagrange runs 4 (credential, i) tasks per lane with one shared inversion and scans each
+    credential for repeated ids once: batches where n * t is not a multiple of 4, lanes straddling
+    credentials, and rows with repeated ids (HashSet semantics, reference secret_sharing
+    lagrange_basis_at_0) must give the oracle's Signature::aggregate and Verkey::aggregate per row."""
+    import random
+    from coconut import signature_aggregate_batch, verkey_aggregate_ids
+    d = golden(mode_name)
+    ctx = ctxs[d["mode"]]
+    mode = 0 if d["mode"] == "G2" else 1
+    q = d["q"]
+    sb, ob = (192, 97) if mode == 0 else (97, 192)
+    keys, sigs = {}, {}
+    for case in d["cases"]:
+        for k, i in enumerate(case["ids"]):
+            keys[i] = (case["X"][k], case["Y"][k])
+            sigs[i] = (case["sigma1"][k], case["sigma2"][k])
+    pool = sorted(set(keys) & set(sigs))
+    ctx.set_issuers(pool, _cat(keys[i][0] for i in pool), _cat(y for i in pool for y in keys[i][1]), q)
+    rng = random.Random(1000 + t)
+    L, n = 9, 13
+    rows = []
+    for r in range(n):
+        row = rng.sample(pool, L)
+        if r % 3 == 1 and t > 1:
+            row[rng.randrange(1, t)] = row[0]  # a repeated id inside the first t entries
+        rows.append(row)
+    s1 = _cat(sigs[i][0] for row in rows for i in row)
+    s2 = _cat(sigs[i][1] for row in rows for i in row)
+    g1, g2 = signature_aggregate_batch(ctx, n, L, t, rows, s1, s2)
+    gX, gY = verkey_aggregate_ids(ctx, n, L, t, rows)
+    o1, o2 = ctypes.create_string_buffer(sb), ctypes.create_string_buffer(sb)
+    oX, oY = ctypes.create_string_buffer(ob), ctypes.create_string_buffer(ob * q)
+    for r, row in enumerate(rows):
+        idarr = (ctypes.c_uint64 * L)(*row)
+        rs1 = _cat(sigs[i][0] for i in row)
+        rs2 = _cat(sigs[i][1] for i in row)
+        assert oc.oc_signature_aggregate(mode, ctypes.c_size_t(L), ctypes.c_size_t(t), idarr, rs1, rs2, o1, o2) == 0
+        assert g1[r * sb:(r + 1) * sb] == o1.raw and g2[r * sb:(r + 1) * sb] == o2.raw, (r, row[:t])
+        X = _cat(keys[i][0] for i in row)
+        Y = _cat(y for i in row for y in keys[i][1])
+        assert oc.oc_verkey_aggregate(mode, ctypes.c_size_t(L), ctypes.c_size_t(t), ctypes.c_size_t(q), idarr,
+                                      X, Y, oX, oY) == 0
+        assert gX[r * ob:(r + 1) * ob] == oX.raw and gY[r * q * ob:(r + 1) * q * ob] == oY.raw, (r, row[:t])
