@@ -16,6 +16,19 @@
 
 namespace cc {
 namespace lz {
+// Build option CC_FEXP_PROF (tools/fexp_phases.py): per-wave shader-clock totals of the kernel's
+// phases, written by lane 0 of each wave with plain vector stores to g_fx_prof[wave][slot].
+#ifdef CC_FEXP_PROF
+constexpr int kProfSlots = 24, kProfWaves = 8192;
+__device__ unsigned long long g_fx_prof[kProfWaves][kProfSlots];
+#define FXP_DECL unsigned long long fxp[kProfSlots] = {}
+#define FXP_T(v) const unsigned long long v = clock64()
+#define FXP_ADD(slot, t0) (fxp[slot] += clock64() - (t0))
+#else
+#define FXP_DECL
+#define FXP_T(v)
+#define FXP_ADD(slot, t0)
+#endif
 namespace {
 
 using F2R = F2<AN, 9>;
@@ -184,7 +197,13 @@ DEV Z4 ld_z4(const Zs& K, int base, size_t i) {
 
 // dst <- src^x (fexp_pl.hip fx_pow_x): 57 compressed squarings with snapshots g^(2^16), g^(2^48) in K,
 // one inversion for the three decompressions, 6 Granger-Scott squarings, 5 Fp12 products, conj.
-DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i) {
+#ifdef CC_FEXP_PROF
+#define FXP_ARG , unsigned long long* fxp
+#else
+#define FXP_ARG
+#endif
+DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i FXP_ARG) {
+    FXP_T(t_sq);
     Z4 c{ld_z(src, 4, i), ld_z(src, 6, i), ld_z(src, 8, i), ld_z(src, 10, i)};
     // three loops, the snapshot stores between them (a store inside the loop body gets its address
     // arithmetic spilled and reloaded at every iteration)
@@ -196,6 +215,8 @@ DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i) {
     st_z4(K, 12, i, c);
 #pragma unroll 1
     for (int k = 48; k < 57; k++) z4_sqr(c);
+    FXP_ADD(18, t_sq);
+    FXP_T(t_dc);
     F2R n0, n1, d57, d16, d48;
     {
         Z4 s = ld_z4(K, 0, i);
@@ -221,17 +242,20 @@ DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i) {
     {
         const FR acc = f12_mul_lds(z4_expand(ld_z4(K, 0, i), ld_z(K, 8, i), ld_z(K, 10, i), mulr(iv2, d48)),
                                    lds);  // g^(2^16) g^(2^48)
+        FXP_ADD(19, t_dc);
         park12(lds, ld12(dst, i));        // y
         st12(K, i, f12_mul_lds(acc, lds));  // acc waits in K while y squares in LDS
     }
     // then y^2 three times, acc *= y (2^60), y^2 twice, acc *= y (2^62), y^2, acc *= y (2^63)
     constexpr uint32_t kSq = 0b010110111u;  // from bit 0: S S S M S S M S M  (1 = square)
+    FXP_T(t_tl);
 #pragma unroll 1
     for (int st = 0; st < 9; st++) {
         if ((kSq >> st) & 1u) park12(lds, rest(f12_cyc_sqr(unpark12(lds))));
         else st12(K, i, f12_mul_lds(ld12(K, i), lds));
     }
     st12(dst, i, f12_conj(ld12(K, i)));
+    FXP_ADD(20, t_tl);
 }
 
 // verdict and GT bytes of the result (fexp_pl.hip fexp_out), through the storage form
@@ -289,8 +313,13 @@ __global__ __launch_bounds__(256, 2) void k_fexp_lz(size_t n, const uint32_t* __
     const size_t sl = (size_t)LN * n;
     const Zs F{scratch, n}, T{scratch + 12 * sl, n}, A{scratch + 24 * sl, n}, S{scratch + 36 * sl, n},
         R{scratch + 48 * sl, n}, K{scratch + 60 * sl, n};
+    FXP_DECL;
+    FXP_T(t_in);
     zx_in(fbuf, n, F, i);
+    FXP_ADD(0, t_in);
+    FXP_T(t_inv);
     zx_inv(F, T, i);
+    FXP_ADD(1, t_inv);
     // The rest of the chain as ONE loop over its steps with the product and the pow-by-x inlined once
     // each: an out-of-line step function saves and restores every callee-saved register it touches
     // (~330 scratch instructions a call, ~20 calls a lane pair).
@@ -298,17 +327,38 @@ __global__ __launch_bounds__(256, 2) void k_fexp_lz(size_t n, const uint32_t* __
     for (int s = 0; s < 16; s++) {
         const ZStep z = kChain[s];
         const Zs a{scratch + z.a * 12 * sl, n}, b{scratch + z.b * 12 * sl, n}, d{scratch + z.d * 12 * sl, n};
+        FXP_T(t_st);
         if (z.kind == 0) zx_mul(a, z.opa, b, z.opb, d, lds, i);
+#ifdef CC_FEXP_PROF
+        else if (z.kind == 1) zx_pow_x(a, d, K, lds, i, fxp);
+#else
         else if (z.kind == 1) zx_pow_x(a, d, K, lds, i);
+#endif
         else zx_cube(a, d, i);
+        FXP_ADD(2 + s, t_st);
     }
+    FXP_T(t_out);
     zexp_out(i, ld12(R, i), flags, verdicts, gt_out);
+    FXP_ADD(21, t_out);
+#ifdef CC_FEXP_PROF
+    const size_t wave = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 6;
+    if ((threadIdx.x & 63) == 0 && wave < (size_t)kProfWaves)
+        for (int k = 0; k < kProfSlots; k++) g_fx_prof[wave][k] = fxp[k];
+#endif
 }
 
 }  // namespace lz
 }  // namespace cc
 
 // scratch: 84 x 14 words per element (cc_ctx sizes it for this kernel)
+#ifdef CC_FEXP_PROF
+extern "C" int cck_fexp_prof_read(unsigned long long* out, size_t nwaves) {
+    if (nwaves > (size_t)cc::lz::kProfWaves) nwaves = cc::lz::kProfWaves;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(cc::lz::g_fx_prof), nwaves * cc::lz::kProfSlots * 8, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int cck_fexp_lz(size_t n, const uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags,
                            uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
     if (!n) return 0;
