@@ -399,7 +399,7 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
                                                       const uint64_t* __restrict__ ids,
                                                       const uint32_t* __restrict__ l,
                                                       const uint64_t* __restrict__ iss_ids, int n_iss,
-                                                      const uint32_t* __restrict__ table,
+                                                      const uint32_t* __restrict__ table, int wbits,
                                                       const uint32_t* __restrict__ binf,
                                                       uint8_t* __restrict__ outX, uint8_t* __restrict__ outY) {
     const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
         }
         const int b = lo * (q + 1) + j;
         if (binf[b]) continue;
-        ft_add<F>(acc, l + (cred * t + k) * 8, table, 8, b, 0, ft_nwin(8));
+        ft_add<F>(acc, l + (cred * t + k) * 8, table, wbits, b, 0, ft_nwin(wbits));
     }
     lane_group_sum<F, L>(acc);
     if (lane) return;
@@ -644,7 +644,7 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
 }
 
 int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uint64_t* d_ids, const uint32_t* d_l,
-                     const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, const uint32_t* d_binf,
+                     const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
                      uint8_t* d_outX, uint8_t* d_outY, hipStream_t st) {
     if (!n) return 0;
     constexpr int L = 8;  // 8 lanes per (credential, key) task: 34.1 ms vs 35.8 (4) and 43.3 (2) at config 4
@@ -656,13 +656,13 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
     }();
     if (group == 1 && vl == 4)
         hipLaunchKernelGGL((k_vk_agg_fixed<Fp, 4>), dim3(nblocks(ntask * 4, 256)), b, 0, st, n, len, t, q, d_ids, d_l,
-                           d_iss_ids, n_iss, d_table, d_binf, d_outX, d_outY);
+                           d_iss_ids, n_iss, d_table, wbits, d_binf, d_outX, d_outY);
     else if (group == 1)
         hipLaunchKernelGGL((k_vk_agg_fixed<Fp, L>), g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
-                           d_binf, d_outX, d_outY);
+                           wbits, d_binf, d_outX, d_outY);
     else
         hipLaunchKernelGGL((k_vk_agg_fixed<Fp2, 4>), dim3(nblocks(ntask * 4, 256)), b, 0, st, n, len, t, q, d_ids,
-                           d_l, d_iss_ids, n_iss, d_table, d_binf, d_outX, d_outY);  // G2 keys: not re-measured
+                           d_l, d_iss_ids, n_iss, d_table, wbits, d_binf, d_outX, d_outY);  // G2 keys: not re-measured
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -59,7 +59,7 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
                    size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
                    hipStream_t st);
 int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uint64_t* d_ids, const uint32_t* d_l,
-                     const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, const uint32_t* d_binf,
+                     const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
                      uint8_t* d_outX, uint8_t* d_outY, hipStream_t st);
 int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
                   uint8_t* d_out, hipStream_t st);
@@ -150,6 +150,7 @@ struct cc_ctx {
     size_t iss_n = 0, iss_q = 0;
     std::vector<uint64_t> iss_ids_host;
     DevBuf iss_ids, iss_aff, iss_inf, iss_table;
+    int iss_wbits = 8;  // window width of the issuer tables
     DevBuf agg_scratch;
     uint32_t rlc_key_host[8] = {0};
     // timing
@@ -1041,20 +1042,45 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
         memcpy(&enc[(r * (q + 1)) * ob], X + k * ob, ob);
         for (size_t j = 0; j < q; j++) memcpy(&enc[(r * (q + 1) + 1 + j) * ob], Y + (k * q + j) * ob, ob);
     }
-    if (c->iss_ids.ensure(n_iss * 8) || c->iss_aff.ensure(nb * aw * 4) || c->iss_inf.ensure(nb * 4) ||
-        c->iss_table.ensure(nb * tab_words(og, 8) * 4))
+    // the widest window whose tables fit the budget (CC_ISSUER_TABLE_GB, default 16 GiB of the 288 GB
+    // HBM; CC_ISSUER_WBITS forces one): t x nwin additions per aggregated key, nwin = ceil(256 / w)
+    static const double budget_gb = [] {
+        const char* e = getenv("CC_ISSUER_TABLE_GB");
+        return e ? atof(e) : 16.0;
+    }();
+    static const int force_wb = [] {
+        const char* e = getenv("CC_ISSUER_WBITS");
+        return e ? atoi(e) : 0;
+    }();
+    int wb = 8;
+    if (force_wb >= 8 && force_wb <= 16) {
+        wb = force_wb;
+    } else {
+        for (int cand : {16, 13, 12, 10})
+            if ((double)(nb * tab_words(og, cand) * 4) <= budget_gb * (double)(1ull << 30)) {
+                wb = cand;
+                break;
+            }
+    }
+    if (c->iss_ids.ensure(n_iss * 8) || c->iss_aff.ensure(nb * aw * 4) || c->iss_inf.ensure(nb * 4))
         return CC_ERR_HIP;
+    if (c->iss_table.ensure(nb * tab_words(og, wb) * 4)) {
+        (void)hipGetLastError();  // clear the failed allocation's error
+        wb = 8;                   // the wide table did not fit the free HBM
+        if (c->iss_table.ensure(nb * tab_words(og, wb) * 4)) return CC_ERR_HIP;
+    }
     cc_status s = decode_points_host(c, og, nb, enc.data(), c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>());
     if (s) return s;
     HIPCK(hipMemcpy(c->iss_ids.p, sid.data(), n_iss * 8, hipMemcpyHostToDevice));
     DevBuf pw;
-    if (pw.ensure(nb * tab_nwin(8) * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
-    KCK(cck_build_table(og, (int)nb, 8, c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>(), pw.as<uint32_t>(),
+    if (pw.ensure(nb * tab_nwin(wb) * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
+    KCK(cck_build_table(og, (int)nb, wb, c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>(), pw.as<uint32_t>(),
                         c->iss_table.as<uint32_t>(), c->stream));
     HIPCK(hipStreamSynchronize(c->stream));
     pw.release();
     c->iss_n = n_iss;
     c->iss_q = q;
+    c->iss_wbits = wb;
     c->iss_ids_host = sid;
     return CC_OK;
 }
@@ -1066,7 +1092,8 @@ static cc_status launch_vk_aggregate_ids(cc_ctx* c, size_t n, size_t len, size_t
     KCK(cck_lagrange(n, len, t, d_ids, c->lag.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     KCK(cck_vk_agg_fixed(oth_group(c->mode), n, len, t, (int)c->iss_q, d_ids, c->lag.as<uint32_t>(),
-                         c->iss_ids.as<uint64_t>(), (int)c->iss_n, c->iss_table.as<uint32_t>(), c->iss_inf.as<uint32_t>(),
+                         c->iss_ids.as<uint64_t>(), (int)c->iss_n, c->iss_table.as<uint32_t>(), c->iss_wbits,
+                         c->iss_inf.as<uint32_t>(),
                          d_oX, d_oY, st));
     if (c->timing) {
         (void)hipEventRecord(c->ev[2], st);

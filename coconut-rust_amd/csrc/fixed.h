@@ -6,8 +6,9 @@
 // nwin mixed additions and no doublings.  The shared-verkey tables use wbits = 16 (16 windows: half
 // the additions of 8-bit windows; 100 MB per G1 base, 200 MB per G2 base — the tables live in HBM and
 // every lookup is one random 96/192-byte read, which the ~8 TB/s HBM serves far faster than the
-// VALU-bound additions consume them); the issuer tables (hundreds of bases) and the one-off
-// cc_fixed_base_mul use wbits = 8.
+// VALU-bound additions consume them); the issuer tables (hundreds of bases) take the widest window
+// in {16, 13, 12, 10, 8} whose tables fit a memory budget (cc_set_issuers), the one-off
+// cc_fixed_base_mul wbits = 8.
 // An entry equal to the identity (only possible for a small-order base) is stored as (0, 0), which
 // lies on neither curve, and skipped.
 #pragma once
@@ -23,10 +24,14 @@ __host__ __device__ constexpr size_t ft_base_words(int wbits) {
     return (size_t)ft_nwin(wbits) * ft_went(wbits) * (sizeof(Aff<F>) / 4);
 }
 
-// window w of a canonical scalar given as 8 little-endian 32-bit limbs
+// window w of a canonical scalar given as 8 little-endian 32-bit limbs (wbits in [8, 16])
 DEV uint32_t ft_digit(const uint32_t k[8], int w, int wbits) {
     if (wbits == 16) return (k[w >> 1] >> (16 * (w & 1))) & 0xffffu;
-    return (k[w >> 2] >> (8 * (w & 3))) & 0xffu;
+    if (wbits == 8) return (k[w >> 2] >> (8 * (w & 3))) & 0xffu;
+    const int o = w * wbits, i = o >> 5, sh = o & 31;
+    uint32_t v = k[i] >> sh;
+    if (sh && i + 1 < 8) v |= k[i + 1] << (32 - sh);
+    return v & ((1u << wbits) - 1u);
 }
 
 template <class F>

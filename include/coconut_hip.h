@@ -137,8 +137,9 @@ cc_status cc_signature_aggregate_batch_device(cc_ctx* ctx, size_t n, size_t len,
 
 /* Issuer table for Verkey::aggregate at scale (BASELINE config 4: t = 67 of n = 100 issuers).  The
  * n_issuers verkeys (X: n_issuers x OtherGroup, Y: n_issuers x q x OtherGroup) and their signer ids
- * (unique) are decoded once and given fixed-base window tables in HBM (one-time cost); a batch then
- * passes only id lists.  cc_verkey_aggregate_ids(_device) computes, per credential, exactly
+ * (unique) are decoded once and given fixed-base window tables in HBM (one-time cost; the widest
+ * window whose tables fit 16 GiB, env CC_ISSUER_TABLE_GB: 13-bit, 11 GB, for 100 issuers x 7 G1
+ * keys); a batch then passes only id lists.  cc_verkey_aggregate_ids(_device) computes, per credential, exactly
  * Verkey::aggregate(t, [(id_k, &issuer[id_k])]) (signature.rs:483-526): first t entries, Lagrange
  * over the de-duplicated id set.  ids: n x len.  CC_ERR_DECODE if an id has no issuer verkey (host
  * form; the device form requires every id to be in the table). */

@@ -699,20 +699,32 @@ def _raw_mul(g, a, b):
     return r
 
 
-def fixed_sum(g, pts, scalars):
-    """k_vk_agg_fixed / msm_fixed: sum of 8-bit-window table entries (entries precomputed, uncounted)."""
+def issuer_wbits(nb, two, budget=16 << 30):
+    """capi.cpp cc_set_issuers: the widest window in {16, 13, 12, 10} whose tables (nb bases, affine
+    entries of 24 / 48 words) fit the default 16 GiB budget, else 8."""
+    for w in (16, 13, 12, 10):
+        if nb * ((256 + w - 1) // w) * ((1 << w) - 1) * (48 if two else 24) * 4 <= budget:
+            return w
+    return 8
+
+
+def fixed_sum(g, pts, scalars, wbits=8):
+    """k_vk_agg_fixed / msm_fixed: sum of wbits-window table entries (entries precomputed, uncounted)."""
     acc = g.inf()
+    nwin = (256 + wbits - 1) // wbits
     for P, k in zip(pts, scalars):
         if P is None:
             continue
-        acc = fixed_table_mul_add(g, acc, k, P, 0, 32)
+        acc = fixed_table_mul_add(g, acc, k, P, 0, nwin, wbits)
     return g.to_aff(acc)
 
 
-def aggregate_case(d, case):
-    """Signature::aggregate (Straus, SignatureGroup) + Verkey::aggregate (issuer tables, OtherGroup)."""
+def aggregate_case(d, case, n_issuers=100):
+    """Signature::aggregate (Straus, SignatureGroup) + Verkey::aggregate (issuer tables, OtherGroup;
+    window width as cc_set_issuers picks it for n_issuers x (q + 1) bases)."""
     gs, go = (G2, G1) if d["mode"] == "G2" else (G1, G2)
     t, q = d["threshold"], d["q"]
+    wb = issuer_wbits(n_issuers * (q + 1), go is G2)
     ids = case["ids"][:t]
     ls = [lagrange0(ids, i) for i in ids]
     s2 = [decode(gs, bytes.fromhex(h)) for h in case["sigma2"][:t]]
@@ -722,8 +734,8 @@ def aggregate_case(d, case):
     Xs = [decode(go, bytes.fromhex(h)) for h in case["X"][:t]]
     Ys = [[decode(go, bytes.fromhex(h)) for h in row] for row in case["Y"][:t]]
     C.take()
-    vkX = fixed_sum(go, Xs, ls)
-    vkY = [fixed_sum(go, [Ys[k][j] for k in range(t)], ls) for j in range(q)]
+    vkX = fixed_sum(go, Xs, ls, wb)
+    vkY = [fixed_sum(go, [Ys[k][j] for k in range(t)], ls, wb) for j in range(q)]
     fixed_m = C.take()
     return sig, vkX, vkY, {"straus_sigma2": straus_m, "fixed_verkey": fixed_m}
 
@@ -896,7 +908,8 @@ def main():
         "credentials_averaged": 1, "M_per_credential": cnt,
         "mads_per_credential": {k: v * 288 for k, v in cnt.items()},
         "note": "straus_sigma2 = Signature::aggregate (67-point G2 Straus MSM); fixed_verkey = Verkey::aggregate "
-                "(q+1 = 7 67-point G1 fixed-base MSMs from the issuer tables); case 0 of "
+                "(q+1 = 7 67-point G1 fixed-base MSMs from the issuer tables, 13-bit windows: the width "
+                "cc_set_issuers picks for 100 issuers x 7 keys); case 0 of "
                 "tests/golden/aggregate_g2_t67_subsets.json, outputs checked against the fixture"}
     with open(os.path.join(root, "tests", "golden", "pok_g2_q32.json")) as f:
         d = json.load(f)
