@@ -52,40 +52,76 @@ DEV void ld_aff_aos(Aff<F>& a, const uint32_t* p) {
 // ================================================================ Lagrange coefficients
 // l[(cred * t + i) * 8 ..]: canonical l_i(0) for the i-th of the first t ids of credential `cred`.
 // LT tasks (credential, i) per lane.
-// - The factors enter as raw integers, not Montgomery images: num and den both take one factor per
-//   other id, so the R^-1 each product picks up cancels in num / den (no conversion multiply).
+// - The factors enter as raw integers, not Montgomery images: num and den take the same number of
+//   factors, so the R^-1 each product picks up cancels in num / den (no conversion multiply).
+// - The numerator is shared: with P = the product of the credential's distinct ids, l_i =
+//   P / (x_i den_i), so a task multiplies only its t - 1 differences (P is formed once per
+//   credential a lane touches; a credential holding the id 0 takes the per-task numerator instead).
 // - The tasks' denominators share ONE Fermat inversion (Montgomery's trick: with
 //   P_q = den_0 ... den_{q-1}, l_q = (num_q P_q) / P_{q+1}, walking q down from 1 / P_cnt and
 //   multiplying den_q back in).
 // - The O(t^2) duplicate scan (HashSet semantics) runs once per credential a lane touches; a
 //   credential without repeated ids takes the plain product loop.
-template <int LT>
-__global__ void k_lagrange(size_t n, size_t len, size_t t, const uint64_t* __restrict__ ids, uint32_t* __restrict__ l) {
+// - kLds: the block's credentials' first t ids are staged in LDS first (the out-of-line products
+//   begin with s_waitcnt vmcnt(0), so a global id load per factor waited its full latency).
+template <int LT, bool kLds>
+__global__ __launch_bounds__(64) void k_lagrange(size_t n, size_t len, size_t t, const uint64_t* __restrict__ ids,
+                                                 uint32_t* __restrict__ l) {
+    extern __shared__ uint64_t sid[];
     const size_t first = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) * LT;
+    size_t c0 = 0;
+    if (kLds) {
+        const size_t b0 = blockIdx.x * (size_t)blockDim.x * LT;
+        const size_t b1 = b0 + (size_t)blockDim.x * LT < n * t ? b0 + (size_t)blockDim.x * LT : n * t;
+        c0 = b0 / t;
+        const size_t nc = (b1 - 1) / t - c0 + 1;
+        for (size_t e = threadIdx.x; e < nc * t; e += blockDim.x) sid[e] = ids[(c0 + e / t) * len + e % t];
+        __syncthreads();
+    }
     if (first >= n * t) return;
     const int cnt = (int)((n * t - first) < (size_t)LT ? (n * t - first) : (size_t)LT);
     Fm nump[LT], den[LT];
     Fm pre = fm_one();  // P_q (a Montgomery 1: the raw factors' R^-k cancel between num and den)
+    Fm prod = fm_one();  // the current credential's product of distinct ids
     size_t have = ~(size_t)0;
-    bool dups = false;
+    bool dups = false, zero = false;
 #pragma unroll
     for (int q = 0; q < LT; q++) {
         if (q >= cnt) break;
         const size_t task = first + q, cred = task / t, i = task % t;
-        const uint64_t* id = ids + cred * len;
+        const uint64_t* id = kLds ? sid + (cred - c0) * t : ids + cred * len;
         if (cred != have) {
             have = cred;
             dups = false;
+            zero = false;
             for (size_t j = 1; j < t && !dups; j++)
                 for (size_t k = 0; k < j; k++)
                     if (id[k] == id[j]) { dups = true; break; }
+            prod = fm_one();
+            for (size_t j = 0; j < t; j++) {
+                const uint64_t xj = id[j];
+                zero |= xj == 0;
+                if (dups) {
+                    bool seen = false;
+                    for (size_t k = 0; k < j; k++)
+                        if (id[k] == xj) { seen = true; break; }
+                    if (seen) continue;
+                }
+                Fm fxj;
+#pragma unroll
+                for (int k = 0; k < NR; k++) fxj.v[k] = 0;
+                fxj.v[0] = (uint32_t)xj;
+                fxj.v[1] = (uint32_t)(xj >> 32);
+                prod = fm_mul_v(prod, fxj);
+            }
         }
         const uint64_t xi = id[i];
-        Fm nm = fm_one(), dn = fm_one(), fxi;
+        Fm nm = fm_one(), fxi;
 #pragma unroll
         for (int k = 0; k < NR; k++) fxi.v[k] = 0;
         fxi.v[0] = (uint32_t)xi;
         fxi.v[1] = (uint32_t)(xi >> 32);
+        Fm dn = zero ? fm_one() : fxi;  // x_i den_i, or den_i with its own numerator
         for (size_t j = 0; j < t; j++) {
             const uint64_t xj = id[j];
             if (xj == xi) continue;
@@ -100,11 +136,11 @@ __global__ void k_lagrange(size_t n, size_t len, size_t t, const uint64_t* __res
             for (int k = 0; k < NR; k++) fxj.v[k] = 0;
             fxj.v[0] = (uint32_t)xj;
             fxj.v[1] = (uint32_t)(xj >> 32);
-            nm = fm_mul_v(nm, fxj);
+            if (zero) nm = fm_mul_v(nm, fxj);
             fm_sub(d, fxj, fxi);
             dn = fm_mul_v(dn, d);
         }
-        nump[q] = fm_mul_v(nm, pre);
+        nump[q] = fm_mul_v(zero ? nm : prod, pre);
         den[q] = dn;
         pre = fm_mul_v(pre, dn);
     }
@@ -595,12 +631,22 @@ int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t
         const char* e = getenv("CC_LAG_LT");
         return e ? atoi(e) : 4;
     }();
+    static const bool lds_ok = [] {
+        const char* e = getenv("CC_LAG_LDS");
+        return !(e && e[0] == '0');
+    }();
+    // ids of the credentials one block's 64 x lt tasks touch: at most 64 lt / t + 2 rows of t
+    const size_t lds = (64 * (size_t)lt + 2 * t) * 8;
+    const bool use_lds = lds_ok && lds <= 64 * 1024;
+    const unsigned nb = nblocks((n * t + lt - 1) / lt, 64);
     if (lt == 8)
-        hipLaunchKernelGGL(k_lagrange<8>, dim3(nblocks((n * t + 7) / 8, 64)), dim3(64), 0, st, n, len, t, d_ids, d_l);
+        hipLaunchKernelGGL((k_lagrange<8, false>), dim3(nb), dim3(64), 0, st, n, len, t, d_ids, d_l);
     else if (lt == 2)
-        hipLaunchKernelGGL(k_lagrange<2>, dim3(nblocks((n * t + 1) / 2, 64)), dim3(64), 0, st, n, len, t, d_ids, d_l);
+        hipLaunchKernelGGL((k_lagrange<2, false>), dim3(nb), dim3(64), 0, st, n, len, t, d_ids, d_l);
+    else if (use_lds)
+        hipLaunchKernelGGL((k_lagrange<4, true>), dim3(nb), dim3(64), lds, st, n, len, t, d_ids, d_l);
     else
-        hipLaunchKernelGGL(k_lagrange<4>, dim3(nblocks((n * t + 3) / 4, 64)), dim3(64), 0, st, n, len, t, d_ids, d_l);
+        hipLaunchKernelGGL((k_lagrange<4, false>), dim3(nb), dim3(64), 0, st, n, len, t, d_ids, d_l);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -179,3 +179,39 @@ def test_lagrange_batching_ragged_against_oracle(ctxs, oc, mode_name, t):
         assert oc.oc_verkey_aggregate(mode, ctypes.c_size_t(L), ctypes.c_size_t(t), ctypes.c_size_t(q), idarr,
                                       X, Y, oX, oY) == 0
         assert gX[r * ob:(r + 1) * ob] == oX.raw and gY[r * q * ob:(r + 1) * q * ob] == oY.raw, (r, row[:t])
+
+
+@pytest.mark.parametrize("t", [1, 2, 5])
+def test_lagrange_with_id_zero_against_oracle(ctxs, oc, t):
+    """An id equal to 0 zeroes the shared numerator product P, so such a credential takes the
+    per-task numerators in k_lagrange; Signature::aggregate must still equal the oracle's."""
+    import random
+    from coconut import signature_aggregate_batch
+    d = golden("aggregate_g2_t67_subsets.json")
+    ctx = ctxs[d["mode"]]
+    sigs = {}
+    for case in d["cases"]:
+        for k, i in enumerate(case["ids"]):
+            sigs[i] = (case["sigma1"][k], case["sigma2"][k])
+    pool = sorted(sigs)
+    rng = random.Random(77 + t)
+    L, n = 6, 7
+    rows, s1, s2 = [], [], []
+    for r in range(n):
+        src = rng.sample(pool, L)
+        row = list(src)
+        if r % 2 == 0:
+            row[rng.randrange(t)] = 0  # id 0 among the first t
+        if r == 3 and t > 2:
+            row[1] = row[0]            # and a repeated id
+        rows.append(row)
+        s1 += [sigs[i][0] for i in src]
+        s2 += [sigs[i][1] for i in src]
+    g1, g2 = signature_aggregate_batch(ctx, n, L, t, rows, _cat(s1), _cat(s2))
+    sb = 192
+    o1, o2 = ctypes.create_string_buffer(sb), ctypes.create_string_buffer(sb)
+    for r, row in enumerate(rows):
+        idarr = (ctypes.c_uint64 * L)(*row)
+        assert oc.oc_signature_aggregate(0, ctypes.c_size_t(L), ctypes.c_size_t(t), idarr, _cat(s1[r * L:(r + 1) * L]),
+                                         _cat(s2[r * L:(r + 1) * L]), o1, o2) == 0
+        assert g1[r * sb:(r + 1) * sb] == o1.raw and g2[r * sb:(r + 1) * sb] == o2.raw, (r, row[:t])
