@@ -11,6 +11,7 @@
 //                    Schnorr check MSM(g~, Y~_hidden.., J; responses.., chal) == T, then
 //                    J' = X~ + J + sum_revealed Y~_i m_i, written in the verify kernels' Miller-loop
 //                    operand layout so k_miller_* / k_fexp finish the 2-pairing check.
+#include <cmath>
 #include <cstdlib>
 
 #include "codec.h"
@@ -305,30 +306,27 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus(size_t ntask, size_t t, c
 // waits on is its table entry (the digit byte and the identity flag were two more dependent global
 // round trips; the out-of-line Fp2 products begin with s_waitcnt vmcnt(0), so a load cannot be
 // prefetched across them).
-template <int L2, bool kLds>
-__global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
-                                                           size_t pt_stride, size_t pt_jstride, size_t pt_step,
-                                                           const uint32_t* __restrict__ l, size_t l_div,
-                                                           uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
-    extern __shared__ int8_t sdig[];
+// one task's share on one lane pair: multiples of the bases k = pair, pair + NG, ... built and
+// batch-normalised, then the 65 windows over them into acc (pl form, this lane's half)
+template <bool kLds>
+DEV void straus_g2pl_pair(cc::Jac<pl::Fp2>& acc, int NG, int pair, int h, size_t task, size_t t,
+                          const uint8_t* __restrict__ pts, size_t pt_stride, size_t pt_jstride, size_t pt_step,
+                          const uint32_t* __restrict__ l, size_t l_div, uint32_t* __restrict__ scratch,
+                          int8_t* sdig_task) {
     using F = pl::Fp2;
     using T = FT<F>;
-    constexpr int L = 2 * L2;
     constexpr int JW = 3 * NL, PW = NL;  // one lane's half of a Jacobian entry / of an Fp2
-    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    const size_t task = g / L;
-    const int pair = (int)((g % L) >> 1), h = (int)(g & 1);
-    if (task >= ntask) return;  // uniform over the lane group (L divides the block)
     const size_t cred = task / l_div;
     const uint8_t* base = pts + cred * pt_stride + (task % l_div) * pt_jstride;
     const uint32_t* lk = l + cred * t * 8;
     uint32_t* ent = scratch + task * straus_words<Fp2>(t);
     uint32_t* pre = ent + t * 8 * (2 * JW);
-    int8_t* dig = kLds ? sdig + (threadIdx.x / L) * t * 65 : reinterpret_cast<int8_t*>(pre + t * 8 * (2 * PW));
+    int8_t* dig = kLds ? sdig_task : reinterpret_cast<int8_t*>(pre + t * 8 * (2 * PW));
+    jac_set_inf(acc);
     F acc_z;
     T::one(acc_z);
 #pragma unroll 1
-    for (size_t k = pair; k < t; k += L2) {
+    for (size_t k = pair; k < t; k += NG) {
         cc::Aff<cc::Fp2> P1;
         const bool ok = pl::pair_all(g2_decode(P1, base + k * pt_step));  // both lanes decode the point
         recode_w4(dig + k * 65, lk + k * 8);                            // both write the same digits
@@ -353,9 +351,9 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
     F inv;
     T::inv(inv, acc_z);
     if (t > (size_t)pair) {
-        const long long kmax = (long long)(((t - 1 - pair) / L2) * L2 + pair);
+        const long long kmax = (long long)(((t - 1 - pair) / NG) * NG + pair);
 #pragma unroll 1
-        for (long long kk = kmax; kk >= pair; kk -= L2) {
+        for (long long kk = kmax; kk >= pair; kk -= NG) {
             unsigned infm = 0;  // identity multiples of base kk (pair-uniform)
             for (int d = 7; d >= 0; d--) {
                 const size_t e = (size_t)kk * 8 + d;
@@ -387,14 +385,12 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
             }
         }
     }
-    cc::Jac<F> acc;
-    jac_set_inf(acc);
 #pragma unroll 1
     for (int win = 64; win >= 0; win--) {
         if (win != 64 && !jac_is_inf(acc))
             for (int z = 0; z < 4; z++) jac_dbl(acc, acc);
 #pragma unroll 1
-        for (size_t k = pair; k < t; k += L2) {
+        for (size_t k = pair; k < t; k += NG) {
             const int d = dig[k * 65 + win];
             if (!d) continue;
             const uint32_t* w = ent + ((k * 8 + (d < 0 ? -d : d) - 1) * 2 + h) * JW;
@@ -408,17 +404,77 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t
             jac_add_aff(acc, acc, e);
         }
     }
+}
+
+DEV void straus_g2pl_out(const cc::Jac<pl::Fp2>& acc, int h, uint8_t* out) {
+    cc::Aff<pl::Fp2> r;
+    const bool fin = jac_to_aff(r, acc);
+    const Fp xs = pl::swp(r.x.c), ys = pl::swp(r.y.c);
+    cc::Aff<cc::Fp2> o;
+    o.x.a = h ? xs : r.x.c;
+    o.x.b = h ? r.x.c : xs;
+    o.y.a = h ? ys : r.y.c;
+    o.y.b = h ? r.y.c : ys;
+    if (!h) g2_encode(out, o, fin);
+}
+
+template <int L2, bool kLds>
+__global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
+                                                           size_t pt_stride, size_t pt_jstride, size_t pt_step,
+                                                           const uint32_t* __restrict__ l, size_t l_div,
+                                                           uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
+    extern __shared__ int8_t sdig[];
+    constexpr int L = 2 * L2;
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t task = g / L;
+    const int pair = (int)((g % L) >> 1), h = (int)(g & 1);
+    if (task >= ntask) return;  // uniform over the lane group (L divides the block)
+    cc::Jac<pl::Fp2> acc;
+    straus_g2pl_pair<kLds>(acc, L2, pair, h, task, t, pts, pt_stride, pt_jstride, pt_step, l, l_div, scratch,
+                           sdig + (threadIdx.x / L) * t * 65);
     pl::pair_group_sum<L>(acc);  // over the L2 pairs of the task
-    if (pair == 0) {
-        cc::Aff<F> r;
-        const bool fin = jac_to_aff(r, acc);
-        const Fp xs = pl::swp(r.x.c), ys = pl::swp(r.y.c);
-        cc::Aff<cc::Fp2> o;
-        o.x.a = h ? xs : r.x.c;
-        o.x.b = h ? r.x.c : xs;
-        o.y.a = h ? ys : r.y.c;
-        o.y.b = h ? r.y.c : ys;
-        if (!h) g2_encode(out + task * 192, o, fin);
+    if (pair == 0) straus_g2pl_out(acc, h, out + task * 192);
+}
+
+// The same with G lane pairs per task for any G (not only powers of two): blockDim = 2G floor(256 /
+// 2G), the pairs' partial sums meet in LDS and pair 0 adds them.  G is chosen so the launch's waves
+// fill whole rounds of the 2 waves/SIMD the registers allow (cck_msm_straus): 10,000 tasks at 8 pairs
+// are 2,500 waves, 1.22 rounds of an MI355X's 2,048 slots, the last one a fifth full.
+__global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl_g(int G, size_t ntask, size_t t,
+                                                             const uint8_t* __restrict__ pts, size_t pt_stride,
+                                                             size_t pt_jstride, size_t pt_step,
+                                                             const uint32_t* __restrict__ l, size_t l_div,
+                                                             uint32_t* __restrict__ scratch,
+                                                             uint8_t* __restrict__ out) {
+    constexpr int JW = 3 * NL;
+    __shared__ uint32_t red[256 * JW];
+    const int L = 2 * G, TB = (int)blockDim.x / L;
+    const int tib = (int)threadIdx.x / L, lit = (int)threadIdx.x % L;
+    const size_t task = (size_t)blockIdx.x * TB + tib;
+    const int pair = lit >> 1, h = lit & 1;
+    const bool active = task < ntask;  // pair-uniform; every lane reaches the barrier
+    cc::Jac<pl::Fp2> acc;
+    if (active)
+        straus_g2pl_pair<false>(acc, G, pair, h, task, t, pts, pt_stride, pt_jstride, pt_step, l, l_div, scratch,
+                                nullptr);
+    else
+        jac_set_inf(acc);
+    {
+        const uint32_t* aw = reinterpret_cast<const uint32_t*>(&acc);
+        uint32_t* my = red + threadIdx.x * JW;
+        for (int c = 0; c < JW; c++) my[c] = aw[c];
+    }
+    __syncthreads();
+    if (active && pair == 0) {
+#pragma unroll 1
+        for (int p = 1; p < G; p++) {
+            cc::Jac<pl::Fp2> o;
+            uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+            const uint32_t* src = red + (tib * L + 2 * p + h) * JW;
+            for (int c = 0; c < JW; c++) ow[c] = src[c];
+            jac_add(acc, acc, o);
+        }
+        straus_g2pl_out(acc, h, out + task * 192);
     }
 }
 
@@ -667,6 +723,35 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
         return !(e && e[0] == '0');
     }();
     const size_t lds = (256 / L) * t * 65;  // digits of the block's 16 tasks
+    static const int force_g = [] {
+        const char* e = getenv("CC_STRAUS_G");
+        return e ? atoi(e) : -1;
+    }();
+    int G = force_g;
+    if (group != 1 && G < 0) {
+        // pairs per task: the fewest rounds of wave slots (2 waves/SIMD), then the least work a wave
+        int dev = 0, cus = 256;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const double slots = (double)cus * 4 * 2;
+        double best = 0;
+        for (int c = 4; c <= 16; c++) {
+            const double per = (double)((t + c - 1) / c) * 73.0 + 143.0;  // additions a pair (model)
+            const int tb = 256 / (2 * c);
+            const double waves = (double)((ntask + tb - 1) / tb) * ((2 * c * tb + 63) / 64);
+            const double est = per * std::ceil(waves / slots);
+            if (G < 0 || est < best) {
+                G = c;
+                best = est;
+            }
+        }
+    }
+    if (group != 1 && G > 0) {
+        const int L = 2 * G, tb = 256 / L;
+        hipLaunchKernelGGL(k_msm_straus_g2pl_g, dim3((unsigned)((ntask + tb - 1) / tb)), dim3(tb * L), 0, st, G, ntask,
+                           t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     if (group == 1)
         hipLaunchKernelGGL((k_msm_straus<Fp, L>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l,
                            l_div, d_scratch, d_out);
