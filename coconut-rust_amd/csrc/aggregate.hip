@@ -478,6 +478,147 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl_g(int G, size_t ntas
     }
 }
 
+// SigG2 PoK prep split by WAVE: a block of 256 lanes serves 128 proofs; its waves 0-1 (role A) decode
+// sigma', add g~ resp_0 and the first `split` hidden responses' table terms and run chal J, waves
+// 2-3 (role B) the other hidden responses, -T and J'.  The partial Schnorr sums meet in LDS and role A
+// checks their sum.  Roles are wave-uniform (no divergence); the launch is 2 waves per proof group,
+// so the 65,536-proof batch fills the 2 waves/SIMD the registers allow instead of 1.
+constexpr int PK_PB = 128;  // proofs per block
+__global__ __launch_bounds__(256, 2) void k_prep_pok_split(size_t n, int q, int r, int split,
+                                                          const uint8_t* __restrict__ s1b,
+                                                          const uint8_t* __restrict__ s2b,
+                                                          const uint8_t* __restrict__ Jb,
+                                                          const uint8_t* __restrict__ Tb,
+                                                          const uint8_t* __restrict__ resp,
+                                                          const uint8_t* __restrict__ chal,
+                                                          const uint8_t* __restrict__ rev_msgs,
+                                                          const uint32_t* __restrict__ rev_idx,
+                                                          const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                          const uint32_t* __restrict__ table, int wbits,
+                                                          const uint32_t* __restrict__ binf,
+                                                          uint32_t* __restrict__ prep, uint32_t* __restrict__ flags,
+                                                          uint32_t* __restrict__ jtab) {
+    using FS_ = Fp2;
+    using FO = Fp;
+    constexpr int JW = sizeof(Jac<FO>) / 4;
+    __shared__ uint32_t part[PK_PB][JW + 1];  // role B's partial Schnorr sum and flags
+    const bool roleB = threadIdx.x >= PK_PB;   // wave-uniform
+    const int slot_in_block = (int)(threadIdx.x & (PK_PB - 1));
+    const size_t i = blockIdx.x * (size_t)PK_PB + slot_in_block;
+    const bool active = i < n;
+    constexpr int SB = ebytes<FS_>(), OB = ebytes<FO>();
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    Jac<FO> acc;
+    jac_set_inf(acc);
+    if (active) {
+        Aff<FO> Ja;
+        const bool Jok = decode_pt<FO>(Ja, Jb + i * OB);
+        const uint8_t* rp = resp + i * (size_t)(q - r + 1) * 48;
+        const int nwin = ft_nwin(wbits);
+        Fr k;
+        if (!roleB) {
+            {
+                Aff<FS_> a;
+                if (!decode_pt<FS_>(a, s1b + i * SB)) fl |= 1u;
+                const Fp* pa = reinterpret_cast<const Fp*>(&a);
+                for (int c = 0; c < 4; c++) st_fp(S, S_Q1 + c, i, pa[c]);
+                if (!decode_pt<FS_>(a, s2b + i * SB)) fl |= 2u;
+                FT<FS_>::neg(a.y, a.y);
+                for (int c = 0; c < 4; c++) st_fp(S, S_Q2 + c, i, pa[c]);
+            }
+            fr_from_be48(k, rp);
+            if (!binf[q]) ft_add<FO>(acc, k.v, table, wbits, q, 0, nwin);  // table base q = g~
+        }
+        // hidden responses: role A the first `split`, role B the rest
+        int slot = 1, hid = 0;
+        for (int h = 0; h < q; h++) {
+            bool revealed = false;
+            for (int z = 0; z < r; z++) revealed |= rev_idx[z] == (uint32_t)h;
+            if (revealed) continue;
+            const bool mine = roleB ? hid >= split : hid < split;
+            hid++;
+            if (mine) {
+                fr_from_be48(k, rp + (size_t)slot * 48);
+                if (!binf[h]) ft_add<FO>(acc, k.v, table, wbits, h, 0, nwin);
+            }
+            slot++;
+        }
+        if (!roleB) {
+            // J * chal in fixed 4-bit windows (k_prep_pok)
+            fr_from_be48(k, chal + i * 48);
+            if (Jok) {
+                auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * JW + w) * n + i]; };
+                Jac<FO> t;
+                jac_from_aff(t, Ja);
+#pragma unroll 1
+                for (int d = 1; d <= 15; d++) {
+                    if (d > 1) jac_add_aff(t, t, Ja);
+                    const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
+                    for (int w = 0; w < JW; w++) tab(d, w) = tw[w];
+                }
+                Jac<FO> sacc;
+                jac_set_inf(sacc);
+#pragma unroll 1
+                for (int win = 63; win >= 0; win--) {
+                    for (int b = 0; b < 4; b++) jac_dbl(sacc, sacc);
+                    const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
+                    if (d) {
+                        uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
+                        for (int w = 0; w < JW; w++) tw[w] = tab((int)d, w);
+                        jac_add(sacc, sacc, t);
+                    }
+                }
+                jac_add(acc, acc, sacc);
+            }
+        } else {
+            Aff<FO> Ta;
+            if (decode_pt<FO>(Ta, Tb + i * OB)) {
+                FT<FO>::neg(Ta.y, Ta.y);
+                jac_add_aff(acc, acc, Ta);
+            }
+            // J' = X~ + J + sum_revealed Y~_i m_i; P1 = J' in line-evaluation form (X Z, Y, Z^3)
+            Jac<FO> jp;
+            if (Xinf) {
+                jac_set_inf(jp);
+            } else {
+                Aff<FO> x;
+                ld_aff_aos<FO>(x, Xaff);
+                jac_from_aff(jp, x);
+            }
+            if (Jok) jac_add_aff(jp, jp, Ja);
+            for (int z = 0; z < r; z++) {
+                Fr m;
+                fr_from_be48(m, rev_msgs + ((size_t)i * r + z) * 48);
+                const int h = (int)rev_idx[z];
+                if (!binf[h]) ft_add<FO>(jp, m.v, table, wbits, h, 0, nwin);
+            }
+            if (jac_is_inf(jp)) fl |= 4u;
+            Fp t;
+            fp_mul(t, jp.x, jp.z);
+            st_fp(S, S_P1, i, t);
+            st_fp(S, S_P1 + 1, i, jp.y);
+            fp_sqr(t, jp.z);
+            fp_mul(t, t, jp.z);
+            st_fp(S, S_P1 + 2, i, t);
+        }
+    }
+    if (roleB) {
+        const uint32_t* aw = reinterpret_cast<const uint32_t*>(&acc);
+        for (int c = 0; c < JW; c++) part[slot_in_block][c] = aw[c];
+        part[slot_in_block][JW] = fl;
+    }
+    __syncthreads();
+    if (roleB || !active) return;
+    Jac<FO> o;
+    uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+    for (int c = 0; c < JW; c++) ow[c] = part[slot_in_block][c];
+    fl |= part[slot_in_block][JW];
+    jac_add(acc, acc, o);
+    if (!jac_is_inf(acc)) fl |= 8u;
+    flags[i] = fl;
+}
+
 // ================================================================ issuer-table Verkey::aggregate
 // Verkey::aggregate (signature.rs:483-526) over a resident issuer table: the bases X~_k, Y~_k,j of
 // the n_iss issuers are FIXED, so cc_set_issuers gives each one an 8-bit window table (32 x 255
@@ -804,7 +945,25 @@ int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const ui
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
     // d_jtab: 15 Jacobian points of the other group per element (<= 15 x 72 words a proof)
-    if (mode == 0)
+    static const bool split_ok = [] {
+        const char* e = getenv("CC_POK_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    if (mode == 0 && split_ok) {
+        // hidden responses for role A: balance nwin (1 + split) + ~233 (chal J) against
+        // nwin (hidden - split) + nwin r + ~10 (mixed-addition units)
+        const int hidden = q - r, nwin = ft_nwin(wbits);
+        int split = (nwin * (hidden + r - 1) - 223) / (2 * nwin);
+        static const int force_split = [] {
+            const char* e = getenv("CC_POK_SPLIT_N");
+            return e ? atoi(e) : -1;
+        }();
+        if (force_split >= 0) split = force_split;
+        split = split < 0 ? 0 : (split > hidden ? hidden : split);
+        hipLaunchKernelGGL(k_prep_pok_split, dim3(nblocks(n, PK_PB)), dim3(2 * PK_PB), 0, st, n, q, r, split, d_s1,
+                           d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf,
+                           d_prep, d_flags, d_jtab);
+    } else if (mode == 0)
         hipLaunchKernelGGL((k_prep_pok<Fp2, Fp, 2>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
                            d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags, d_jtab);
     else
