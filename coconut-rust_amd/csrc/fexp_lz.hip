@@ -11,6 +11,8 @@
 #ifdef CC_HOT_INLINE  // build option (Makefile HOT_INLINE=1): inline every Fp multiplication
 #define CC_FP_INLINE 1
 #endif
+#include <cstdlib>
+
 #include "codec.h"
 #include "tower_lz.h"
 
@@ -185,6 +187,15 @@ template <class I>
 DEV FR z4_expand(const Z4& x, const F2R& n0, const F2R& n1, const I& inv) {
     return {{reduce(mulr(n0, inv)), reduce(mulr(n1, inv))}, {x.b0, x.b1}, {x.c0, x.c1}};
 }
+// a compressed snapshot (4 Fp2 = 52 packed words a lane) in the park rows, while the squaring loops
+// leave LDS free
+DEV void park4(Park lds, const Z4& x) {
+    pack_fq<FB>(lds, 0, x.b0.c);
+    pack_fq<FB>(lds, PW, x.b1.c);
+    pack_fq<FB>(lds, 2 * PW, x.c0.c);
+    pack_fq<FB>(lds, 3 * PW, x.c1.c);
+}
+DEV Z4 unpark4(Park lds) { return {unp(lds, 0), unp(lds, 1), unp(lds, 2), unp(lds, 3)}; }
 DEV void st_z4(const Zs& K, int base, size_t i, const Z4& x) {
     st_z(K, base + 0, i, x.b0);
     st_z(K, base + 2, i, x.b1);
@@ -202,6 +213,7 @@ DEV Z4 ld_z4(const Zs& K, int base, size_t i) {
 #else
 #define FXP_ARG
 #endif
+template <bool kSnapLds>
 DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i FXP_ARG) {
     FXP_T(t_sq);
     Z4 c{ld_z(src, 4, i), ld_z(src, 6, i), ld_z(src, 8, i), ld_z(src, 10, i)};
@@ -212,7 +224,8 @@ DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i FXP_ARG) {
     st_z4(K, 0, i, c);
 #pragma unroll 1
     for (int k = 16; k < 48; k++) z4_sqr(c);
-    st_z4(K, 12, i, c);
+    if (kSnapLds) park4(lds, c);
+    else st_z4(K, 12, i, c);
 #pragma unroll 1
     for (int k = 48; k < 57; k++) z4_sqr(c);
     FXP_ADD(18, t_sq);
@@ -223,10 +236,15 @@ DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i FXP_ARG) {
         z4_num(n0, n1, d16, s);
         st_z(K, 8, i, n0);
         st_z(K, 10, i, n1);
-        s = ld_z4(K, 12, i);
+        s = kSnapLds ? unpark4(lds) : ld_z4(K, 12, i);
         z4_num(n0, n1, d48, s);
-        st_z(K, 20, i, n0);
-        st_z(K, 22, i, n1);
+        if (kSnapLds) {  // the park rows after the snapshot's four
+            pack_fq<FB>(lds, 4 * PW, n0.c);
+            pack_fq<FB>(lds, 5 * PW, n1.c);
+        } else {
+            st_z(K, 20, i, n0);
+            st_z(K, 22, i, n1);
+        }
     }
     z4_num(n0, n1, d57, c);
     const auto p1 = mulr(d16, d48);
@@ -238,7 +256,8 @@ DEV void zx_pow_x(Zs src, Zs dst, Zs K, Park lds, size_t i FXP_ARG) {
     const auto iv = inv(p2);
     st12(dst, i, z4_expand(c, n0, n1, mulr(iv, p1)));  // y = g^(2^57), waits in dst
     const auto iv2 = mulr(iv, d57);                   // (d16 d48)^-1
-    park12(lds, z4_expand(ld_z4(K, 12, i), ld_z(K, 20, i), ld_z(K, 22, i), mulr(iv2, d16)));  // g^(2^48)
+    park12(lds, z4_expand(kSnapLds ? unpark4(lds) : ld_z4(K, 12, i), kSnapLds ? unp(lds, 4) : ld_z(K, 20, i),
+                          kSnapLds ? unp(lds, 5) : ld_z(K, 22, i), mulr(iv2, d16)));  // g^(2^48)
     {
         const FR acc = f12_mul_lds(z4_expand(ld_z4(K, 0, i), ld_z(K, 8, i), ld_z(K, 10, i), mulr(iv2, d48)),
                                    lds);  // g^(2^16) g^(2^48)
@@ -304,6 +323,7 @@ __constant__ static const ZStep kChain[16] = {
 }  // namespace
 
 // fbuf: Miller output f (12 x 32 SoA, 12 slots); scratch: 84 lazy Fp slots (F, T, A, S, R, K)
+template <bool kSnapLds>
 __global__ __launch_bounds__(256, 2) void k_fexp_lz(size_t n, const uint32_t* __restrict__ fbuf,
                                                  int32_t* __restrict__ scratch, const uint32_t* __restrict__ flags,
                                                  uint8_t* __restrict__ verdicts, uint8_t* __restrict__ gt_out) {
@@ -330,9 +350,9 @@ __global__ __launch_bounds__(256, 2) void k_fexp_lz(size_t n, const uint32_t* __
         FXP_T(t_st);
         if (z.kind == 0) zx_mul(a, z.opa, b, z.opb, d, lds, i);
 #ifdef CC_FEXP_PROF
-        else if (z.kind == 1) zx_pow_x(a, d, K, lds, i, fxp);
+        else if (z.kind == 1) zx_pow_x<kSnapLds>(a, d, K, lds, i, fxp);
 #else
-        else if (z.kind == 1) zx_pow_x(a, d, K, lds, i);
+        else if (z.kind == 1) zx_pow_x<kSnapLds>(a, d, K, lds, i);
 #endif
         else zx_cube(a, d, i);
         FXP_ADD(2 + s, t_st);
@@ -362,7 +382,15 @@ extern "C" int cck_fexp_prof_read(unsigned long long* out, size_t nwaves) {
 extern "C" int cck_fexp_lz(size_t n, const uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags,
                            uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
     if (!n) return 0;
-    hipLaunchKernelGGL(cc::lz::k_fexp_lz, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, st, n, d_f,
-                       reinterpret_cast<int32_t*>(d_scratch), d_flags, d_verdicts, d_gt);
+    static const bool snap = [] {
+        const char* e = getenv("CC_FEXP_SNAP");
+        return !(e && e[0] == '0');
+    }();
+    if (snap)
+        hipLaunchKernelGGL(cc::lz::k_fexp_lz<true>, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, st, n, d_f,
+                           reinterpret_cast<int32_t*>(d_scratch), d_flags, d_verdicts, d_gt);
+    else
+        hipLaunchKernelGGL(cc::lz::k_fexp_lz<false>, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, st, n,
+                           d_f, reinterpret_cast<int32_t*>(d_scratch), d_flags, d_verdicts, d_gt);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
