@@ -128,9 +128,18 @@ static __device__ __noinline__ void zx_in(const uint32_t* fbuf, size_t n, Zs dst
 }
 static __device__ __noinline__ void zx_inv(Zs src, Zs dst, size_t i) { st12(dst, i, rest(f12_inv(ld12(src, i)))); }
 // dst <- op_a(a) * op_b(b)
+// (a == b, opb in {id, conj}: a is read back from LDS, not reloaded from the scratch; conj is an
+// involution commuting with the Frobenius maps)
 DEV void zx_mul(Zs a, int opa, Zs b, int opb, Zs dst, Park lds, size_t i) {
     park12(lds, zapply(ld12(b, i), opb));
-    const FR x = zapply(ld12(a, i), opa);
+    FR y;
+    if (a.p == b.p && (opb == OP_ID || opb == OP_CONJ)) {
+        y = unpark12(lds);
+        if (opb == OP_CONJ) y = f12_conj(y);
+    } else {
+        y = ld12(a, i);
+    }
+    const FR x = zapply(y, opa);
     st12(dst, i, f12_mul_lds(x, lds));
 }
 // dst <- src^3 (cyclotomic)
