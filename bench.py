@@ -46,6 +46,9 @@ UBENCH = os.path.join(ROOT, "profiles", "r02_ubench_int.jsonl")
 HBM_PEAK_GBS = 8000.0
 OPCOUNT = os.path.join(ROOT, "tests", "fixtures", "opcount.json")
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
+# per-mode rocprofv3 evidence of the current build (tools/gpu_modes_prof.sh): kernel-trace stats and the
+# PMC passes of one bench step, summarised per kernel by tools/pmc_summary.py
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r03", "modes")
 
 
 def peak_mad_per_s():
@@ -66,14 +69,20 @@ def opcounts(key):
         return json.load(f)["configs"][key]["M_per_credential"]
 
 
-def pmc(kernel_key):
-    """Per-launch PMC figures of the same build (profiles/r02/pmc_summary.json, separate rocprofv3
-    --pmc passes, tools/pmc_summary.py): HBM bytes = 2 x FETCH_SIZE (gfx950 counts half of wide reads,
-    MI355X_MICROARCH.md §HBM) + WRITE_SIZE, and VALU wave-instructions per CU per clock."""
-    try:
-        with open(PMC_SUMMARY) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
+def pmc(kernel_key, mode=None):
+    """Per-launch PMC figures of the same build (profiles/r03/modes/<mode>/pmc_summary.json, else
+    profiles/r02/pmc_summary.json; separate rocprofv3 --pmc passes, tools/pmc_summary.py): HBM bytes =
+    2 x FETCH_SIZE (gfx950 counts half of wide reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, and VALU
+    wave-instructions per CU per clock."""
+    d = None
+    for path in ([os.path.join(PROFILE_DIR, mode, "pmc_summary.json")] if mode else []) + [PMC_SUMMARY]:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            break
+        except (OSError, ValueError):
+            continue
+    if d is None:
         return {}
     for name, c in d.items():
         if kernel_key in name:
@@ -84,6 +93,45 @@ def pmc(kernel_key):
                 out["valu_issue_per_cu_clk"] = round(c["SQ_INSTS_VALU"] / 256 / (c["GRBM_GUI_ACTIVE"] / 8), 3)
             return out
     return {}
+
+
+def kernel_pmc_report(mode):
+    """North_star's per-kernel rocprof report for one bench mode: every product kernel's average
+    duration (rocprofv3 --kernel-trace --stats), HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE,
+    MI355X_MICROARCH.md gfx950 correction), achieved HBM GB/s, VALU issue (wave-instructions per CU per
+    clock; 1.0 = every SIMD issuing a wave64 VALU op every 4 clocks) and the fraction of wave-cycles
+    waiting.  Read from profiles/r03/modes/<mode>/ (committed evidence of the same build)."""
+    import csv
+    d = os.path.join(PROFILE_DIR, mode)
+    try:
+        with open(os.path.join(d, "pmc_summary.json")) as f:
+            pm = json.load(f)
+        with open(os.path.join(d, "rocprof_kernel_stats.csv")) as f:
+            st = {r["Name"]: r for r in csv.DictReader(f)}
+    except (OSError, ValueError):
+        return None
+    out = {}
+    for name, c in pm.items():
+        if not any(k in name for k in ("k_", "cc::")) or "k_table" in name or "k_decode_points" in name \
+                or "k_fixed_mul" in name or "k_subgroup<" in name:
+            continue  # setup kernels (tables, synthetic data) are outside the timed step
+        r = st.get(name)
+        if not r:
+            continue
+        ms = float(r["AverageNs"]) / 1e6
+        row = {"avg_ms": round(ms, 4), "calls": int(r["Calls"])}
+        if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+            tb = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+            row["hbm_bytes_per_launch"] = round(tb)
+            row["hbm_GB_s"] = round(tb / (ms * 1e-3) / 1e9, 1) if ms > 0 else None
+            row["hbm_frac"] = round(tb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if ms > 0 else None
+        if "SQ_INSTS_VALU" in c and c.get("GRBM_GUI_ACTIVE"):
+            row["valu_issue_per_cu_clk"] = round(c["SQ_INSTS_VALU"] / 256 / (c["GRBM_GUI_ACTIVE"] / 8), 3)
+        if c.get("SQ_WAVE_CYCLES"):
+            row["wait_frac"] = round(c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"], 3)
+        short = name.split("(")[0].replace("void ", "")
+        out[short] = row
+    return {"source": f"profiles/r03/modes/{mode}/ (rocprofv3 kernel stats + PMC passes)", "kernels": out}
 
 
 def cpu_info():
@@ -121,6 +169,9 @@ def _free_port():
     return p
 
 
+BACKEND = os.environ.get("COCONUT_BENCH_BACKEND", "nccl")  # bench.py --backend
+
+
 def _dist_setup():
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,8 +180,9 @@ def _dist_setup():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        if BACKEND == "nccl":  # RCCL over xGMI: one GPU per rank
+            torch.cuda.set_device(local)
+        dist.init_process_group(BACKEND)
     return world, rank, local, dist
 
 
@@ -138,7 +190,7 @@ def _max_over_ranks(x, dist, dev):
     if not dist:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    t = torch.tensor([x], dtype=torch.float64, device=dev if BACKEND == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -148,36 +200,72 @@ def rand_fr(rng):
     return int.from_bytes(rng.bytes(32), "big") % R_ORDER
 
 
+CORRUPT_KINDS = ("sigma2+G", "msg+1", "swapped", "sigma1=O", "sigma2=O", "wrong vk")
+
+
 def make_verify_batch(ctx, mode, n, q, seed, bad_every=16):
-    """sigma_1 = k G, sigma_2 = k (x + sum y_j m_j) G; verkey X = x g~, Y_j = y_j g~, g~ = gk G'.
-    mode 0 = SigG2 (sigma in G2), 1 = SigG1.  bad_every = 0: all valid."""
+    """one shared verkey AGGREGATED 3-of-5 (Shamir-shared issuer keys, the
+    product's Verkey::aggregate on the GPU, checked against x g~ before use); per-credential messages
+    uniform; sigma_1 = k G, sigma_2 = k (x + sum y_j m_j) G.  Every bad_every-th credential is corrupted,
+    the kinds split evenly over CORRUPT_KINDS: sigma_2 + G, one m_j + 1, sigma_1 <-> sigma_2 swapped,
+    sigma_1 = O, sigma_2 = O, signed under another verkey.  mode 0 = SigG2 (sigma in G2), 1 = SigG1.
+    bad_every = 0: all valid."""
     import numpy as np
     import coconut
     rng = np.random.default_rng(seed)
-    x = rand_fr(rng)
-    y = [rand_fr(rng) for _ in range(q)]
-    gk = rand_fr(rng) or 1
     og, sg = (1, 2) if mode == 0 else (2, 1)
     gen = {1: coconut.G1_GENERATOR, 2: coconut.G2_GENERATOR}
-    ob = 97 if og == 1 else 192
-    sc = b"".join(v.to_bytes(48, "big") for v in [x * gk % R_ORDER] + [yj * gk % R_ORDER for yj in y] + [gk])
-    pts = coconut.fixed_base_mul(ctx, og, gen[og], sc)
-    X, Y, g_tilde = pts[:ob], pts[ob:ob * (q + 1)], pts[ob * (q + 1):]
+    ob, sb = (97, 192) if mode == 0 else (192, 97)
+    # 3-of-5 Shamir keygen (reference keygen.rs:48-72 trusted_party_SSS_keygen): degree-2 polynomials
+    fx = [rand_fr(rng) for _ in range(3)]
+    fy = [[rand_fr(rng) for _ in range(3)] for _ in range(q)]
+    ev = lambda c, i: (c[0] + c[1] * i + c[2] * i * i) % R_ORDER  # noqa: E731
+    x, y = fx[0], [c[0] for c in fy]
+    gk = rand_fr(rng) or 1
+    ids = [1, 2, 3, 4, 5]
+    sc = b"".join(v.to_bytes(48, "big") for i in ids for v in [ev(fx, i) * gk % R_ORDER] +
+                  [ev(c, i) * gk % R_ORDER for c in fy])
+    keys = coconut.fixed_base_mul(ctx, og, gen[og], sc)
+    g_tilde = coconut.fixed_base_mul(ctx, og, gen[og], gk.to_bytes(48, "big"))
+    use = [0, 2, 4]  # issuers 1, 3, 5
+    kX = b"".join(keys[(u * (q + 1)) * ob:(u * (q + 1) + 1) * ob] for u in use)
+    kY = b"".join(keys[(u * (q + 1) + 1) * ob:(u * (q + 1) + 1 + q) * ob] for u in use)
+    X, Y = coconut.verkey_aggregate_batch(ctx, 1, 3, 3, q, [[ids[u] for u in use]], kX, kY)
+    want = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(v.to_bytes(48, "big") for v in
+                                                              [x * gk % R_ORDER] + [v * gk % R_ORDER for v in y]))
+    if X + Y != want:
+        raise SystemExit("aggregated verkey differs from g~ * master secret — refusing to build the batch")
     m = [[rand_fr(rng) for _ in range(q)] for _ in range(n)]
     ks = [rand_fr(rng) or 1 for _ in range(n)]
-    e1, e2 = bytearray(), bytearray()
+    x_other = (x + 0x5EED) % R_ORDER
+    e1, e2 = [], []
     expect = np.ones(n, dtype=np.uint8)
+    kind = [None] * n
     for i in range(n):
         e = ks[i] * ((x + sum(yj * mj for yj, mj in zip(y, m[i]))) % R_ORDER) % R_ORDER
+        k1 = ks[i]
         if bad_every and i % bad_every == bad_every - 1:
-            e = (e + 1) % R_ORDER  # sigma_2 + G: must be rejected
+            kd = CORRUPT_KINDS[(i // bad_every) % len(CORRUPT_KINDS)]
+            kind[i] = kd
             expect[i] = 0
-        e1 += ks[i].to_bytes(48, "big")
-        e2 += e.to_bytes(48, "big")
-    s1 = coconut.fixed_base_mul(ctx, sg, gen[sg], bytes(e1))
-    s2 = coconut.fixed_base_mul(ctx, sg, gen[sg], bytes(e2))
+            if kd == "sigma2+G":
+                e = (e + 1) % R_ORDER
+            elif kd == "msg+1":
+                m[i][0] = (m[i][0] + 1) % R_ORDER
+            elif kd == "swapped":
+                k1, e = e, k1
+            elif kd == "sigma1=O":
+                k1 = 0
+            elif kd == "sigma2=O":
+                e = 0
+            else:  # wrong vk
+                e = ks[i] * ((x_other + sum(yj * mj for yj, mj in zip(y, m[i]))) % R_ORDER) % R_ORDER
+        e1.append(k1.to_bytes(48, "big"))
+        e2.append(e.to_bytes(48, "big"))
+    s1 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e1))
+    s2 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e2))
     msgs = b"".join(v.to_bytes(48, "big") for row in m for v in row)
-    return dict(X=X, Y=Y, g_tilde=g_tilde, s1=s1, s2=s2, msgs=msgs, expect=expect, mode=mode, q=q, n=n)
+    return dict(X=X, Y=Y, g_tilde=g_tilde, s1=s1, s2=s2, msgs=msgs, expect=expect, mode=mode, q=q, n=n, kind=kind)
 
 
 def to_dev(b, dev):
@@ -217,29 +305,38 @@ def cpu_verify_rate(batch, threads, target_s):
     return k / dt, k, dt, agree
 
 
-def cpu_baseline_verify(batch, value):
+def cpu_baseline_verify(batch, value, what="shared vk"):
+    """The CPU path timed on this box's host cores in the same run.  The pool grants one GPU's job a
+    share of the host (OMP_NUM_THREADS = 16 CPUs per GPU; it kills jobs that run wider), so the timed
+    figure is that share; the whole host (nproc CPUs) is single_thread x nproc scaled by the measured
+    per-thread efficiency of the share — an extrapolation, labelled as one.  gpu_over_cpu compares with
+    that whole-host figure (the conservative ratio); gpu_over_cpu_share with the timed share."""
     model, nproc, aff = cpu_info()
     thr = host_threads()
     v_mt, k_mt, dt_mt, ok_mt = cpu_verify_rate(batch, thr, target_s=2.0)
     v_1, k_1, dt_1, ok_1 = cpu_verify_rate(batch, 1, target_s=3.0)
+    eff = min(1.0, v_mt / (thr * v_1)) if thr > 1 else 1.0
+    host = v_1 * nproc * eff
     layout = "SigG2" if batch["mode"] == 0 else "SigG1"
     return {
         "value": round(v_mt, 1), "unit": "credentials/s", "cores": thr, "kind": "port",
-        "sample": f"{k_mt} credentials of the timed batch (q={batch['q']}, shared vk, {layout}) on {thr} threads "
+        "sample": f"{k_mt} credentials of the timed batch (q={batch['q']}, {what}, {layout}) on {thr} threads "
                   f"in {dt_mt:.2f} s, plus {k_1} on 1 thread in {dt_1:.2f} s; oracle/c bls_oracle.c oc_verify_batch "
-                  f"(test infrastructure); verdicts agree with construction: {ok_mt and ok_1}",
+                  f"(per-credential verify, test infrastructure); verdicts agree with construction: {ok_mt and ok_1}",
         "single_thread": round(v_1, 1),
+        "per_thread_efficiency": round(eff, 3),
         "nproc": nproc, "affinity_cpus": aff, "cpu_model": model,
-        "threads_note": "threads = the CPU share this box grants per GPU (OMP_NUM_THREADS / affinity); "
-                        "all_cores_extrapolated = single_thread x nproc (linear, an upper bound for the host)",
-        "all_cores_extrapolated": round(v_1 * nproc, 1),
-        "gpu_over_cpu": round(value / v_mt, 1),
-        "gpu_over_all_cores_extrapolated": round(value / (v_1 * nproc), 2),
+        "threads_note": f"timed on the {thr}-CPU share this box grants per GPU (OMP_NUM_THREADS); the pool does "
+                        f"not allow a job to load all {nproc} host CPUs, so the whole host is extrapolated: "
+                        "single_thread x nproc x per_thread_efficiency",
+        "all_cores_extrapolated": round(host, 1),
+        "gpu_over_cpu": round(value / host, 2),
+        "gpu_over_cpu_share": round(value / v_mt, 1),
     }
 
 
 # ---------------------------------------------------------------- modes
-def kernel_table(phase_ms, n, counts, in_bytes_per_cred, peak, prep_kernel="k_prep_sigg2_pair"):
+def kernel_table(phase_ms, n, counts, in_bytes_per_cred, peak, prep_kernel="k_prep_sigg2_pair", mode=None):
     """Per-kernel roofline: algorithmic M (tests/fixtures/opcount.json) x 288 mads x n / kernel time.
     PMC columns only where the committed summary holds that exact kernel (prep_kernel names it)."""
     out = {}
@@ -251,7 +348,7 @@ def kernel_table(phase_ms, n, counts, in_bytes_per_cred, peak, prep_kernel="k_pr
                "frac": round(ach / peak, 4)}
         if k == "prep":
             row["input_GB_s"] = round(n * in_bytes_per_cred / (ms * 1e-3) / 1e9, 2)
-        row.update(pmc({"prep": prep_kernel, "miller": "k_miller", "fexp": "k_fexp"}[k]))
+        row.update(pmc({"prep": prep_kernel, "miller": "k_miller", "fexp": "k_fexp"}[k], mode))
         out[k] = row
     return out
 
@@ -322,8 +419,9 @@ def bench_verify(args, mode):
         peak = peak_mad_per_s()
         phase_ms = phase / max(args.steps, 1)
         sb = 192 if mode == 0 else 97
+        mname = "verify" if mode == 0 else "verify-g1"
         kt = kernel_table(phase_ms, n, counts, 2 * sb + q * 48, peak,
-                          "k_prep_sigg2_pair" if mode == 0 else "k_prep_sigg1_pair")
+                          "k_prep_sigg2_pair" if mode == 0 else "k_prep_sigg1_pair", mname)
         dom = max(kt, key=lambda k: kt[k]["ms"])
         ms_per_step = elapsed / args.steps * 1e3
         total_mads = sum(counts.values()) * MADS_PER_M * n
@@ -335,7 +433,8 @@ def bench_verify(args, mode):
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None,
             "dtype": "int32/u32 (pairing kernels: 14 signed 28-bit-radix limbs, lazy; elsewhere 12x32-bit Montgomery; integer-only)",
-            "data": "synthetic (seeded; sigma = k*G, k*(x+sum y m)*G built on the GPU; 1/16 corrupted)",
+            "data": "synthetic (seeded, SURVEY.md §8d config 2: verkey aggregated 3-of-5 on the GPU; sigma = k*G, "
+                    "k*(x+sum y m)*G built on the GPU; 1/16 corrupted, split evenly over " + ", ".join(CORRUPT_KINDS) + ")",
             "config": {"workload": f"config2: batch of {n:,} Signature::verify per GPU, msg_count=6, shared "
                                    f"aggregated verkey, {layout}",
                        "credentials_per_gpu": n, "msg_count": q, "parallelism": f"shard-by-credential x{world}"},
@@ -343,13 +442,14 @@ def bench_verify(args, mode):
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),
-                         "traffic_unit": "HBM-side bytes per launch (PMC, profiles/r02/pmc_summary.json)",
+                         "traffic_unit": "HBM-side bytes per launch (PMC, 2 x FETCH_SIZE + WRITE_SIZE)",
                          "algorithmic_mads_per_credential": round(counts[dom] * MADS_PER_M),
                          "opcount_fixture": "tests/fixtures/opcount.json (tools/opcount.py)",
                          "whole_step_frac": round(total_mads / (ms_per_step * 1e-3) / peak, 4),
                          "hbm_view_GBs": round(n * (2 * sb + q * 48 + 1) / (ms_per_step * 1e-3) / 1e9, 3),
                          "hbm_peak_GBs": HBM_PEAK_GBS},
             "kernels": kt,
+            "rocprof_kernels": kernel_pmc_report(mname),
             "pcie_inclusive": {"value": round(pcie_rate, 1), "unit": "credentials/s",
                                "note": "cc_verify_batch with host buffers: H2D of the serialized batch + D2H "
                                        "of verdicts included (not `value`)"},
@@ -439,34 +539,74 @@ def bench_rlc(args):
             ach = counts[k] * MADS_PER_M * n / (ms * 1e-3) if ms > 0 else 0.0
             kt[k] = {"ms": round(float(ms), 3), "achieved_Tmad_s": round(ach / 1e12, 3), "frac": round(ach / peak, 4)}
         out["kernels"] = kt
+        rk = kernel_pmc_report("rlc")
+        out["rocprof_kernels"] = rk
+        mk = (rk or {}).get("kernels", {}).get("cc::lz::k_miller<2, false, 1>", {})
         out["roofline"] = {"bound": "valu-int", "kernel": "miller (one-pair Miller + bucket pairs)",
                            "achieved": kt["miller"]["achieved_Tmad_s"], "peak": round(peak / 1e12, 3),
                            "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)", "frac": kt["miller"]["frac"],
-                           "traffic": None, "algorithmic_mads_per_credential": round(counts["miller"] * MADS_PER_M),
+                           "traffic": mk.get("hbm_bytes_per_launch"),
+                           "traffic_unit": "HBM-side bytes per launch of the credentials' one-pair Miller kernel (PMC)",
+                           "algorithmic_mads_per_credential": round(counts["miller"] * MADS_PER_M),
                            "opcount_fixture": "tests/fixtures/opcount.json rlc_sigg2_q16",
                            "note": "the batch's one final exponentiation (single element, latency-bound) and the "
                                    "all-gather are outside the three phases but inside ms_per_step"}
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline_verify(batch, value, "shared vk, per-credential verify")
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
     ctx.close()
 
 
+def bench_stub(args):
+    """The multi-rank skeleton without a GPU (tests/test_bench_cli.py): relaunch, rendezvous, barrier,
+    timed loop of a CPU stub step, max over ranks, one JSON line from rank 0.  Not a measurement."""
+    import numpy as np
+    world, rank, local, dist = _dist_setup()
+    a = np.arange(1 << 16, dtype=np.uint64)
+    for _ in range(args.warmup):
+        a = (a * 6364136223846793005 + 1) & 0xFFFFFFFF
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        a = (a * 6364136223846793005 + 1) & 0xFFFFFFFF
+    if dist:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, dist, "cpu")
+    if rank == 0:
+        print(json.dumps({"metric": "stub (CPU skeleton check, not a measurement)", "value": None, "unit": None,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(el / max(args.steps, 1) * 1e3, 4), "backend": BACKEND,
+                          "scaling": "weak"}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
+    global BACKEND
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
+                    help="torch.distributed backend for --gpus N (default nccl = RCCL; gloo: CPU skeleton tests)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=0, help="credentials per GPU per step (0 = the config's size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mode", choices=["verify", "verify-g1", "rlc", "aggregate", "pok"], default="verify")
+    ap.add_argument("--mode", choices=["verify", "verify-g1", "rlc", "aggregate", "pok", "stub"], default="verify")
     args = ap.parse_args()
+    if args.backend:
+        BACKEND = args.backend
+        os.environ["COCONUT_BENCH_BACKEND"] = args.backend  # inherited by the relaunched ranks
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # one process per GPU: relaunch under torch.distributed.run BEFORE any GPU call (no exec from a
         # process that touched the GPU: this one has not), and exit with its status
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
                "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
         return subprocess.call(cmd)
+    if args.mode == "stub":
+        return bench_stub(args)
     if args.mode == "verify":
         return bench_verify(args, 0)
     if args.mode == "verify-g1":

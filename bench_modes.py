@@ -194,6 +194,8 @@ def bench_aggregate(args):
         k_sig = counts["straus_sigma2"] * MADS_PER_M * n / (sig_ms * 1e-3)
         k_vk = counts["fixed_verkey"] * MADS_PER_M * n / (vk_ms * 1e-3)
         dom, ach = ("signature_msm", k_sig) if sig_ms >= vk_ms else ("verkey_msm", k_vk)
+        from bench import kernel_pmc_report
+        rk = kernel_pmc_report("aggregate")
         out = {
             "metric": "aggregated credentials/sec (Signature::aggregate + Verkey::aggregate, t=67 of n=100)",
             "value": round(value, 1), "unit": "credentials/s", "n_gpus": world, "steps": args.steps,
@@ -206,10 +208,15 @@ def bench_aggregate(args):
                        "parallelism": f"shard-by-credential x{world}"},
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 3),
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
-                         "frac": round(ach / peak, 4), "traffic": None},
+                         "frac": round(ach / peak, 4),
+                         "traffic": (rk or {}).get("kernels", {}).get(
+                             "k_msm_straus_g2pl_g" if dom == "signature_msm" else "k_vk_agg_fixed<cc::Fp, 8>",
+                             {}).get("hbm_bytes_per_launch"),
+                         "traffic_unit": "HBM-side bytes per launch (PMC, 2 x FETCH_SIZE + WRITE_SIZE)"},
             "kernels": {"lagrange_ms": round((phases["sig"][0]) / args.steps, 3),
                         "signature_msm_ms": round(sig_ms, 3), "verkey_msm_ms": round(vk_ms, 3),
                         "signature_msm_frac": round(k_sig / peak, 4), "verkey_msm_frac": round(k_vk / peak, 4)},
+            "rocprof_kernels": rk,
             "setup": {"issuer_tables_ms": round(iss_ms, 1), "synthetic_data_s": round(gen_s, 2)},
         }
         if not args.no_cpu_baseline and world == 1:
@@ -282,10 +289,10 @@ def bench_pok(args):
         raise SystemExit("PoK verdicts disagree with construction — refusing to report a number")
     value = n * world * args.steps / el
     if rank == 0:
-        from bench import kernel_table, cpu_info
+        from bench import kernel_table, cpu_info, kernel_pmc_report
         peak = peak_mad_per_s()
         counts = opcounts("pok_sigg2_q32_r8")
-        kt = kernel_table(phase_ms, n, counts, 2 * 192 + 2 * 97 + (nresp + 1 + r) * 48, peak, "k_prep_pok")
+        kt = kernel_table(phase_ms, n, counts, 2 * 192 + 2 * 97 + (nresp + 1 + r) * 48, peak, "k_prep_pok", "pok")
         dom = max(kt, key=lambda k: kt[k]["ms"])
         out = {
             "metric": "verified PoK-of-signature proofs/sec (msg_count=32, 8 revealed)",
@@ -298,8 +305,10 @@ def bench_pok(args):
                        "parallelism": f"shard-by-proof x{world}"},
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
-                         "frac": kt[dom]["frac"], "traffic": None},
+                         "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),
+                         "traffic_unit": "HBM-side bytes per launch (PMC, 2 x FETCH_SIZE + WRITE_SIZE)"},
             "kernels": kt,
+            "rocprof_kernels": kernel_pmc_report("pok"),
             "setup": {"synthetic_data_s": round(gen_s, 2)},
         }
         if not args.no_cpu_baseline and world == 1:

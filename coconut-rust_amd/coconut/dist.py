@@ -39,15 +39,22 @@ def _dist():
 
 
 def gather_partials(part, group=None):
-    """All-gather the per-rank partials (one tensor of PARTIAL_WORDS int32 each) -> (stacked, k)."""
+    """All-gather the per-rank partials (one tensor of PARTIAL_WORDS int32 each) -> (stacked, k).
+    Over RCCL ("nccl") the device tensors are gathered in place (580 B per rank over xGMI); over gloo
+    (CPU transport: tests, hosts without RCCL) a device partial crosses through host memory and the
+    gathered partials return to its device."""
     import torch
     dist = _dist()
     world = dist.get_world_size(group) if dist else 1
     if world == 1:
         return part.reshape(1, -1), 1
-    parts = [torch.empty_like(part) for _ in range(world)]
-    dist.all_gather(parts, part, group=group)
-    return torch.stack(parts), world
+    dev = part.device
+    host = dev.type != "cpu" and dist.get_backend(group) == "gloo"
+    src = part.cpu() if host else part
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src, group=group)
+    out = torch.stack(parts)
+    return (out.to(dev) if host else out), world
 
 
 def rlc_accept(engine, group=None) -> bool:

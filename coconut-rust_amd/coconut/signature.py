@@ -188,6 +188,22 @@ class Context:
         check(lib.cc_set_issuers(self.h, len(ids), q, ctypes.c_void_p(ids.ctypes.data), px, py), "cc_set_issuers")
         self._iss_q = q
 
+    def set_table_bits(self, verkey_bits: int = 0, issuer_bits: int = 0):
+        """Window widths of the tables later set_verkey / set_issuers calls build (0: by memory)."""
+        check(lib.cc_set_table_bits(self.h, verkey_bits, issuer_bits), "cc_set_table_bits")
+
+    def table_bits(self):
+        """(verkey table bits, issuer table bits) of the current tables (0: none)."""
+        v, i = ctypes.c_int(), ctypes.c_int()
+        check(lib.cc_table_bits(self.h, ctypes.byref(v), ctypes.byref(i)), "cc_table_bits")
+        return v.value, i.value
+
+    def device_error(self, stream=None) -> int:
+        """CC_DEVERR_* bits raised by *_device calls since the last read (synchronises the stream)."""
+        v = ctypes.c_uint32()
+        check(lib.cc_device_error(self.h, stream, ctypes.byref(v)), "cc_device_error")
+        return v.value
+
     def num_devices(self) -> int:
         n = ctypes.c_int()
         check(lib.cc_ctx_num_devices(self.h, ctypes.byref(n)), "cc_ctx_num_devices")

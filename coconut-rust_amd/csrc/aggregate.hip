@@ -300,19 +300,11 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus(size_t ntask, size_t t, c
 // G2 point in 3 Fp a lane (2 waves/SIMD) and halves each lane's share of every Fp2 product.  L2 pairs
 // per task take the bases k = pair, pair + L2, ...; the scratch layout is straus_words<Fp2> with
 // each entry's two halves side by side ([entry][half][words]).
-//
-// kLds: the task's digits live in LDS (t x 65 bytes a task, dynamic shared memory), and a digit whose
-// multiple is the identity is zeroed there after normalisation, so the only global load an addition
-// waits on is its table entry (the digit byte and the identity flag were two more dependent global
-// round trips; the out-of-line Fp2 products begin with s_waitcnt vmcnt(0), so a load cannot be
-// prefetched across them).
-// one task's share on one lane pair: multiples of the bases k = pair, pair + NG, ... built and
+// One task's share on one lane pair: multiples of the bases k = pair, pair + NG, ... built and
 // batch-normalised, then the 65 windows over them into acc (pl form, this lane's half)
-template <bool kLds>
 DEV void straus_g2pl_pair(cc::Jac<pl::Fp2>& acc, int NG, int pair, int h, size_t task, size_t t,
                           const uint8_t* __restrict__ pts, size_t pt_stride, size_t pt_jstride, size_t pt_step,
-                          const uint32_t* __restrict__ l, size_t l_div, uint32_t* __restrict__ scratch,
-                          int8_t* sdig_task) {
+                          const uint32_t* __restrict__ l, size_t l_div, uint32_t* __restrict__ scratch) {
     using F = pl::Fp2;
     using T = FT<F>;
     constexpr int JW = 3 * NL, PW = NL;  // one lane's half of a Jacobian entry / of an Fp2
@@ -321,7 +313,7 @@ DEV void straus_g2pl_pair(cc::Jac<pl::Fp2>& acc, int NG, int pair, int h, size_t
     const uint32_t* lk = l + cred * t * 8;
     uint32_t* ent = scratch + task * straus_words<Fp2>(t);
     uint32_t* pre = ent + t * 8 * (2 * JW);
-    int8_t* dig = kLds ? sdig_task : reinterpret_cast<int8_t*>(pre + t * 8 * (2 * PW));
+    int8_t* dig = reinterpret_cast<int8_t*>(pre + t * 8 * (2 * PW));
     jac_set_inf(acc);
     F acc_z;
     T::one(acc_z);
@@ -354,7 +346,6 @@ DEV void straus_g2pl_pair(cc::Jac<pl::Fp2>& acc, int NG, int pair, int h, size_t
         const long long kmax = (long long)(((t - 1 - pair) / NG) * NG + pair);
 #pragma unroll 1
         for (long long kk = kmax; kk >= pair; kk -= NG) {
-            unsigned infm = 0;  // identity multiples of base kk (pair-uniform)
             for (int d = 7; d >= 0; d--) {
                 const size_t e = (size_t)kk * 8 + d;
                 cc::Jac<F> J;
@@ -362,7 +353,6 @@ DEV void straus_g2pl_pair(cc::Jac<pl::Fp2>& acc, int NG, int pair, int h, size_t
                 uint32_t* jw = reinterpret_cast<uint32_t*>(&J);
                 for (int c = 0; c < JW; c++) jw[c] = w[c];
                 const bool inf = jac_is_inf(J);
-                infm |= (inf ? 1u : 0u) << d;
                 if (!inf) {
                     F pz, zi, zi2;
                     for (int c = 0; c < PW; c++) pz.c.v[c] = pre[(e * 2 + h) * PW + c];
@@ -376,13 +366,6 @@ DEV void straus_g2pl_pair(cc::Jac<pl::Fp2>& acc, int NG, int pair, int h, size_t
                 for (int c = 0; c < 2 * PW; c++) w[c] = jw[c];  // this half's affine x, y
                 w[2 * PW] = inf ? 1u : 0u;
             }
-            if (kLds && infm) {
-                int8_t* dk = dig + kk * 65;
-                for (int win = 0; win < 65; win++) {
-                    const int d = dk[win];
-                    if (d && ((infm >> ((d < 0 ? -d : d) - 1)) & 1u)) dk[win] = 0;
-                }
-            }
         }
     }
 #pragma unroll 1
@@ -394,7 +377,7 @@ DEV void straus_g2pl_pair(cc::Jac<pl::Fp2>& acc, int NG, int pair, int h, size_t
             const int d = dig[k * 65 + win];
             if (!d) continue;
             const uint32_t* w = ent + ((k * 8 + (d < 0 ? -d : d) - 1) * 2 + h) * JW;
-            if (!kLds && w[2 * PW]) continue;  // identity multiple (pair-uniform: both halves carry the flag)
+            if (w[2 * PW]) continue;  // identity multiple (pair-uniform: both halves carry the flag)
             cc::Aff<F> e;
             for (int c = 0; c < PW; c++) {
                 e.x.c.v[c] = w[c];
@@ -418,26 +401,8 @@ DEV void straus_g2pl_out(const cc::Jac<pl::Fp2>& acc, int h, uint8_t* out) {
     if (!h) g2_encode(out, o, fin);
 }
 
-template <int L2, bool kLds>
-__global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl(size_t ntask, size_t t, const uint8_t* __restrict__ pts,
-                                                           size_t pt_stride, size_t pt_jstride, size_t pt_step,
-                                                           const uint32_t* __restrict__ l, size_t l_div,
-                                                           uint32_t* __restrict__ scratch, uint8_t* __restrict__ out) {
-    extern __shared__ int8_t sdig[];
-    constexpr int L = 2 * L2;
-    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    const size_t task = g / L;
-    const int pair = (int)((g % L) >> 1), h = (int)(g & 1);
-    if (task >= ntask) return;  // uniform over the lane group (L divides the block)
-    cc::Jac<pl::Fp2> acc;
-    straus_g2pl_pair<kLds>(acc, L2, pair, h, task, t, pts, pt_stride, pt_jstride, pt_step, l, l_div, scratch,
-                           sdig + (threadIdx.x / L) * t * 65);
-    pl::pair_group_sum<L>(acc);  // over the L2 pairs of the task
-    if (pair == 0) straus_g2pl_out(acc, h, out + task * 192);
-}
-
-// The same with G lane pairs per task for any G (not only powers of two): blockDim = 2G floor(256 /
-// 2G), the pairs' partial sums meet in LDS and pair 0 adds them.  G is chosen so the launch's waves
+// G lane pairs per task for any G (not only powers of two): blockDim = 2G floor(256 / 2G), the
+// pairs' partial sums meet in LDS and pair 0 adds them.  G is chosen so the launch's waves
 // fill whole rounds of the 2 waves/SIMD the registers allow (cck_msm_straus): 10,000 tasks at 8 pairs
 // are 2,500 waves, 1.22 rounds of an MI355X's 2,048 slots, the last one a fifth full.
 __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl_g(int G, size_t ntask, size_t t,
@@ -455,8 +420,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl_g(int G, size_t ntas
     const bool active = task < ntask;  // pair-uniform; every lane reaches the barrier
     cc::Jac<pl::Fp2> acc;
     if (active)
-        straus_g2pl_pair<false>(acc, G, pair, h, task, t, pts, pt_stride, pt_jstride, pt_step, l, l_div, scratch,
-                                nullptr);
+        straus_g2pl_pair(acc, G, pair, h, task, t, pts, pt_stride, pt_jstride, pt_step, l, l_div, scratch);
     else
         jac_set_inf(acc);
     {
@@ -624,9 +588,11 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_split(size_t n, int q, int 
 // the n_iss issuers are FIXED, so cc_set_issuers gives each one an 8-bit window table (32 x 255
 // affine multiples, the layout of the shared-verkey tables) and every Lagrange-weighted MSM is a
 // fixed-base sum: t x 32 mixed additions, no doublings.  Task = (credential, j): j = 0 -> X~,
-// j = 1..q -> Y~_{j-1}.  Issuer ids are sorted; each entry's id is found by binary search (the
-// host entry point has checked they all exist).  Table entries that are the identity (possible only
-// for small-order bases) are stored as (0, 0), which is on neither curve, and skipped.
+// j = 1..q -> Y~_{j-1}.  Issuer ids are sorted; each entry's id is found by binary search.  An id
+// that is not in the table (the host entry point rejects those before launching; the device entry
+// point cannot) makes the task write the identity and raise bit CC_DEVERR_UNKNOWN_ID in *err.  Table
+// entries that are the identity (possible only for small-order bases) are stored as (0, 0), which is
+// on neither curve, and skipped.
 template <class F, int L>
 __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size_t t, int q,
                                                       const uint64_t* __restrict__ ids,
@@ -634,7 +600,8 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
                                                       const uint64_t* __restrict__ iss_ids, int n_iss,
                                                       const uint32_t* __restrict__ table, int wbits,
                                                       const uint32_t* __restrict__ binf,
-                                                      uint8_t* __restrict__ outX, uint8_t* __restrict__ outY) {
+                                                      uint8_t* __restrict__ outX, uint8_t* __restrict__ outY,
+                                                      uint32_t* __restrict__ err) {
     const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const size_t task = g / L;
     const int lane = (int)(g % L);
@@ -643,6 +610,7 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
     const int j = (int)(task % (q + 1));
     Jac<F> acc;
     jac_set_inf(acc);
+    int bad = 0;
 #pragma unroll 1
     for (size_t k = lane; k < t; k += L) {
         const uint64_t id = ids[cred * len + k];
@@ -651,12 +619,22 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
             const int mid = (lo + hi) >> 1;
             if (iss_ids[mid] < id) lo = mid + 1; else hi = mid;
         }
+        if (lo >= n_iss || iss_ids[lo] != id) {  // no issuer verkey for this id
+            bad = 1;
+            continue;
+        }
         const int b = lo * (q + 1) + j;
         if (binf[b]) continue;
         ft_add<F>(acc, l + (cred * t + k) * 8, table, wbits, b, 0, ft_nwin(wbits));
     }
     lane_group_sum<F, L>(acc);
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) bad |= __shfl_xor(bad, o, L);
     if (lane) return;
+    if (bad) {
+        atomicOr(err, 1u);  // CC_DEVERR_UNKNOWN_ID
+        jac_set_inf(acc);
+    }
     Aff<F> r;
     const bool fin = jac_to_aff(r, acc);
     uint8_t* o = j == 0 ? outX + cred * ebytes<F>() : outY + (cred * q + (j - 1)) * ebytes<F>();
@@ -824,26 +802,15 @@ extern "C" {
 
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st) {
     if (!n || !t) return 0;
-    static const int lt = [] {
-        const char* e = getenv("CC_LAG_LT");
-        return e ? atoi(e) : 4;
-    }();
-    static const bool lds_ok = [] {
-        const char* e = getenv("CC_LAG_LDS");
-        return !(e && e[0] == '0');
-    }();
-    // ids of the credentials one block's 64 x lt tasks touch: at most 64 lt / t + 2 rows of t
+    constexpr int lt = 4;  // tasks per lane: 3.96 / 3.62 / 4.10 ms for 2 / 4 / 8 at config 4
+    // ids of the credentials one block's 64 x lt tasks touch: at most 64 lt / t + 2 rows of t; past
+    // 64 KiB (t > 3,968) the ids are read from global memory
     const size_t lds = (64 * (size_t)lt + 2 * t) * 8;
-    const bool use_lds = lds_ok && lds <= 64 * 1024;
     const unsigned nb = nblocks((n * t + lt - 1) / lt, 64);
-    if (lt == 8)
-        hipLaunchKernelGGL((k_lagrange<8, false>), dim3(nb), dim3(64), 0, st, n, len, t, d_ids, d_l);
-    else if (lt == 2)
-        hipLaunchKernelGGL((k_lagrange<2, false>), dim3(nb), dim3(64), 0, st, n, len, t, d_ids, d_l);
-    else if (use_lds)
-        hipLaunchKernelGGL((k_lagrange<4, true>), dim3(nb), dim3(64), lds, st, n, len, t, d_ids, d_l);
+    if (lds <= 64 * 1024)
+        hipLaunchKernelGGL((k_lagrange<lt, true>), dim3(nb), dim3(64), lds, st, n, len, t, d_ids, d_l);
     else
-        hipLaunchKernelGGL((k_lagrange<4, false>), dim3(nb), dim3(64), 0, st, n, len, t, d_ids, d_l);
+        hipLaunchKernelGGL((k_lagrange<lt, false>), dim3(nb), dim3(64), 0, st, n, len, t, d_ids, d_l);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -853,88 +820,49 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
                    size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
                    hipStream_t st) {
     if (!ntask) return 0;
-    constexpr int L = 16;
-    dim3 g(nblocks(ntask * L, 256)), b(256);
-    static const int l2 = [] {
-        const char* e = getenv("CC_STRAUS_L2");
-        return e ? atoi(e) : L / 2;
-    }();
-    static const bool lds_ok = [] {
-        const char* e = getenv("CC_STRAUS_LDS");
-        return !(e && e[0] == '0');
-    }();
-    const size_t lds = (256 / L) * t * 65;  // digits of the block's 16 tasks
-    static const int force_g = [] {
-        const char* e = getenv("CC_STRAUS_G");
-        return e ? atoi(e) : -1;
-    }();
-    int G = force_g;
-    if (group != 1 && G < 0) {
-        // pairs per task: the fewest rounds of wave slots (2 waves/SIMD), then the least work a wave
-        int dev = 0, cus = 256;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const double slots = (double)cus * 4 * 2;
-        double best = 0;
-        for (int c = 4; c <= 16; c++) {
-            const double per = (double)((t + c - 1) / c) * 73.0 + 143.0;  // additions a pair (model)
-            const int tb = 256 / (2 * c);
-            const double waves = (double)((ntask + tb - 1) / tb) * ((2 * c * tb + 63) / 64);
-            const double est = per * std::ceil(waves / slots);
-            if (G < 0 || est < best) {
-                G = c;
-                best = est;
-            }
-        }
-    }
-    if (group != 1 && G > 0) {
-        const int L = 2 * G, tb = 256 / L;
-        hipLaunchKernelGGL(k_msm_straus_g2pl_g, dim3((unsigned)((ntask + tb - 1) / tb)), dim3(tb * L), 0, st, G, ntask,
-                           t, d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
+    if (group == 1) {
+        constexpr int L = 16;
+        hipLaunchKernelGGL((k_msm_straus<Fp, L>), dim3(nblocks(ntask * L, 256)), dim3(256), 0, st, ntask, t, d_pts,
+                           pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    if (group == 1)
-        hipLaunchKernelGGL((k_msm_straus<Fp, L>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride, pt_step, d_l,
-                           l_div, d_scratch, d_out);
-    else if (l2 == 4)
-        hipLaunchKernelGGL((k_msm_straus_g2pl<4, false>), dim3(nblocks(ntask * 8, 256)), b, 0, st, ntask, t, d_pts,
-                           pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
-    else if (l2 == 16)
-        hipLaunchKernelGGL((k_msm_straus_g2pl<16, false>), dim3(nblocks(ntask * 32, 256)), b, 0, st, ntask, t, d_pts,
-                           pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
-    else if (lds_ok && lds <= 80 * 1024) {  // two blocks a CU (the 2 waves/SIMD the registers allow)
-        static const bool attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_msm_straus_g2pl<L / 2, true>),
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     80 * 1024) == hipSuccess;
-        if (!attr) return -1;
-        hipLaunchKernelGGL((k_msm_straus_g2pl<L / 2, true>), g, b, lds, st, ntask, t, d_pts, pt_stride, pt_jstride,
-                           pt_step, d_l, l_div, d_scratch, d_out);
-    } else
-        hipLaunchKernelGGL((k_msm_straus_g2pl<L / 2, false>), g, b, 0, st, ntask, t, d_pts, pt_stride, pt_jstride,
-                           pt_step, d_l, l_div, d_scratch, d_out);
+    // G2: lane pairs per task G chosen for the fewest rounds of wave slots (2 waves/SIMD), then the least
+    // work a wave (a pair's work modelled as ceil(t / G) 73 + 143 additions)
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const double slots = (double)cus * 4 * 2;
+    int G = 0;
+    double best = 0;
+    for (int c = 4; c <= 16; c++) {
+        const double per = (double)((t + c - 1) / c) * 73.0 + 143.0;
+        const int tb = 256 / (2 * c);
+        const double waves = (double)((ntask + tb - 1) / tb) * ((2 * c * tb + 63) / 64);
+        const double est = per * std::ceil(waves / slots);
+        if (!G || est < best) {
+            G = c;
+            best = est;
+        }
+    }
+    const int L = 2 * G, tb = 256 / L;
+    hipLaunchKernelGGL(k_msm_straus_g2pl_g, dim3((unsigned)((ntask + tb - 1) / tb)), dim3(tb * L), 0, st, G, ntask, t,
+                       d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uint64_t* d_ids, const uint32_t* d_l,
                      const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
-                     uint8_t* d_outX, uint8_t* d_outY, hipStream_t st) {
+                     uint8_t* d_outX, uint8_t* d_outY, uint32_t* d_err, hipStream_t st) {
     if (!n) return 0;
     constexpr int L = 8;  // 8 lanes per (credential, key) task: 34.1 ms vs 35.8 (4) and 43.3 (2) at config 4
     const size_t ntask = n * (size_t)(q + 1);
     dim3 g(nblocks(ntask * L, 256)), b(256);
-    static const int vl = [] {
-        const char* e = getenv("CC_VKF_L");
-        return e ? atoi(e) : L;
-    }();
-    if (group == 1 && vl == 4)
-        hipLaunchKernelGGL((k_vk_agg_fixed<Fp, 4>), dim3(nblocks(ntask * 4, 256)), b, 0, st, n, len, t, q, d_ids, d_l,
-                           d_iss_ids, n_iss, d_table, wbits, d_binf, d_outX, d_outY);
-    else if (group == 1)
+    if (group == 1)
         hipLaunchKernelGGL((k_vk_agg_fixed<Fp, L>), g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
-                           wbits, d_binf, d_outX, d_outY);
+                           wbits, d_binf, d_outX, d_outY, d_err);
     else
         hipLaunchKernelGGL((k_vk_agg_fixed<Fp2, 4>), dim3(nblocks(ntask * 4, 256)), b, 0, st, n, len, t, q, d_ids,
-                           d_l, d_iss_ids, n_iss, d_table, wbits, d_binf, d_outX, d_outY);  // G2 keys: not re-measured
+                           d_l, d_iss_ids, n_iss, d_table, wbits, d_binf, d_outX, d_outY, d_err);  // G2 keys: 4 lanes
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -945,28 +873,16 @@ int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const ui
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
     // d_jtab: 15 Jacobian points of the other group per element (<= 15 x 72 words a proof)
-    static const bool split_ok = [] {
-        const char* e = getenv("CC_POK_SPLIT");
-        return !(e && e[0] == '0');
-    }();
-    if (mode == 0 && split_ok) {
+    if (mode == 0) {
         // hidden responses for role A: balance nwin (1 + split) + ~233 (chal J) against
         // nwin (hidden - split) + nwin r + ~10 (mixed-addition units)
         const int hidden = q - r, nwin = ft_nwin(wbits);
         int split = (nwin * (hidden + r - 1) - 223) / (2 * nwin);
-        static const int force_split = [] {
-            const char* e = getenv("CC_POK_SPLIT_N");
-            return e ? atoi(e) : -1;
-        }();
-        if (force_split >= 0) split = force_split;
         split = split < 0 ? 0 : (split > hidden ? hidden : split);
         hipLaunchKernelGGL(k_prep_pok_split, dim3(nblocks(n, PK_PB)), dim3(2 * PK_PB), 0, st, n, q, r, split, d_s1,
                            d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf,
                            d_prep, d_flags, d_jtab);
-    } else if (mode == 0)
-        hipLaunchKernelGGL((k_prep_pok<Fp2, Fp, 2>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
-                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags, d_jtab);
-    else
+    } else
         hipLaunchKernelGGL((k_prep_pok<Fp, Fp2, 1>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
                            d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags, d_jtab);
     return hipGetLastError() == hipSuccess ? 0 : -1;

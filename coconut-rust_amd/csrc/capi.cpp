@@ -40,18 +40,18 @@ int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* 
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
-int cck_miller_pl_g2(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+int cck_miller_lz_g2(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
-int cck_miller_pl_g1(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+int cck_miller_lz_g1(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
 size_t cck_fold_words(int mode, size_t n);
 int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok,
              int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
              uint32_t* d_flags2, hipStream_t st);
-int cck_fexp_pl(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
-                uint8_t* d_gt, hipStream_t st);
+int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
+             uint8_t* d_gt, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
 
 size_t cck_straus_words(int group, size_t t);
@@ -60,7 +60,7 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
                    hipStream_t st);
 int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uint64_t* d_ids, const uint32_t* d_l,
                      const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
-                     uint8_t* d_outX, uint8_t* d_outY, hipStream_t st);
+                     uint8_t* d_outX, uint8_t* d_outY, uint32_t* d_err, hipStream_t st);
 int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
                   uint8_t* d_out, hipStream_t st);
 int cck_prep_rlc(int mode, int part, size_t n, int q, uint64_t base_index, const uint32_t* d_key,
@@ -83,11 +83,14 @@ static inline size_t tab_words(int group, int wbits) {
     return (size_t)((256 + wbits - 1) / wbits) * (((size_t)1 << wbits) - 1) * (group == 1 ? 24 : 48);
 }
 static inline size_t tab_nwin(int wbits) { return (size_t)((256 + wbits - 1) / wbits); }
-// shared-verkey tables: 16-bit windows (half the additions of 8-bit ones; 100/200 MB per G1/G2 base in
-// HBM); COCONUT_TABLE_BITS=8 selects the small L2-resident form
-static int verkey_table_bits() {
-    const char* e = getenv("COCONUT_TABLE_BITS");
-    return (e && atoi(e) == 8) ? 8 : 16;
+// free HBM of the current device (0 if the runtime cannot say)
+static size_t free_hbm() {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return fr;
 }
 constexpr int PREP_SLOTS = 14;  // soa.h
 
@@ -134,6 +137,7 @@ struct cc_ctx {
     DevBuf table;        // fixed-base tables for Y~[0..q), g~ and X~ (q + 2 bases; X~ for RLC)
     DevBuf table_inf;    // q + 2 base flags
     int wbits = 16;      // window width of `table`
+    int force_vk_bits = 0, force_iss_bits = 0;  // cc_set_table_bits (0: chosen by memory)
     bool vk_subgroup = false;  // X~, Y~ and g~ all in the order-r subgroup (RLC soundness needs it)
     uint32_t X_inf = 0;
     // workspaces
@@ -152,6 +156,7 @@ struct cc_ctx {
     DevBuf iss_ids, iss_aff, iss_inf, iss_table;
     int iss_wbits = 8;  // window width of the issuer tables
     DevBuf agg_scratch;
+    DevBuf dev_err;  // device-side argument errors of *_device calls (cc_device_error)
     uint32_t rlc_key_host[8] = {0};
     // timing
     bool timing = false;
@@ -200,18 +205,14 @@ static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t
                       uint32_t* d_f, hipStream_t st, int np = 2, size_t fstride = 0, size_t foff = 0,
                       uint32_t* d_qcheck = nullptr) {
     if (!fstride) fstride = n;
-    return mode == 0 ? cck_miller_pl_g2(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, d_qcheck, st)
-                     : cck_miller_pl_g1(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, nullptr, st);
+    return mode == 0 ? cck_miller_lz_g2(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, d_qcheck, st)
+                     : cck_miller_lz_g1(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, nullptr, st);
 }
 // the RLC fold's pseudo-credentials: one (Q, P) pair per lane pair, Q affine G2 and P in evaluation
 // form, both per lane (either group mode: the SigG2 instantiation reads exactly that)
 static int cck_miller_pairs(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
                             size_t fstride, size_t foff, hipStream_t st) {
-    return cck_miller_pl_g2(0, 1, n, d_prep, d_flags, nullptr, d_f, fstride, foff, nullptr, st);
-}
-static int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
-                    uint8_t* d_gt, hipStream_t st) {
-    return cck_fexp_pl(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st);
+    return cck_miller_lz_g2(0, 1, n, d_prep, d_flags, nullptr, d_f, fstride, foff, nullptr, st);
 }
 
 static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }
@@ -295,7 +296,7 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag,
                       &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->pok_idx, &c->rlc_gath,
                       &c->rlc_pts, &c->rlc_dig, &c->rlc_work, &c->rlc_prep2, &c->rlc_finf, &c->rlc_flags2,
-                      &c->iss_ids, &c->iss_aff, &c->iss_inf, &c->iss_table, &c->agg_scratch};
+                      &c->iss_ids, &c->iss_aff, &c->iss_inf, &c->iss_table, &c->agg_scratch, &c->dev_err};
     for (auto* b : bufs) b->release();
     for (auto& b : c->in_aux) b.release();
     for (auto& e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -353,14 +354,29 @@ static cc_status subgroup_host(cc_ctx* c, int group, size_t n, const uint8_t* by
     return CC_OK;
 }
 
+// Shared-verkey tables: 16-bit windows (half the additions of 8-bit ones; 100 / 200 MB per G1 / G2
+// base) when the q + 2 bases' tables fit half the free HBM (at most 64 GiB), else 8-bit windows
+// (32 x 255 entries, 0.8 / 1.6 MB a base); a failed 16-bit allocation falls back to 8 bits.
+// cc_set_table_bits forces either width.  On failure the caller leaves the context without a verkey.
 static cc_status rebuild_tables(cc_ctx* c) {
     // bases for the fixed-base tables: Y~[0..q), g~ (PoK Schnorr base), X~ (RLC) -> q + 2 bases
     int og = oth_group(c->mode);
     size_t aw = aff_words(og);
     int nb = (int)c->q + 2;
-    c->wbits = verkey_table_bits();
     c->rlc_fixed_ok = false;
-    if (c->table.ensure((size_t)nb * tab_words(og, c->wbits) * 4)) return CC_ERR_HIP;
+    int wb = c->force_vk_bits;
+    if (wb != 8 && wb != 16) {
+        const double want = (double)nb * (double)tab_words(og, 16) * 4.0;
+        const double cap = std::min(0.5 * (double)free_hbm(), 64.0 * (double)(1ull << 30));
+        wb = want <= cap ? 16 : 8;
+    }
+    if (c->table.ensure((size_t)nb * tab_words(og, wb) * 4)) {
+        (void)hipGetLastError();  // clear the failed allocation's error
+        if (wb == 8 || c->force_vk_bits == 16) return CC_ERR_HIP;
+        wb = 8;
+        if (c->table.ensure((size_t)nb * tab_words(og, wb) * 4)) return CC_ERR_HIP;
+    }
+    c->wbits = wb;
     if (c->table_inf.ensure((size_t)nb * 4)) return CC_ERR_HIP;
     // [Y~..., g~, X~] are contiguous in vk_aff (X~ at 0, Y~ at 1..q, g~ at q+1, X~ again at q+2)
     HIPCK(hipMemcpyAsync(c->table_inf.p, c->vk_inf.as<uint32_t>() + 1, (size_t)nb * 4, hipMemcpyDeviceToDevice,
@@ -405,7 +421,12 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
         // refresh g~ slot of the verkey block and its table
         HIPCK(hipMemcpy(c->vk_aff.as<uint32_t>() + (c->q + 1) * aw, c->gtilde_aff.p, aw * 4, hipMemcpyDeviceToDevice));
         HIPCK(hipMemcpy(c->vk_inf.as<uint32_t>() + (c->q + 1), &c->gtilde_inf, 4, hipMemcpyHostToDevice));
-        return rebuild_tables(c);
+        cc_status st = rebuild_tables(c);
+        if (st) {
+            c->have_vk = false;
+            c->q = 0;
+        }
+        return st;
     }
     return CC_OK;
 }
@@ -413,6 +434,10 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
 cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q) {
     if (!c || !X || (q && !Y) || q > 4096) return CC_ERR_DECODE;
     if (!c->have_params) return CC_ERR_STATE;
+    // no verkey until every step below has succeeded: a failed call leaves the context refusing
+    // verify / RLC / PoK calls with CC_ERR_STATE instead of running on a half-built table
+    c->have_vk = false;
+    c->q = 0;
     if (!c->peers.empty()) {
         for (cc_ctx* p : c->peers) {
             cc_status s = cc_set_verkey(p, X, Y, q);
@@ -449,8 +474,34 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
         c->vk_subgroup = ok;
     }
     c->q = q;
+    cc_status st = rebuild_tables(c);
+    if (st) {
+        c->q = 0;
+        return st;
+    }
     c->have_vk = true;
-    return rebuild_tables(c);
+    return CC_OK;
+}
+
+cc_status cc_set_table_bits(cc_ctx* c, int verkey_bits, int issuer_bits) {
+    if (!c || (verkey_bits != 0 && verkey_bits != 8 && verkey_bits != 16) ||
+        (issuer_bits != 0 && (issuer_bits < 8 || issuer_bits > 16)))
+        return CC_ERR_DECODE;
+    for (cc_ctx* p : c->peers) {
+        p->force_vk_bits = verkey_bits;
+        p->force_iss_bits = issuer_bits;
+    }
+    c->force_vk_bits = verkey_bits;
+    c->force_iss_bits = issuer_bits;
+    return CC_OK;
+}
+
+cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
+    c = primary(c);
+    if (!c) return CC_ERR_DECODE;
+    if (verkey_bits) *verkey_bits = c->have_vk ? c->wbits : 0;
+    if (issuer_bits) *issuer_bits = c->iss_n ? c->iss_wbits : 0;
+    return CC_OK;
 }
 
 static cc_status ensure_work(cc_ctx* c, size_t n) {
@@ -1024,6 +1075,11 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
         }
         return CC_OK;
     }
+    // no issuer table until every step below has succeeded (a failed call leaves CC_ERR_STATE behind,
+    // never stale metadata over a rebuilt buffer)
+    c->iss_n = 0;
+    c->iss_q = 0;
+    c->iss_ids_host.clear();
     HIPCK(hipSetDevice(c->device));
     const int og = oth_group(c->mode);
     const size_t ob = (size_t)oth_bytes(c->mode), aw = aff_words(og);
@@ -1042,22 +1098,15 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
         memcpy(&enc[(r * (q + 1)) * ob], X + k * ob, ob);
         for (size_t j = 0; j < q; j++) memcpy(&enc[(r * (q + 1) + 1 + j) * ob], Y + (k * q + j) * ob, ob);
     }
-    // the widest window whose tables fit the budget (CC_ISSUER_TABLE_GB, default 16 GiB of the 288 GB
-    // HBM; CC_ISSUER_WBITS forces one): t x nwin additions per aggregated key, nwin = ceil(256 / w)
-    static const double budget_gb = [] {
-        const char* e = getenv("CC_ISSUER_TABLE_GB");
-        return e ? atof(e) : 16.0;
-    }();
-    static const int force_wb = [] {
-        const char* e = getenv("CC_ISSUER_WBITS");
-        return e ? atoi(e) : 0;
-    }();
+    // the widest window whose tables fit the budget (16 GiB of the 288 GB HBM, at most half of what is
+    // free; cc_set_table_bits forces a width): t x nwin additions per aggregated key, nwin = ceil(256 / w)
+    const double budget = std::min(16.0 * (double)(1ull << 30), 0.5 * (double)free_hbm());
     int wb = 8;
-    if (force_wb >= 8 && force_wb <= 16) {
-        wb = force_wb;
+    if (c->force_iss_bits >= 8 && c->force_iss_bits <= 16) {
+        wb = c->force_iss_bits;
     } else {
         for (int cand : {16, 13, 12, 10})
-            if ((double)(nb * tab_words(og, cand) * 4) <= budget_gb * (double)(1ull << 30)) {
+            if ((double)(nb * tab_words(og, cand) * 4) <= budget) {
                 wb = cand;
                 break;
             }
@@ -1066,6 +1115,7 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
         return CC_ERR_HIP;
     if (c->iss_table.ensure(nb * tab_words(og, wb) * 4)) {
         (void)hipGetLastError();  // clear the failed allocation's error
+        if (c->force_iss_bits) return CC_ERR_HIP;
         wb = 8;                   // the wide table did not fit the free HBM
         if (c->iss_table.ensure(nb * tab_words(og, wb) * 4)) return CC_ERR_HIP;
     }
@@ -1091,10 +1141,13 @@ static cc_status launch_vk_aggregate_ids(cc_ctx* c, size_t n, size_t len, size_t
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_lagrange(n, len, t, d_ids, c->lag.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    if (!c->dev_err.p) {  // sticky until cc_device_error reads it
+        if (c->dev_err.ensure(4)) return CC_ERR_HIP;
+        HIPCK(hipMemsetAsync(c->dev_err.p, 0, 4, st));
+    }
     KCK(cck_vk_agg_fixed(oth_group(c->mode), n, len, t, (int)c->iss_q, d_ids, c->lag.as<uint32_t>(),
                          c->iss_ids.as<uint64_t>(), (int)c->iss_n, c->iss_table.as<uint32_t>(), c->iss_wbits,
-                         c->iss_inf.as<uint32_t>(),
-                         d_oX, d_oY, st));
+                         c->iss_inf.as<uint32_t>(), d_oX, d_oY, c->dev_err.as<uint32_t>(), st));
     if (c->timing) {
         (void)hipEventRecord(c->ev[2], st);
         (void)hipEventRecord(c->ev[3], st);
@@ -1142,6 +1195,22 @@ cc_status cc_verkey_aggregate_ids(cc_ctx* c, size_t n, size_t len, size_t t, con
     HIPCK(hipMemcpyAsync(outX, d_oX.p, n * ob, hipMemcpyDeviceToHost, st));
     if (q) HIPCK(hipMemcpyAsync(outY, d_oY.p, n * q * ob, hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
+    return CC_OK;
+}
+
+cc_status cc_device_error(cc_ctx* c, void* stream, uint32_t* out) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || !out) return CC_ERR_DECODE;
+    *out = 0;
+    if (!c->dev_err.p) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    StreamOrder order(c, st);
+    uint32_t v = 0;
+    HIPCK(hipMemcpyAsync(&v, c->dev_err.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemsetAsync(c->dev_err.p, 0, 4, st));
+    HIPCK(hipStreamSynchronize(st));
+    *out = v;
     return CC_OK;
 }
 

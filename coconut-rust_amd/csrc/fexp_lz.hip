@@ -391,15 +391,7 @@ extern "C" int cck_fexp_prof_read(unsigned long long* out, size_t nwaves) {
 extern "C" int cck_fexp_lz(size_t n, const uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags,
                            uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
     if (!n) return 0;
-    static const bool snap = [] {
-        const char* e = getenv("CC_FEXP_SNAP");
-        return !(e && e[0] == '0');
-    }();
-    if (snap)
-        hipLaunchKernelGGL(cc::lz::k_fexp_lz<true>, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, st, n, d_f,
-                           reinterpret_cast<int32_t*>(d_scratch), d_flags, d_verdicts, d_gt);
-    else
-        hipLaunchKernelGGL(cc::lz::k_fexp_lz<false>, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, st, n,
-                           d_f, reinterpret_cast<int32_t*>(d_scratch), d_flags, d_verdicts, d_gt);
+    hipLaunchKernelGGL(cc::lz::k_fexp_lz<true>, dim3((unsigned)((2 * n + 255) / 256)), dim3(256), 0, st, n, d_f,
+                       reinterpret_cast<int32_t*>(d_scratch), d_flags, d_verdicts, d_gt);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -478,19 +478,9 @@ DEV void fexp_out(size_t n, size_t i, const uint32_t* scratch, const uint32_t* f
     }
 }
 
-// fbuf: Miller output f (12 slots); scratch: 4 x 12 slots (T, A, S, R) + 24 slots K (fx_pow_x snapshots)
-__global__ __launch_bounds__(256, 2) void k_fexp(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
-                                              const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
-                                              uint8_t* __restrict__ gt_out) {
-    const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
-    if (i >= n) return;  // pair-uniform
-    fexp_chain<false>(n, i, fbuf, scratch);
-    fexp_out(n, i, scratch, flags, verdicts, gt_out, true);
-}
-
 // one element on one wave (64 lanes, all pairs holding the same values; pair 0 writes the outputs).
-// One wave per SIMD (HIP's second bound): the whole register file; every step function is a W = true
-// instantiation of its own, so the bound does not reach k_fexp's 2 waves/SIMD budget.
+// One wave per SIMD (HIP's second bound): the whole register file (every step function is a W = true
+// instantiation).  Batches (n > 1) run the lazy-field kernel of fexp_lz.hip.
 __global__ __launch_bounds__(64, 1) void k_fexp1(uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
                                               const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
                                               uint8_t* __restrict__ gt_out) {
@@ -507,19 +497,11 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 extern "C" int cck_fexp_lz(size_t n, const uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags,
                            uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st);
 
-extern "C" int cck_fexp_pl(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
+extern "C" int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                         uint8_t* d_gt, hipStream_t st) {
     if (!n) return 0;
-    // batches: the lazy-field kernel unless CC_FEXP=pl (A/B runs)
-    static const bool lz = [] {
-        const char* e = getenv("CC_FEXP");
-        return !(e && !strcmp(e, "pl"));
-    }();
-    if (n > 1 && lz) return cck_fexp_lz(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st);
-    if (n == 1)  // latency-bound: the wide one-wave form
-        hipLaunchKernelGGL(cc::pl::k_fexp1, dim3(1), dim3(64), 0, st, d_f, d_scratch, d_flags, d_verdicts, d_gt);
-    else
-        hipLaunchKernelGGL(cc::pl::k_fexp, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, d_f, d_scratch, d_flags,
-                           d_verdicts, d_gt);
+    if (n > 1) return cck_fexp_lz(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st);
+    // one element (the RLC batch's combined product): latency-bound, the wide one-wave form
+    hipLaunchKernelGGL(cc::pl::k_fexp1, dim3(1), dim3(64), 0, st, d_f, d_scratch, d_flags, d_verdicts, d_gt);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

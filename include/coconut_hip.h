@@ -75,8 +75,17 @@ cc_status cc_ctx_mode(const cc_ctx* ctx, int* mode_out);
 cc_status cc_set_params(cc_ctx* ctx, const uint8_t* g_tilde);
 
 /* Shared verkey (X~, Y~[q]) for cc_verify_batch with vk == NULL: builds fixed-base tables on the
- * device (one-time cost, reported separately from batch throughput). */
+ * device (one-time cost, reported separately from batch throughput): 16-bit windows when the q + 2
+ * bases' tables fit half the free HBM (at most 64 GiB), else 8-bit windows.  On any failure the
+ * context is left WITHOUT a verkey (verify / RLC / PoK calls then return CC_ERR_STATE). */
 cc_status cc_set_verkey(cc_ctx* ctx, const uint8_t* X, const uint8_t* Y, size_t q);
+
+/* Window widths of the fixed-base tables built by later cc_set_verkey / cc_set_issuers calls:
+ * verkey_bits 0 (chosen by memory), 8 or 16; issuer_bits 0 (chosen by memory) or 8..16.  A forced
+ * width that does not fit HBM makes the building call fail.  cc_table_bits reports the widths of the
+ * current tables (0: none built). */
+cc_status cc_set_table_bits(cc_ctx* ctx, int verkey_bits, int issuer_bits);
+cc_status cc_table_bits(const cc_ctx* ctx, int* verkey_bits, int* issuer_bits);
 
 /* Batch Signature::verify.
  *   sigma1, sigma2 : n x SignatureGroup encodings
@@ -138,17 +147,27 @@ cc_status cc_signature_aggregate_batch_device(cc_ctx* ctx, size_t n, size_t len,
 /* Issuer table for Verkey::aggregate at scale (BASELINE config 4: t = 67 of n = 100 issuers).  The
  * n_issuers verkeys (X: n_issuers x OtherGroup, Y: n_issuers x q x OtherGroup) and their signer ids
  * (unique) are decoded once and given fixed-base window tables in HBM (one-time cost; the widest
- * window whose tables fit 16 GiB, env CC_ISSUER_TABLE_GB: 13-bit, 11 GB, for 100 issuers x 7 G1
- * keys); a batch then passes only id lists.  cc_verkey_aggregate_ids(_device) computes, per credential, exactly
+ * window in {16, 13, 12, 10, 8} whose tables fit 16 GiB and half the free HBM — 13-bit, 11 GB, for
+ * 100 issuers x 7 G1 keys — or the width forced by cc_set_table_bits); a batch then passes only id
+ * lists.  A failed call leaves no issuer table (CC_ERR_STATE afterwards).
+ * cc_verkey_aggregate_ids(_device) computes, per credential, exactly
  * Verkey::aggregate(t, [(id_k, &issuer[id_k])]) (signature.rs:483-526): first t entries, Lagrange
- * over the de-duplicated id set.  ids: n x len.  CC_ERR_DECODE if an id has no issuer verkey (host
- * form; the device form requires every id to be in the table). */
+ * over the de-duplicated id set.  ids: n x len.  An id without an issuer verkey (the reference would
+ * index a missing key): the host form returns CC_ERR_DECODE before launching; the device form writes
+ * the identity encoding for the affected outputs and raises the context's device error word
+ * (CC_DEVERR_UNKNOWN_ID), which cc_device_error reads. */
 cc_status cc_set_issuers(cc_ctx* ctx, size_t n_issuers, size_t q, const uint64_t* ids, const uint8_t* X,
                          const uint8_t* Y);
 cc_status cc_verkey_aggregate_ids(cc_ctx* ctx, size_t n, size_t len, size_t t, const uint64_t* ids, uint8_t* outX,
                                   uint8_t* outY);
 cc_status cc_verkey_aggregate_ids_device(cc_ctx* ctx, size_t n, size_t len, size_t t, const uint64_t* d_ids,
                                          uint8_t* d_outX, uint8_t* d_outY, void* stream);
+
+/* Argument errors that only the device can see (ids checked inside a kernel of a *_device call):
+ * synchronises `stream` (NULL: the context stream), returns the OR of the CC_DEVERR_* bits raised since
+ * the last read in *out, and clears them. */
+#define CC_DEVERR_UNKNOWN_ID 1u
+cc_status cc_device_error(cc_ctx* ctx, void* stream, uint32_t* out);
 
 /* Batch PoKOfSignatureProof::verify against the shared verkey and params.
  *   sigma1, sigma2  : n x SignatureGroup (sigma'_1, sigma'_2)

@@ -234,6 +234,35 @@ def test_full_size_batch_config2(ctxs):
     assert np.array_equal(v, b["expect"])
 
 
+@pytest.mark.parametrize("mode,n", [("G2", 65536), ("G1", 4096)])
+def test_config2_survey_batch_every_corruption_kind(ctxs, mode, n):
+    """bench.py's timed config-2 batch: verkey aggregated 3-of-5 on the GPU, 1/16
+    corrupted split evenly over sigma_2 + G, m_j + 1, swapped, sigma_1 = O, sigma_2 = O, wrong vk —
+    every verdict equals construction; a slice's GT bytes equal the C oracle's."""
+    import bench
+    from coconut import verify_batch
+    m = MODES[mode]
+    ctx = ctxs[mode]
+    q = 6
+    b = bench.make_verify_batch(ctx, m, n, q, seed=2)
+    kinds = {k for k in b["kind"] if k}
+    assert kinds == set(bench.CORRUPT_KINDS)
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    v = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"])
+    assert np.array_equal(v, b["expect"])
+    k = 192  # covers every kind twice
+    sb = 192 if m == 0 else 97
+    vk_, gts = verify_batch(ctx, k, q, b["s1"][:k * sb], b["s2"][:k * sb], b["msgs"][:k * q * 48], want_gt=True)
+    oc = oracle_lib()
+    ver = ctypes.create_string_buffer(k)
+    ref = ctypes.create_string_buffer(576 * k)
+    oc.oc_verify_batch(m, ctypes.c_size_t(k), ctypes.c_size_t(q), b["s1"][:k * sb], b["s2"][:k * sb],
+                       b["msgs"][:k * q * 48], b["X"], b["Y"], 0, b["g_tilde"], ver, ref, host_threads())
+    assert ref.raw == gts
+    assert np.array_equal(np.frombuffer(ver.raw, np.uint8), vk_)
+
+
 # ---------------------------------------------------------------- RLC batch mode (SURVEY.md §8e)
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_rlc_batch_accepts_valid_and_falls_back_exactly(ctxs, mode):

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Per-mode evidence for configs 3/4/5 (and SigG1 config 2): rocprofv3 kernel-trace stats of a short
+# bench run, then the PMC passes of tools/pmc_round.sh, one directory per mode.
+# Each GPU step has its own time limit; the first failure ends the script.
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+R=$(pwd)
+TAG=${1:-modes}
+shift || true
+MODES=${*:-rlc aggregate pok verify-g1}
+export TMPDIR=/tmp
+for m in $MODES; do
+  OUT=$R/gpurun_out/$TAG/$m
+  mkdir -p "$OUT"
+  echo "[modes] $m: rocprofv3 stats"
+  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 "$R/bench.py" --mode $m --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err")
+  echo "[modes] $m: pmc"
+  PMC_OUT="$OUT/pmc" BENCH_ARGS="--mode $m" bash tools/pmc_round.sh > "$OUT/pmc.log" 2>&1
+  python3 tools/pmc_summary.py "$OUT/pmc" "$OUT/pmc_summary.json" > "$OUT/pmc_summary.log" 2>&1
+done
+echo "[modes] done"
