@@ -53,6 +53,7 @@ _SIGS = {
     "cc_set_issuers": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p]),
     "cc_verkey_aggregate_ids": (c_int, [c_p, c_sz, c_sz, c_sz, c_p, c_p, c_p]),
     "cc_verkey_aggregate_ids_device": (c_int, [c_p, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p]),
+    "cc_aggregate_credential_batch_device": (c_int, [c_p, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "cc_subgroup_check": (c_int, [c_p, c_int, c_sz, c_p, c_p]),
     "cc_hash_to_curve": (c_int, [c_p, c_int, c_sz, c_p, c_p, c_p]),
     "cc_hash_msg": (c_int, [c_p, c_sz, c_p, c_p, c_p]),

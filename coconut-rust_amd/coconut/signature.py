@@ -176,6 +176,7 @@ class Context:
         q = len(Yb) // self.mode.other_bytes
         px, k1 = buf(X)
         py, k2 = buf(Yb)
+        self._vk = None  # a failed call leaves the context without a verkey
         check(lib.cc_set_verkey(self.h, px, py, q), "cc_set_verkey")
         self._vk = key
 
@@ -191,6 +192,7 @@ class Context:
     def set_table_bits(self, verkey_bits: int = 0, issuer_bits: int = 0):
         """Window widths of the tables later set_verkey / set_issuers calls build (0: by memory)."""
         check(lib.cc_set_table_bits(self.h, verkey_bits, issuer_bits), "cc_set_table_bits")
+        self._vk = None  # the next set_verkey rebuilds its tables at the new width, even for the same key
 
     def table_bits(self):
         """(verkey table bits, issuer table bits) of the current tables (0: none)."""

@@ -365,10 +365,20 @@ static cc_status rebuild_tables(cc_ctx* c) {
     int nb = (int)c->q + 2;
     c->rlc_fixed_ok = false;
     int wb = c->force_vk_bits;
+    // the old table is released first so its memory counts as free
+    c->table.release();
+    const double fr = (double)free_hbm();
     if (wb != 8 && wb != 16) {
         const double want = (double)nb * (double)tab_words(og, 16) * 4.0;
-        const double cap = std::min(0.5 * (double)free_hbm(), 64.0 * (double)(1ull << 30));
+        const double cap = std::min(0.5 * fr, 64.0 * (double)(1ull << 30));
         wb = want <= cap ? 16 : 8;
+    }
+    // a forced width is refused up front when it exceeds the free HBM: hipMalloc does not reliably fail
+    // for sizes above it (the runtime may over-commit), and a build kernel writing such a table would not
+    // end well
+    if (fr > 0 && (double)nb * (double)tab_words(og, wb) * 4.0 > 0.9 * fr) {
+        if (c->force_vk_bits == 16 || wb == 8) return CC_ERR_HIP;
+        wb = 8;
     }
     if (c->table.ensure((size_t)nb * tab_words(og, wb) * 4)) {
         (void)hipGetLastError();  // clear the failed allocation's error
@@ -506,9 +516,11 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
 
 static cc_status ensure_work(cc_ctx* c, size_t n) {
     size_t words = n * 12;  // one Fp slot
-    // fexp scratch: 84 lazy Fp slots of 14 words (fexp_lz.hip) >= 72 slots of 12 (fexp_pl.hip)
+    // scratch: the PoK prep's per-proof table of d J (15 Jacobian points, <= 15 x 72 words), and the
+    // one-element fexp's (fexp_pl.hip k_fexp1: 72 slots of 12 words); the batched fexp (fexp_q.hip)
+    // keeps its chain in registers
     if (c->prep.ensure(words * 4 * PREP_SLOTS) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
-        c->scratch.ensure(n * 14 * 84 * 4) || c->verdicts.ensure(n))
+        c->scratch.ensure((n * 15 * 72 + 72 * 12) * 4) || c->verdicts.ensure(n))
         return CC_ERR_HIP;
     return CC_OK;
 }
@@ -1113,6 +1125,12 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
     }
     if (c->iss_ids.ensure(n_iss * 8) || c->iss_aff.ensure(nb * aw * 4) || c->iss_inf.ensure(nb * 4))
         return CC_ERR_HIP;
+    c->iss_table.release();
+    const double fr = (double)free_hbm();
+    if (fr > 0 && (double)(nb * tab_words(og, wb) * 4) > 0.9 * fr) {  // see rebuild_tables
+        if (c->force_iss_bits) return CC_ERR_HIP;
+        wb = 8;
+    }
     if (c->iss_table.ensure(nb * tab_words(og, wb) * 4)) {
         (void)hipGetLastError();  // clear the failed allocation's error
         if (c->force_iss_bits) return CC_ERR_HIP;
@@ -1168,6 +1186,47 @@ cc_status cc_verkey_aggregate_ids_device(cc_ctx* c, size_t n, size_t len, size_t
     cc_status s = launch_vk_aggregate_ids(c, n, len, t, d_ids, d_outX, d_outY, st);
     if (s) return s;
     if (c->timing) collect_timing(c);
+    return CC_OK;
+}
+
+// Signature::aggregate + Verkey::aggregate of the same credentials (same id lists): the Lagrange
+// coefficients depend only on the ids (signature.rs:454-463 and 496-509 compute the same l_i), so one
+// k_lagrange launch serves both MSMs.  Timing: (Lagrange, signature MSM, verkey MSM).
+cc_status cc_aggregate_credential_batch_device(cc_ctx* c, size_t n, size_t len, size_t t, const uint64_t* d_ids,
+                                               const uint8_t* d_s1, const uint8_t* d_s2, uint8_t* d_out_s1,
+                                               uint8_t* d_out_s2, uint8_t* d_outX, uint8_t* d_outY, void* stream) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || (n && (!d_ids || !d_s1 || !d_s2 || !d_out_s1 || !d_out_s2 || !d_outX || (c->iss_q && !d_outY))))
+        return CC_ERR_DECODE;
+    if (!c->iss_n) return CC_ERR_STATE;
+    if (len < t || len == 0) return CC_ERR_THRESHOLD;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    StreamOrder order(c, st);
+    const size_t sb = (size_t)sig_bytes(c->mode);
+    const int sg = sig_group(c->mode);
+    if (c->lag.ensure(n * t * 32 + 32)) return CC_ERR_HIP;
+    cc_status s = agg_scratch(c, sg, n, t);
+    if (s) return s;
+    if (!c->dev_err.p) {
+        if (c->dev_err.ensure(4)) return CC_ERR_HIP;
+        HIPCK(hipMemsetAsync(c->dev_err.p, 0, 4, st));
+    }
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
+    KCK(cck_lagrange(n, len, t, d_ids, c->lag.as<uint32_t>(), st));
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    KCK(cck_msm_straus(sg, n, t, d_s2, len * sb, 0, sb, c->lag.as<uint32_t>(), 1, c->agg_scratch.as<uint32_t>(),
+                       d_out_s2, st));
+    HIPCK(hipMemcpy2DAsync(d_out_s1, sb, d_s1, len * sb, sb, n, hipMemcpyDeviceToDevice, st));
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
+    KCK(cck_vk_agg_fixed(oth_group(c->mode), n, len, t, (int)c->iss_q, d_ids, c->lag.as<uint32_t>(),
+                         c->iss_ids.as<uint64_t>(), (int)c->iss_n, c->iss_table.as<uint32_t>(), c->iss_wbits,
+                         c->iss_inf.as<uint32_t>(), d_outX, d_outY, c->dev_err.as<uint32_t>(), st));
+    if (c->timing) {
+        (void)hipEventRecord(c->ev[3], st);
+        collect_timing(c);
+    }
     return CC_OK;
 }
 

@@ -480,7 +480,7 @@ DEV void fexp_out(size_t n, size_t i, const uint32_t* scratch, const uint32_t* f
 
 // one element on one wave (64 lanes, all pairs holding the same values; pair 0 writes the outputs).
 // One wave per SIMD (HIP's second bound): the whole register file (every step function is a W = true
-// instantiation).  Batches (n > 1) run the lazy-field kernel of fexp_lz.hip.
+// instantiation).  Batches (n > 1) run the quad-lane lazy-field kernel of fexp_q.hip.
 __global__ __launch_bounds__(64, 1) void k_fexp1(uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
                                               const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
                                               uint8_t* __restrict__ gt_out) {
@@ -493,14 +493,14 @@ __global__ __launch_bounds__(64, 1) void k_fexp1(uint32_t* __restrict__ fbuf, ui
 
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
-// the lazy-field kernel (fexp_lz.hip), same arguments; its scratch is 84 x 14 words per element
-extern "C" int cck_fexp_lz(size_t n, const uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags,
-                           uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st);
+// the batched kernel: lazy field, one credential per lane quad, the chain in registers (fexp_q.hip)
+extern "C" int cck_fexp_q(size_t n, const uint32_t* d_f, const uint32_t* d_flags, uint8_t* d_verdicts, uint8_t* d_gt,
+                          hipStream_t st);
 
 extern "C" int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
                         uint8_t* d_gt, hipStream_t st) {
     if (!n) return 0;
-    if (n > 1) return cck_fexp_lz(n, d_f, d_scratch, d_flags, d_verdicts, d_gt, st);
+    if (n > 1) return cck_fexp_q(n, d_f, d_flags, d_verdicts, d_gt, st);
     // one element (the RLC batch's combined product): latency-bound, the wide one-wave form
     hipLaunchKernelGGL(cc::pl::k_fexp1, dim3(1), dim3(64), 0, st, d_f, d_scratch, d_flags, d_verdicts, d_gt);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -1,0 +1,178 @@
+// Final-exponentiation kernel for gfx950 on the lazy field, ONE credential per QUAD of lanes (tower_q.h)
+// — AMCL `pair::fexp` via amcl_wrapper `GT::ate_2_pairing` (reference src/lib.rs:13; SURVEY.md §8a
+// V6/V7).  Same chain as fexp_pl.hip: easy part f^((p^6 - 1)(p^2 + 1)), hard part
+// 3 + (x-1)^2 [p^3 + x p^2 + (x^2-1) p + x^3 - x] = 3 Phi_12(p) / r, each pow-by-x as 57 compressed
+// cyclotomic squarings, one batched decompression (snapshots g^(2^16), g^(2^48), g^(2^57), one Fp2
+// inversion) and 6 Granger-Scott squarings.
+//
+// The quad layout holds an Fp12 in 42 words a lane, so the whole chain stays in registers: no
+// scratch round trips between steps (the pair layout's chain rested every Fp12 in an 84-slot HBM
+// scratch and reloaded it for the next step).
+#include "codec.h"
+#include "tower_q.h"
+
+namespace cc {
+namespace lz {
+namespace {
+
+// ---------------------------------------------------------------- compressed cyclotomic squaring
+// fexp_pl.hip cyc4_sqr (Karabina's compression restated for this tower), this lane holding component j
+// of b = b0 + b1 s and c = c0 + c1 s:
+//     b0' = 3 (2 xi c0 c1) + 2 b0    b1' = 3 (c0^2 + xi c1^2) - 2 b1
+//     c0' = 3 (b0^2 + xi b1^2) - 2 c0    c1' = 3 (2 b0 b1) + 2 c1
+// Pair 0 squares b0, c0 and b0 + b1; pair 1 squares b1, c1 and c0 + c1 (3 Fp2 squarings a lane).
+using F2R = F2<AN, 9>;
+struct QZ {
+    F2R B, C;  // b_j, c_j
+};
+DEV void qz_sqr(QZ& x) {
+    const bool j = qhi();
+    const auto sB = sqrr(x.B);
+    const auto sC = sqrr(x.C);
+    const auto M = sqrr(add(qsel(j, x.C, x.B), qx(qsel(j, x.B, x.C))));  // (b0 + b1)^2 | (c0 + c1)^2
+    const auto pSB = qx(sB), pSC = qx(sC), pM = qx(M);
+    // pair 0: 2 xi c0 c1 and b0^2 + xi b1^2; pair 1: c0^2 + xi c1^2 and 2 b0 b1
+    const auto u = norm(qsel(j, add(pSC, xi(sC)), xi(sub(sub(pM, sC), pSC))));
+    const auto v = norm(qsel(j, sub(sub(pM, pSB), sB), add(sB, xi(pSB))));
+    // 3u + 2y = u + 2 (u + y), 3u - 2y = u + 2 (u - y)
+    x.B = reduce(add(u, dbl(add(u, qsel(j, neg(x.B), x.B)))));
+    x.C = reduce(add(v, dbl(add(v, qsel(j, x.C, neg(x.C))))));
+}
+// numerator of this lane's a_j and the common denominator D (fexp_pl.hip cyc4_num):
+//     a0 = (b0 Nb + xi c1 Nc) / D,  a1 = (c0 Nc + b1 Nb) / D,
+//     Nb = b0^2 - xi b1^2,  Nc = c0^2 - xi c1^2,  D = 2 (b0 c0 - xi b1 c1)
+DEV void qz_num(F2R& nj, F2R& den, const QZ& x) {
+    const bool j = qhi();
+    const auto sB = sqrr(x.B), sC = sqrr(x.C);
+    const auto pSB = qx(sB), pSC = qx(sC);
+    const auto Nb = norm(qsel(j, sub(pSB, xi(sB)), sub(sB, xi(pSB))));  // the same on both pairs
+    const auto Nc = norm(qsel(j, sub(pSC, xi(sC)), sub(sC, xi(pSC))));
+    const auto P1 = mulr(x.B, Nb), P2 = mulr(x.C, Nc), P3 = mulr(x.B, x.C);
+    const auto pP2 = qx(P2), pP3 = qx(P3);
+    nj = reduce(qsel(j, add(pP2, P1), add(P1, xi(pP2))));
+    den = reduce(dbl(qsel(j, sub(pP3, xi(P3)), sub(P3, xi(pP3)))));
+}
+template <class I>
+DEV QR qz_expand(const QZ& x, const F2R& nj, const I& inv) {
+    return {reduce(mulr(nj, inv)), x.B, x.C};
+}
+
+// src^x by Granger-Scott square-and-multiply: the fallback of q_pow_x for a zero decompression
+// denominator (never reached by honest inputs)
+static __device__ __noinline__ QR q_pow_x_gs(QR src) {
+    QR acc = src;
+#pragma unroll 1
+    for (int b = 62; b >= 0; b--) {
+        acc = rest(q12_cyc_sqr(acc));
+        if ((X_ABS >> b) & 1ull) acc = rest(q12_mul(acc, src));
+    }
+    return q12_conj(acc);
+}
+
+// src^x, x = -|x| (bits 63, 62, 60, 57, 48, 16 of |x|)
+DEV QR q_pow_x(const QR& src) {
+    QZ c{src.b, src.c};
+#pragma unroll 1
+    for (int k = 0; k < 16; k++) qz_sqr(c);
+    const QZ s16 = c;
+#pragma unroll 1
+    for (int k = 16; k < 48; k++) qz_sqr(c);
+    const QZ s48 = c;
+#pragma unroll 1
+    for (int k = 48; k < 57; k++) qz_sqr(c);
+    F2R n16, d16, n48, d48, n57, d57;
+    qz_num(n16, d16, s16);
+    qz_num(n48, d48, s48);
+    qz_num(n57, d57, c);
+    const auto p1 = mulr(d16, d48);
+    const auto p2 = mulr(p1, d57);
+    if (is_zero(p2)) return q_pow_x_gs(src);  // quad-uniform (D is the same on both pairs)
+    const auto iv = inv(p2);
+    QR y = qz_expand(c, n57, mulr(iv, p1));    // g^(2^57)
+    const auto iv2 = mulr(iv, d57);           // (d16 d48)^-1
+    QR acc = rest(q12_mul(qz_expand(s16, n16, mulr(iv2, d48)), qz_expand(s48, n48, mulr(iv2, d16))));
+    acc = rest(q12_mul(acc, y));
+    // then y^2 three times, acc *= y (2^60), y^2 twice, acc *= y (2^62), y^2, acc *= y (2^63)
+    constexpr uint32_t kSq = 0b010110111u;  // from bit 0: S S S M S S M S M  (1 = square)
+#pragma unroll 1
+    for (int st = 0; st < 9; st++) {
+        if ((kSq >> st) & 1u) y = rest(q12_cyc_sqr(y));
+        else acc = rest(q12_mul(acc, y));
+    }
+    return q12_conj(acc);
+}
+
+// verdict and GT bytes of the result, through the storage form (12 x 32, R = 2^406)
+DEV void qexp_out(size_t i, const QR& res, const uint32_t* flags, uint8_t* verdicts, uint8_t* gt_out) {
+    const bool j = qhi();
+    const int h = (int)half_id();
+    const pl::Fp2 oa = out_r2(res.a), ob = out_r2(res.b), oc = out_r2(res.c);
+    Fp one;
+    fp_one(one);
+    // one = (1, 0, 0, 0, 0, 0): only the real half of a's component 0 is non-zero
+    bool own = (!j && !h ? fp_eq(oa.c, one) : fp_is_zero(oa.c)) && fp_is_zero(ob.c) && fp_is_zero(oc.c);
+    const uint32_t fl = flags ? flags[i] : 0u;
+    const bool ok = quad_all(own) && (fl & 11u) == 0;  // sigma_1/sigma_2 = O or PoK Schnorr failure
+    if ((__builtin_amdgcn_mbcnt_lo(~0u, 0u) & 3u) == 0) verdicts[i] = ok ? 1 : 0;
+    if (gt_out) {  // Fp2 k of the AMCL FP12 order at 96 k, half h at + 48 h; component j of a, b, c is k = j, 2 + j, 4 + j
+        uint8_t* o = gt_out + i * 576 + 48 * h + 96 * (int)j;
+        Fp c;
+        fp_from_mont(c, oa.c);
+        store_be48_aligned(o, c);
+        fp_from_mont(c, ob.c);
+        store_be48_aligned(o + 192, c);
+        fp_from_mont(c, oc.c);
+        store_be48_aligned(o + 384, c);
+    }
+}
+
+}  // namespace
+
+// fbuf: Miller output f (12 x 32 SoA, 12 slots, R form); one credential per lane quad
+__global__ __launch_bounds__(256, 2) void k_fexp_q(size_t n, const uint32_t* __restrict__ fbuf,
+                                                const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
+                                                uint8_t* __restrict__ gt_out) {
+    const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 2;  // credential of this lane quad
+    if (i >= n) return;                                                     // quad-uniform
+    const int j = qhi() ? 1 : 0;
+    const Soa S{const_cast<uint32_t*>(fbuf), n};
+    const auto ld = [&](int k) {
+        pl::Fp2 v;
+        pl::ld_f2(v, S, 2 * k, i);
+        return reduce(in_r2(v));
+    };
+    QR f{ld(j), ld(2 + j), ld(4 + j)};  // Fp2 k = a.a, a.b, b.a, b.b, c.a, c.b
+    // easy part: f^(p^6 - 1) = conj(f) f^-1, then ^(p^2 + 1)
+    f = rest(q12_mul(q12_conj(f), rest(q12_inv(f))));
+    f = rest(q12_mul(rest(q12_frob2(f)), f));
+    QR r = rest(q12_mul(rest(q12_cyc_sqr(f)), f));  // res = f^3
+    // hard part: five pow-by-x, each followed by its share of the chain (fexp_pl.hip fexp_chain)
+    //   0: t = f^x, t *= conj(f)                       (f^(x-1))
+    //   1: a = t^x, a *= conj(t), res *= (a^(p^2) conj(a))^p
+    //   2: b = a^x, res *= b^(p^2) conj(b)
+    //   3: c = b^x, res *= c^p
+    //   4: d = c^x, res *= d
+    QR cur = f;
+#pragma unroll 1
+    for (int it = 0; it < 5; it++) {
+        QR y = q_pow_x(cur);
+        if (it <= 1) y = rest(q12_mul(y, q12_conj(cur)));
+        QR z = y;
+        if (it == 1 || it == 2) z = rest(q12_mul(rest(q12_frob2(y)), q12_conj(y)));
+        if (it == 1 || it == 3) z = rest(q12_frob(z));
+        if (it >= 1) r = rest(q12_mul(z, r));
+        cur = y;
+    }
+    qexp_out(i, r, flags, verdicts, gt_out);
+}
+
+}  // namespace lz
+}  // namespace cc
+
+extern "C" int cck_fexp_q(size_t n, const uint32_t* d_f, const uint32_t* d_flags, uint8_t* d_verdicts, uint8_t* d_gt,
+                          hipStream_t st) {
+    if (!n) return 0;
+    hipLaunchKernelGGL(cc::lz::k_fexp_q, dim3((unsigned)((4 * n + 255) / 256)), dim3(256), 0, st, n, d_f, d_flags,
+                       d_verdicts, d_gt);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}

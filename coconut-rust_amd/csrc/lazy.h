@@ -499,7 +499,7 @@ DEV bool lz_opaque_false() {
     return x != 0;
 }
 // x^2 with the multiplication inlined (its own basic block): for small hot loops whose whole body then
-// runs without call boundaries (no values saved around calls; fexp_lz.hip's compressed squarings)
+// runs without call boundaries (no values saved around calls)
 template <int A, int B>
 DEV F2<AN, bprod(4LL * B * B)> sqr_in(const F2<A, B>& x) {
     static_assert(4LL * A * A <= AMAX, "f2 sqr: limb bound");

@@ -163,6 +163,16 @@ cc_status cc_verkey_aggregate_ids(cc_ctx* ctx, size_t n, size_t len, size_t t, c
 cc_status cc_verkey_aggregate_ids_device(cc_ctx* ctx, size_t n, size_t len, size_t t, const uint64_t* d_ids,
                                          uint8_t* d_outX, uint8_t* d_outY, void* stream);
 
+/* Both aggregations of the same credentials, as a verifier holding per-credential shares does them:
+ * Signature::aggregate(t, [(id_k, sig_k)]) (signature.rs:448-470) and Verkey::aggregate(t, [(id_k,
+ * issuer[id_k])]) (signature.rs:483-526) over ONE id list per credential, so the Lagrange coefficients
+ * (signature.rs:454-463 = 496-509) are computed once.  Outputs and errors as the two calls above
+ * (device error word as cc_verkey_aggregate_ids_device).  Asynchronous on `stream`. */
+cc_status cc_aggregate_credential_batch_device(cc_ctx* ctx, size_t n, size_t len, size_t t, const uint64_t* d_ids,
+                                               const uint8_t* d_sigma1, const uint8_t* d_sigma2,
+                                               uint8_t* d_out_sigma1, uint8_t* d_out_sigma2, uint8_t* d_outX,
+                                               uint8_t* d_outY, void* stream);
+
 /* Argument errors that only the device can see (ids checked inside a kernel of a *_device call):
  * synchronises `stream` (NULL: the context stream), returns the OR of the CC_DEVERR_* bits raised since
  * the last read in *out, and clears them. */

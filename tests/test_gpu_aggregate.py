@@ -93,6 +93,62 @@ def test_config4_full_size_property(ctxs):
     assert bytes(o1.cpu().numpy()) == b["want_s1"]
 
 
+def test_config4_fused_entry_one_lagrange(ctxs):
+    """cc_aggregate_credential_batch_device (one Lagrange launch for both MSMs) equals the two separate
+    entry points on 2,000 config-4 credentials, and the golden t = 67 subsets equal the oracle."""
+    import torch
+    import bench_modes
+    from coconut import _lib
+    ctx = ctxs["G2"]
+    n = 2000
+    b = bench_modes.make_aggregate_batch(ctx, 0, n, seed=45)
+    ctx.set_issuers(b["iss"], b["X"], b["Y"], b["q"])
+    t, q, sb, ob = b["t"], b["q"], b["sb"], b["ob"]
+    dev = torch.device("cuda", 0)
+    d_ids = torch.from_numpy(b["ids"].view(np.int64).copy()).to(dev)
+    d_s1 = torch.frombuffer(bytearray(b["s1"]), dtype=torch.uint8).to(dev)
+    d_s2 = torch.frombuffer(bytearray(b["s2"]), dtype=torch.uint8).to(dev)
+    o1, o2 = (torch.zeros(n * sb, dtype=torch.uint8, device=dev) for _ in range(2))
+    oX = torch.zeros(n * ob, dtype=torch.uint8, device=dev)
+    oY = torch.zeros(n * q * ob, dtype=torch.uint8, device=dev)
+    P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    torch.cuda.synchronize()
+    lib = _lib.lib
+    assert lib.cc_aggregate_credential_batch_device(ctx.h, n, t, t, P(d_ids), P(d_s1), P(d_s2), P(o1), P(o2),
+                                                    P(oX), P(oY), None) == 0
+    assert ctx.device_error() == 0
+    assert bytes(oX.cpu().numpy()) == b["want_X"] * n
+    assert bytes(oY.cpu().numpy()) == b["want_Y"] * n
+    assert bytes(o2.cpu().numpy()) == b["want_s2"][:n * sb]
+    assert bytes(o1.cpu().numpy()) == b["want_s1"][:n * sb]
+    # golden t = 67 random subsets (oracle outputs), both aggregates through the fused entry
+    d = golden("aggregate_g2_t67_subsets.json")
+    t = d["threshold"]
+    table = {}
+    for case in d["cases"]:
+        for i, x, ys in zip(case["ids"], case["X"], case["Y"]):
+            table[i] = (x, ys)
+    ids = sorted(table)
+    ctx.set_issuers(ids, _cat(table[i][0] for i in ids), _cat(y for i in ids for y in table[i][1]), d["q"])
+    for case in d["cases"]:
+        L = len(case["ids"])
+        g_ids = torch.from_numpy(np.array(case["ids"], dtype=np.uint64).view(np.int64)).to(dev)
+        g1 = torch.frombuffer(bytearray(_cat(case["sigma1"])), dtype=torch.uint8).to(dev)
+        g2 = torch.frombuffer(bytearray(_cat(case["sigma2"])), dtype=torch.uint8).to(dev)
+        r1, r2 = (torch.zeros(sb, dtype=torch.uint8, device=dev) for _ in range(2))
+        rX = torch.zeros(ob, dtype=torch.uint8, device=dev)
+        rY = torch.zeros(d["q"] * ob, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        assert lib.cc_aggregate_credential_batch_device(ctx.h, 1, L, t, P(g_ids), P(g1), P(g2), P(r1), P(r2),
+                                                        P(rX), P(rY), None) == 0
+        assert ctx.device_error() == 0
+        assert bytes(r2.cpu().numpy()).hex() == case["out_sigma2"]
+        assert bytes(r1.cpu().numpy()).hex() == case["out_sigma1"]
+        assert bytes(rX.cpu().numpy()).hex() == case["out_X"]
+        oy = bytes(rY.cpu().numpy())
+        assert [oy[j * ob:(j + 1) * ob].hex() for j in range(d["q"])] == case["out_Y"]
+
+
 def test_config5_full_size_pok_device(ctxs):
     """65,536 PoK proofs (q = 32, 8 revealed) through cc_pok_verify_batch_device: verdicts equal
     construction (1/16 corrupted responses); the host entry point agrees on a slice."""
