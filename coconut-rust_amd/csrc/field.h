@@ -355,15 +355,6 @@ constexpr uint32_t PINV30 = 0x30003u;
 #define CC_R3_LIMBS                                                                             \
     0x49217d6au, 0x73ac2317u, 0x73c452c4u, 0x2c409357u, 0x79c0a55eu, 0xfe1f49acu, 0xaaa3c553u, \
         0x1bdc0da2u, 0xc3f31a9du, 0x75d3a486u, 0x84da1a2du, 0x15e5ecfbu
-// -(2i+1)^-1 mod 256
-__constant__ static const uint8_t kInv256[128] = {
-    255, 85,  51,  73,  199, 93,  59,  17,  15,  229, 195, 89,  215, 237, 203, 33,  31,  117, 83,  105, 231, 125,
-    91,  49,  47,  5,   227, 121, 247, 13,  235, 65,  63,  149, 115, 137, 7,   157, 123, 81,  79,  37,  3,   153,
-    23,  45,  11,  97,  95,  181, 147, 169, 39,  189, 155, 113, 111, 69,  35,  185, 55,  77,  43,  129, 127, 213,
-    179, 201, 71,  221, 187, 145, 143, 101, 67,  217, 87,  109, 75,  161, 159, 245, 211, 233, 103, 253, 219, 177,
-    175, 133, 99,  249, 119, 141, 107, 193, 191, 21,  243, 9,   135, 29,  251, 209, 207, 165, 131, 25,  151, 173,
-    139, 225, 223, 53,  19,  41,  167, 61,  27,  241, 239, 197, 163, 57,  183, 205, 171, 1};
-
 DEV int32_t p30_limb(int j) {
     constexpr int32_t P[S30N] = {CC_P30_LIMBS};
     return P[j];
@@ -371,7 +362,7 @@ DEV int32_t p30_limb(int j) {
 
 // 30 divsteps on the low words of f, g (f odd); returns the new eta (= -delta) and the matrix t
 // with 2^30 [f', g'] = t [f, g].  Zero runs of g are consumed at once; otherwise up to 8 low bits of
-// g are cancelled by one multiple of f (the 8-bit inverse table).
+// g are cancelled by one multiple of f (-f^-1 mod 256 from two Newton steps).
 DEV int32_t divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
     uint32_t u = 1, v = 0, q = 0, r = 1;
     int i = 30;
@@ -397,7 +388,11 @@ DEV int32_t divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
         }
         const int limit = (eta + 1) > i ? i : (eta + 1);
         const uint32_t m = (0xffffffffu >> (32 - limit)) & 255u;
-        const uint32_t w = (g * (uint32_t)kInv256[(f >> 1) & 127]) & m;
+        // -f^-1 mod 256 by Newton's iteration (f odd): (3f) ^ 2 is f^-1 to 5 bits, one step gives 10
+        // (a table lookup here was a vector memory load with its full latency, every iteration)
+        uint32_t fi = (3u * f) ^ 2u;
+        fi *= 2u - f * fi;
+        const uint32_t w = (g * (0u - fi)) & m;
         g += f * w;
         q += u * w;
         r += v * w;

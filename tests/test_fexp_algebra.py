@@ -64,6 +64,13 @@ P30 = [(P >> (30 * i)) & M30 for i in range(N)]
 INV256 = [(-pow(2 * i + 1, -1, 256)) % 256 for i in range(128)]
 
 
+def _neg_inv256(f):
+    """field.h divsteps30: -f^-1 mod 256 by Newton's iteration from (3f) ^ 2 (32-bit wrapping)."""
+    fi = _u32(3 * f) ^ 2
+    fi = _u32(fi * _u32(2 - f * fi))
+    return _u32(-fi)
+
+
 def _u32(x):
     return x & 0xFFFFFFFF
 
@@ -71,6 +78,12 @@ def _u32(x):
 def _i32(x):
     x &= 0xFFFFFFFF
     return x - (1 << 32) if x >> 31 else x
+
+
+def test_newton_inverse_matches_the_table():
+    """Every odd 32-bit word's Newton inverse agrees with -f^-1 mod 256 on the low byte."""
+    for f in list(range(1, 1 << 12, 2)) + [0xFFFFFFFF, 0x80000001, 0xDEADBEEF]:
+        assert _neg_inv256(f) & 255 == INV256[(f >> 1) & 127], f
 
 
 def _divsteps(eta, f, g):
@@ -87,7 +100,7 @@ def _divsteps(eta, f, g):
             u, q = q, _u32(-u)
             v, r = r, _u32(-v)
         limit = min(eta + 1, i)
-        w = _u32(g * INV256[(f >> 1) & 127]) & (0xFFFFFFFF >> (32 - limit)) & 255
+        w = _u32(g * _neg_inv256(f)) & (0xFFFFFFFF >> (32 - limit)) & 255
         g, q, r = _u32(g + f * w), _u32(q + u * w), _u32(r + v * w)
     return eta, [_i32(u), _i32(v), _i32(q), _i32(r)]
 
