@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "codec.h"
+#include "curve_lz.h"
 #include "curve_pl.h"
 #include "fixed.h"
 #include "fr.h"
@@ -294,110 +295,124 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus(size_t ntask, size_t t, c
     }
 }
 
-// G2 bases on the pair-lane Fp2 (curve_pl.h): the same algorithm with ONE task lane per lane PAIR
-// (lane 2i + h holds half h of every Fp2 coordinate).  The one-lane G2 form of this kernel needs 512
-// VGPRs (1 wave/SIMD, spills) and runs a full doubling chain per lane; the pair form keeps a Jacobian
-// G2 point in 3 Fp a lane (2 waves/SIMD) and halves each lane's share of every Fp2 product.  L2 pairs
-// per task take the bases k = pair, pair + L2, ...; the scratch layout is straus_words<Fp2> with
-// each entry's two halves side by side ([entry][half][words]).
-// One task's share on one lane pair: multiples of the bases k = pair, pair + NG, ... built and
-// batch-normalised, then the 65 windows over them into acc (pl form, this lane's half)
-DEV void straus_g2pl_pair(cc::Jac<pl::Fp2>& acc, int NG, int pair, int h, size_t task, size_t t,
+// G2 bases on the lazy pair-lane field (curve_lz.h): the same algorithm with ONE task lane per lane
+// PAIR (lane 2i + h holds half h of every Fp2 coordinate) and lazy radix-2^28 arithmetic (no conversion
+// per multiplication, carry-free additions, identity and exceptional cases tested on reduced values).
+// The pair form keeps a Jacobian G2 point in 3 Fp a lane (2 waves/SIMD) and halves each lane's share of
+// every Fp2 product; the one-lane G2 form needed 512 VGPRs.  NG pairs per task take the bases
+// k = pair, pair + NG, ...  Scratch per task (lazy words, each entry's two halves side by side):
+// 8t Jacobian entries [entry][half][3 LN + 1] (x, y, z, infinity flag; affine x, y written back in
+// place), 8t prefix products [entry][half][LN], 65t digit bytes.
+__host__ __device__ inline size_t straus_lz_words(size_t t) {
+    return t * 8 * 2 * (3 * lz::LN + 1) + t * 8 * 2 * lz::LN + (t * 65 + 3) / 4;
+}
+DEV void st_w(uint32_t* w, const lz::F2R& x) {
+#pragma unroll
+    for (int c = 0; c < lz::LN; c++) w[c] = (uint32_t)x.c.v[c];
+}
+DEV lz::F2R ld_w(const uint32_t* w) {
+    lz::F2R x;
+#pragma unroll
+    for (int c = 0; c < lz::LN; c++) x.c.v[c] = (int32_t)w[c];
+    return x;
+}
+// One task's share on one lane pair: multiples of its bases built and batch-normalised, then the 65
+// windows over them into acc
+DEV void straus_g2lz_pair(lz::JL& acc, int NG, int pair, int h, size_t task, size_t t,
                           const uint8_t* __restrict__ pts, size_t pt_stride, size_t pt_jstride, size_t pt_step,
                           const uint32_t* __restrict__ l, size_t l_div, uint32_t* __restrict__ scratch) {
-    using F = pl::Fp2;
-    using T = FT<F>;
-    constexpr int JW = 3 * NL, PW = NL;  // one lane's half of a Jacobian entry / of an Fp2
+    using namespace lz;
+    constexpr int JW = 3 * LN + 1;
     const size_t cred = task / l_div;
     const uint8_t* base = pts + cred * pt_stride + (task % l_div) * pt_jstride;
     const uint32_t* lk = l + cred * t * 8;
-    uint32_t* ent = scratch + task * straus_words<Fp2>(t);
-    uint32_t* pre = ent + t * 8 * (2 * JW);
-    int8_t* dig = reinterpret_cast<int8_t*>(pre + t * 8 * (2 * PW));
-    jac_set_inf(acc);
-    F acc_z;
-    T::one(acc_z);
+    uint32_t* ent = scratch + task * straus_lz_words(t);
+    uint32_t* pre = ent + t * 8 * 2 * JW;
+    int8_t* dig = reinterpret_cast<int8_t*>(pre + t * 8 * 2 * LN);
+    acc = jl_inf();
+    F2R acc_z = r_one();
 #pragma unroll 1
     for (size_t k = pair; k < t; k += NG) {
         cc::Aff<cc::Fp2> P1;
         const bool ok = pl::pair_all(g2_decode(P1, base + k * pt_step));  // both lanes decode the point
         recode_w4(dig + k * 65, lk + k * 8);                            // both write the same digits
-        cc::Aff<F> P;
-        P.x.c = h ? P1.x.b : P1.x.a;
-        P.y.c = h ? P1.y.b : P1.y.a;
-        cc::Jac<F> J;
-        if (ok) jac_from_aff(J, P);
-        else jac_set_inf(J);
+        pl::Fp2 hx, hy;
+        hx.c = h ? P1.x.b : P1.x.a;
+        hy.c = h ? P1.y.b : P1.y.a;
+        const AL P{reduce(in_r2(hx)), reduce(in_r2(hy))};
+        JL J = ok ? jl_from_aff(P) : jl_inf();
 #pragma unroll 1
         for (int d = 0; d < 8; d++) {
-            if (d == 1) jac_dbl(J, J);
-            else if (d > 1 && ok) jac_add_aff(J, J, P);
+            if (d == 1) J = jl_dbl(J);
+            else if (d > 1 && ok) J = jl_add_aff(J, P);
             const size_t e = k * 8 + d;
             uint32_t* w = ent + (e * 2 + h) * JW;
-            const uint32_t* jw = reinterpret_cast<const uint32_t*>(&J);
-            for (int c = 0; c < JW; c++) w[c] = jw[c];
-            for (int c = 0; c < PW; c++) pre[(e * 2 + h) * PW + c] = acc_z.c.v[c];
-            if (!jac_is_inf(J)) T::mul(acc_z, acc_z, J.z);
+            const bool inf = jl_is_inf(J);
+            st_w(w, J.x);
+            st_w(w + LN, J.y);
+            st_w(w + 2 * LN, J.z);
+            w[3 * LN] = inf ? 1u : 0u;
+            st_w(pre + (e * 2 + h) * LN, acc_z);
+            if (!inf) acc_z = reduce(mulr(acc_z, J.z));
         }
     }
-    F inv;
-    T::inv(inv, acc_z);
+    F2R zinv = reduce(inv(acc_z));
     if (t > (size_t)pair) {
         const long long kmax = (long long)(((t - 1 - pair) / NG) * NG + pair);
 #pragma unroll 1
         for (long long kk = kmax; kk >= pair; kk -= NG) {
+#pragma unroll 1
             for (int d = 7; d >= 0; d--) {
                 const size_t e = (size_t)kk * 8 + d;
-                cc::Jac<F> J;
                 uint32_t* w = ent + (e * 2 + h) * JW;
-                uint32_t* jw = reinterpret_cast<uint32_t*>(&J);
-                for (int c = 0; c < JW; c++) jw[c] = w[c];
-                const bool inf = jac_is_inf(J);
-                if (!inf) {
-                    F pz, zi, zi2;
-                    for (int c = 0; c < PW; c++) pz.c.v[c] = pre[(e * 2 + h) * PW + c];
-                    T::mul(zi, inv, pz);
-                    T::mul(inv, inv, J.z);
-                    T::sqr(zi2, zi);
-                    T::mul(J.x, J.x, zi2);
-                    T::mul(zi2, zi2, zi);
-                    T::mul(J.y, J.y, zi2);
-                }
-                for (int c = 0; c < 2 * PW; c++) w[c] = jw[c];  // this half's affine x, y
-                w[2 * PW] = inf ? 1u : 0u;
+                if (w[3 * LN]) continue;  // identity multiple (pair-uniform: both halves carry the flag)
+                const F2R z = ld_w(w + 2 * LN);
+                const auto zi = mulr(zinv, ld_w(pre + (e * 2 + h) * LN));
+                zinv = reduce(mulr(zinv, z));
+                const auto zi2 = sqrr(zi);
+                st_w(w, reduce(mulr(ld_w(w), zi2)));
+                st_w(w + LN, reduce(mulr(ld_w(w + LN), mulr(zi2, zi))));
             }
         }
     }
 #pragma unroll 1
     for (int win = 64; win >= 0; win--) {
-        if (win != 64 && !jac_is_inf(acc))
-            for (int z = 0; z < 4; z++) jac_dbl(acc, acc);
+        if (win != 64 && !jl_is_inf(acc))
+#pragma unroll 1
+            for (int z = 0; z < 4; z++) acc = jl_dbl(acc);
 #pragma unroll 1
         for (size_t k = pair; k < t; k += NG) {
             const int d = dig[k * 65 + win];
             if (!d) continue;
             const uint32_t* w = ent + ((k * 8 + (d < 0 ? -d : d) - 1) * 2 + h) * JW;
-            if (w[2 * PW]) continue;  // identity multiple (pair-uniform: both halves carry the flag)
-            cc::Aff<F> e;
-            for (int c = 0; c < PW; c++) {
-                e.x.c.v[c] = w[c];
-                e.y.c.v[c] = w[PW + c];
-            }
-            if (d < 0) T::neg(e.y, e.y);
-            jac_add_aff(acc, acc, e);
+            if (w[3 * LN]) continue;  // identity multiple
+            AL e{ld_w(w), ld_w(w + LN)};
+            if (d < 0) e = jl_neg_aff(e);
+            acc = jl_add_aff(acc, e);
         }
     }
 }
 
-DEV void straus_g2pl_out(const cc::Jac<pl::Fp2>& acc, int h, uint8_t* out) {
-    cc::Aff<pl::Fp2> r;
-    const bool fin = jac_to_aff(r, acc);
-    const Fp xs = pl::swp(r.x.c), ys = pl::swp(r.y.c);
+// affine encoding (amcl_wrapper to_bytes) of a lane-pair point; lane h = 0 writes
+DEV void straus_g2lz_out(const lz::JL& acc, int h, uint8_t* out) {
+    using namespace lz;
     cc::Aff<cc::Fp2> o;
-    o.x.a = h ? xs : r.x.c;
-    o.x.b = h ? r.x.c : xs;
-    o.y.a = h ? ys : r.y.c;
-    o.y.b = h ? r.y.c : ys;
+    const bool fin = !jl_is_inf(acc);
+    pl::Fp2 x, y;
+    if (fin) {
+        const auto zi = inv(acc.z);
+        const auto zi2 = sqrr(zi);
+        x = out_r2(mulr(acc.x, zi2));
+        y = out_r2(mulr(acc.y, mulr(zi2, zi)));
+    } else {
+        fp_zero(x.c);
+        fp_zero(y.c);
+    }
+    const Fp xs = pl::swp(x.c), ys = pl::swp(y.c);
+    o.x.a = h ? xs : x.c;
+    o.x.b = h ? x.c : xs;
+    o.y.a = h ? ys : y.c;
+    o.y.b = h ? y.c : ys;
     if (!h) g2_encode(out, o, fin);
 }
 
@@ -405,40 +420,46 @@ DEV void straus_g2pl_out(const cc::Jac<pl::Fp2>& acc, int h, uint8_t* out) {
 // pairs' partial sums meet in LDS and pair 0 adds them.  G is chosen so the launch's waves
 // fill whole rounds of the 2 waves/SIMD the registers allow (cck_msm_straus): 10,000 tasks at 8 pairs
 // are 2,500 waves, 1.22 rounds of an MI355X's 2,048 slots, the last one a fifth full.
-__global__ __launch_bounds__(256, 2) void k_msm_straus_g2pl_g(int G, size_t ntask, size_t t,
+__global__ __launch_bounds__(256, 2) void k_msm_straus_g2lz_g(int G, size_t ntask, size_t t,
                                                              const uint8_t* __restrict__ pts, size_t pt_stride,
                                                              size_t pt_jstride, size_t pt_step,
                                                              const uint32_t* __restrict__ l, size_t l_div,
                                                              uint32_t* __restrict__ scratch,
                                                              uint8_t* __restrict__ out) {
-    constexpr int JW = 3 * NL;
-    __shared__ uint32_t red[256 * JW];
+    constexpr int JW = 3 * lz::LN;
+    __shared__ int32_t red[256 * JW];
     const int L = 2 * G, TB = (int)blockDim.x / L;
     const int tib = (int)threadIdx.x / L, lit = (int)threadIdx.x % L;
     const size_t task = (size_t)blockIdx.x * TB + tib;
     const int pair = lit >> 1, h = lit & 1;
     const bool active = task < ntask;  // pair-uniform; every lane reaches the barrier
-    cc::Jac<pl::Fp2> acc;
+    lz::JL acc;
     if (active)
-        straus_g2pl_pair(acc, G, pair, h, task, t, pts, pt_stride, pt_jstride, pt_step, l, l_div, scratch);
+        straus_g2lz_pair(acc, G, pair, h, task, t, pts, pt_stride, pt_jstride, pt_step, l, l_div, scratch);
     else
-        jac_set_inf(acc);
+        acc = lz::jl_inf();
     {
-        const uint32_t* aw = reinterpret_cast<const uint32_t*>(&acc);
-        uint32_t* my = red + threadIdx.x * JW;
-        for (int c = 0; c < JW; c++) my[c] = aw[c];
+        int32_t* my = red + threadIdx.x * JW;
+        for (int c = 0; c < lz::LN; c++) {
+            my[c] = acc.x.c.v[c];
+            my[lz::LN + c] = acc.y.c.v[c];
+            my[2 * lz::LN + c] = acc.z.c.v[c];
+        }
     }
     __syncthreads();
     if (active && pair == 0) {
 #pragma unroll 1
         for (int p = 1; p < G; p++) {
-            cc::Jac<pl::Fp2> o;
-            uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
-            const uint32_t* src = red + (tib * L + 2 * p + h) * JW;
-            for (int c = 0; c < JW; c++) ow[c] = src[c];
-            jac_add(acc, acc, o);
+            lz::JL o;
+            const int32_t* src = red + (tib * L + 2 * p + h) * JW;
+            for (int c = 0; c < lz::LN; c++) {
+                o.x.c.v[c] = src[c];
+                o.y.c.v[c] = src[lz::LN + c];
+                o.z.c.v[c] = src[2 * lz::LN + c];
+            }
+            acc = lz::jl_add(acc, o);
         }
-        straus_g2pl_out(acc, h, out + task * 192);
+        straus_g2lz_out(acc, h, out + task * 192);
     }
 }
 
@@ -814,7 +835,7 @@ int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-size_t cck_straus_words(int group, size_t t) { return group == 1 ? straus_words<Fp>(t) : straus_words<Fp2>(t); }
+size_t cck_straus_words(int group, size_t t) { return group == 1 ? straus_words<Fp>(t) : straus_lz_words(t); }
 
 int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
                    size_t pt_step, const uint32_t* d_l, size_t l_div, uint32_t* d_scratch, uint8_t* d_out,
@@ -845,7 +866,7 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
         }
     }
     const int L = 2 * G, tb = 256 / L;
-    hipLaunchKernelGGL(k_msm_straus_g2pl_g, dim3((unsigned)((ntask + tb - 1) / tb)), dim3(tb * L), 0, st, G, ntask, t,
+    hipLaunchKernelGGL(k_msm_straus_g2lz_g, dim3((unsigned)((ntask + tb - 1) / tb)), dim3(tb * L), 0, st, G, ntask, t,
                        d_pts, pt_stride, pt_jstride, pt_step, d_l, l_div, d_scratch, d_out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
