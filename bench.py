@@ -45,7 +45,6 @@ MADS_PER_M = 288   # one Montgomery multiplication: 12x12 a*b + 12x12 m*p 32x32-
 UBENCH = os.path.join(ROOT, "profiles", "r02_ubench_int.jsonl")
 HBM_PEAK_GBS = 8000.0
 OPCOUNT = os.path.join(ROOT, "tests", "fixtures", "opcount.json")
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_summary.json")
 # per-mode rocprofv3 evidence of the current build (tools/gpu_modes_prof.sh): kernel-trace stats and the
 # PMC passes of one bench step, summarised per kernel by tools/pmc_summary.py
 PROFILE_DIR = os.path.join(ROOT, "profiles", "r03", "modes")
@@ -70,12 +69,12 @@ def opcounts(key):
 
 
 def pmc(kernel_key, mode=None):
-    """Per-launch PMC figures of the same build (profiles/r03/modes/<mode>/pmc_summary.json, else
-    profiles/r02/pmc_summary.json; separate rocprofv3 --pmc passes, tools/pmc_summary.py): HBM bytes =
+    """Per-launch PMC figures of the same build (profiles/r03/modes/<mode>/pmc_summary.json; separate
+    rocprofv3 --pmc passes, tools/pmc_summary.py; none if that mode has no committed summary): HBM bytes =
     2 x FETCH_SIZE (gfx950 counts half of wide reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, and VALU
     wave-instructions per CU per clock."""
     d = None
-    for path in ([os.path.join(PROFILE_DIR, mode, "pmc_summary.json")] if mode else []) + [PMC_SUMMARY]:
+    for path in [os.path.join(PROFILE_DIR, mode, "pmc_summary.json")] if mode else []:
         try:
             with open(path) as f:
                 d = json.load(f)
@@ -326,9 +325,11 @@ def cpu_baseline_verify(batch, value, what="shared vk"):
         "single_thread": round(v_1, 1),
         "per_thread_efficiency": round(eff, 3),
         "nproc": nproc, "affinity_cpus": aff, "cpu_model": model,
-        "threads_note": f"timed on the {thr}-CPU share this box grants per GPU (OMP_NUM_THREADS); the pool does "
-                        f"not allow a job to load all {nproc} host CPUs, so the whole host is extrapolated: "
-                        "single_thread x nproc x per_thread_efficiency",
+        "threads_note": f"timed on the {thr}-CPU share this box grants per GPU (OMP_NUM_THREADS); the pool's rules "
+                        f"cap a one-GPU job at that share (worker pools sized to it; nproc = {nproc} counts the whole "
+                        "machine), so all cores are NOT timed: the whole host is extrapolated as single_thread x nproc "
+                        "x per_thread_efficiency (all_cores_extrapolated), and gpu_over_cpu quotes that conservative "
+                        "ratio",
         "all_cores_extrapolated": round(host, 1),
         "gpu_over_cpu": round(value / host, 2),
         "gpu_over_cpu_share": round(value / v_mt, 1),

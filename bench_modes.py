@@ -208,7 +208,7 @@ def bench_aggregate(args):
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": round(ach / peak, 4),
                          "traffic": (rk or {}).get("kernels", {}).get(
-                             "k_msm_straus_g2pl_g" if dom == "signature_msm" else "k_vk_agg_fixed<cc::Fp, 8>",
+                             "k_msm_straus_g2lz_g" if dom == "signature_msm" else "k_vk_agg_fixed<cc::Fp, 8>",
                              {}).get("hbm_bytes_per_launch"),
                          "traffic_unit": "HBM-side bytes per launch (PMC, 2 x FETCH_SIZE + WRITE_SIZE)"},
             "kernels": {"lagrange_ms": round(phase[0], 3),

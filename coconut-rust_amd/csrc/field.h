@@ -404,16 +404,24 @@ DEV int32_t divsteps30(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
     return eta;
 }
 
+// c + a b for signed 32-bit a, b (one v_mad_i64_i32: left to itself the compiler multiplies these
+// sign-extended, 64 x 64 bits, with two extra v_mul_lo_u32 and a v_add3)
+DEV int64_t smad(int32_t a, int32_t b, int64_t c) {
+    int64_t r;
+    uint64_t cy;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(cy) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 // [f, g] <- t [f, g] / 2^30 (exact)
 DEV void s30_update_fg(S30& f, S30& g, const int32_t t[4]) {
-    int64_t cf = (int64_t)t[0] * f.v[0] + (int64_t)t[1] * g.v[0];
-    int64_t cg = (int64_t)t[2] * f.v[0] + (int64_t)t[3] * g.v[0];
+    int64_t cf = smad(t[1], g.v[0], smad(t[0], f.v[0], 0));
+    int64_t cg = smad(t[3], g.v[0], smad(t[2], f.v[0], 0));
     cf >>= 30;
     cg >>= 30;
 #pragma unroll
     for (int i = 1; i < S30N; i++) {
-        cf += (int64_t)t[0] * f.v[i] + (int64_t)t[1] * g.v[i];
-        cg += (int64_t)t[2] * f.v[i] + (int64_t)t[3] * g.v[i];
+        cf = smad(t[1], g.v[i], smad(t[0], f.v[i], cf));
+        cg = smad(t[3], g.v[i], smad(t[2], f.v[i], cg));
         f.v[i - 1] = (int32_t)cf & M30;
         g.v[i - 1] = (int32_t)cg & M30;
         cf >>= 30;
@@ -429,18 +437,18 @@ DEV void s30_update_de(S30& d, S30& e, const int32_t t[4]) {
     const int32_t sd = d.v[S30N - 1] >> 31, se = e.v[S30N - 1] >> 31;
     int32_t md = (t[0] & sd) + (t[1] & se);
     int32_t me = (t[2] & sd) + (t[3] & se);
-    int64_t cd = (int64_t)t[0] * d.v[0] + (int64_t)t[1] * e.v[0];
-    int64_t ce = (int64_t)t[2] * d.v[0] + (int64_t)t[3] * e.v[0];
+    int64_t cd = smad(t[1], e.v[0], smad(t[0], d.v[0], 0));
+    int64_t ce = smad(t[3], e.v[0], smad(t[2], d.v[0], 0));
     md -= (int32_t)((PINV30 * (uint32_t)cd + (uint32_t)md) & (uint32_t)M30);
     me -= (int32_t)((PINV30 * (uint32_t)ce + (uint32_t)me) & (uint32_t)M30);
-    cd += (int64_t)p30_limb(0) * md;
-    ce += (int64_t)p30_limb(0) * me;
+    cd = smad(p30_limb(0), md, cd);
+    ce = smad(p30_limb(0), me, ce);
     cd >>= 30;
     ce >>= 30;
 #pragma unroll
     for (int i = 1; i < S30N; i++) {
-        cd += (int64_t)t[0] * d.v[i] + (int64_t)t[1] * e.v[i] + (int64_t)p30_limb(i) * md;
-        ce += (int64_t)t[2] * d.v[i] + (int64_t)t[3] * e.v[i] + (int64_t)p30_limb(i) * me;
+        cd = smad(p30_limb(i), md, smad(t[1], e.v[i], smad(t[0], d.v[i], cd)));
+        ce = smad(p30_limb(i), me, smad(t[3], e.v[i], smad(t[2], d.v[i], ce)));
         d.v[i - 1] = (int32_t)cd & M30;
         e.v[i - 1] = (int32_t)ce & M30;
         cd >>= 30;
