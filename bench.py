@@ -366,6 +366,8 @@ def bench_verify(args, mode):
     batch = make_verify_batch(ctx, mode, n, q, seed=1000 + rank + 100 * mode)
     ctx.set_params(batch["g_tilde"])
     t_vk = time.perf_counter()
+    if args.vk_bits:
+        ctx.set_table_bits(args.vk_bits, 0)
     ctx.set_verkey(batch["X"], batch["Y"])
     vk_ms = (time.perf_counter() - t_vk) * 1e3
     setup_s = time.perf_counter() - t_setup
@@ -457,7 +459,8 @@ def bench_verify(args, mode):
             "pcie_inclusive": {"value": round(pcie_rate, 1) if pcie_rate else None, "unit": "credentials/s",
                                "note": "cc_verify_batch with host buffers: H2D of the serialized batch + D2H "
                                        "of verdicts included (not `value`)"},
-            "setup": {"verkey_tables_ms": round(vk_ms, 1), "synthetic_data_s": round(setup_s, 2)},
+            "setup": {"verkey_tables_ms": round(vk_ms, 1), "verkey_table_bits": ctx.table_bits()[0],
+                      "synthetic_data_s": round(setup_s, 2)},
         }
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline_verify(batch, value)
@@ -483,6 +486,8 @@ def bench_rlc(args):
     ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
     batch = make_verify_batch(ctx, 0, n, q, seed=3000 + rank, bad_every=0)
     ctx.set_params(batch["g_tilde"])
+    if args.vk_bits:
+        ctx.set_table_bits(args.vk_bits, 0)
     ctx.set_verkey(batch["X"], batch["Y"])
     d_s1, d_s2, d_m = to_dev(batch["s1"], dev), to_dev(batch["s2"], dev), to_dev(batch["msgs"], dev)
     eng = DeviceEngine(ctx, n, q, d_s1, d_s2, d_m, base_index=rank * n)
@@ -599,6 +604,8 @@ def main():
     ap.add_argument("--n", type=int, default=0, help="credentials per GPU per step (0 = the config's size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) rate")
+    ap.add_argument("--vk-bits", type=int, default=0,
+                    help="verkey table window width (cc_set_table_bits; 0 = the library's choice)")
     ap.add_argument("--mode", choices=["verify", "verify-g1", "rlc", "aggregate", "pok", "stub"], default="verify")
     args = ap.parse_args()
     if args.backend:

@@ -265,6 +265,8 @@ def bench_pok(args):
     b = make_pok_batch(ctx, 0, n, seed=5000 + rank)
     gen_s = time.perf_counter() - t0
     ctx.set_params(b["g_tilde"])
+    if args.vk_bits:
+        ctx.set_table_bits(args.vk_bits, 0)
     ctx.set_verkey(b["X"], b["Y"])
     q, r, nresp = b["q"], len(b["revealed"]), b["nresp"]
     D = {k: to_dev(b[k], dev) for k in ("s1", "s2", "J", "T", "resp", "chal", "rev")}
@@ -307,7 +309,7 @@ def bench_pok(args):
                          "traffic_unit": "HBM-side bytes per launch (PMC, 2 x FETCH_SIZE + WRITE_SIZE)"},
             "kernels": kt,
             "rocprof_kernels": kernel_pmc_report("pok"),
-            "setup": {"synthetic_data_s": round(gen_s, 2)},
+            "setup": {"synthetic_data_s": round(gen_s, 2), "verkey_table_bits": ctx.table_bits()[0]},
         }
         if not args.no_cpu_baseline and world == 1:
             oc = __import__("bench")._oracle()

@@ -53,6 +53,7 @@ int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uin
 int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
              uint8_t* d_gt, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
+int cck_h_input_canon(int group, size_t n, size_t len, int kn, uint8_t* d_data, hipStream_t st);
 
 size_t cck_straus_words(int group, size_t t);
 int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size_t pt_stride, size_t pt_jstride,
@@ -357,7 +358,8 @@ static cc_status subgroup_host(cc_ctx* c, int group, size_t n, const uint8_t* by
 // Shared-verkey tables: 16-bit windows (half the additions of 8-bit ones; 100 / 200 MB per G1 / G2
 // base) when the q + 2 bases' tables fit half the free HBM (at most 64 GiB), else 8-bit windows
 // (32 x 255 entries, 0.8 / 1.6 MB a base); a failed 16-bit allocation falls back to 8 bits.
-// cc_set_table_bits forces either width.  On failure the caller leaves the context without a verkey.
+// cc_set_table_bits forces a width in [8, 22] (ceil(256 / w) windows of 2^w - 1 entries: 20 bits = 13
+// windows, 1.3 / 2.6 GB a G1 / G2 base).  On failure the caller leaves the context without a verkey.
 static cc_status rebuild_tables(cc_ctx* c) {
     // bases for the fixed-base tables: Y~[0..q), g~ (PoK Schnorr base), X~ (RLC) -> q + 2 bases
     int og = oth_group(c->mode);
@@ -368,7 +370,7 @@ static cc_status rebuild_tables(cc_ctx* c) {
     // the old table is released first so its memory counts as free
     c->table.release();
     const double fr = (double)free_hbm();
-    if (wb != 8 && wb != 16) {
+    if (!wb) {
         const double want = (double)nb * (double)tab_words(og, 16) * 4.0;
         const double cap = std::min(0.5 * fr, 64.0 * (double)(1ull << 30));
         wb = want <= cap ? 16 : 8;
@@ -377,12 +379,12 @@ static cc_status rebuild_tables(cc_ctx* c) {
     // for sizes above it (the runtime may over-commit), and a build kernel writing such a table would not
     // end well
     if (fr > 0 && (double)nb * (double)tab_words(og, wb) * 4.0 > 0.9 * fr) {
-        if (c->force_vk_bits == 16 || wb == 8) return CC_ERR_HIP;
+        if (c->force_vk_bits || wb == 8) return CC_ERR_HIP;
         wb = 8;
     }
     if (c->table.ensure((size_t)nb * tab_words(og, wb) * 4)) {
         (void)hipGetLastError();  // clear the failed allocation's error
-        if (wb == 8 || c->force_vk_bits == 16) return CC_ERR_HIP;
+        if (wb == 8 || c->force_vk_bits) return CC_ERR_HIP;
         wb = 8;
         if (c->table.ensure((size_t)nb * tab_words(og, wb) * 4)) return CC_ERR_HIP;
     }
@@ -494,7 +496,7 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
 }
 
 cc_status cc_set_table_bits(cc_ctx* c, int verkey_bits, int issuer_bits) {
-    if (!c || (verkey_bits != 0 && verkey_bits != 8 && verkey_bits != 16) ||
+    if (!c || (verkey_bits != 0 && (verkey_bits < 8 || verkey_bits > 22)) ||
         (issuer_bits != 0 && (issuer_bits < 8 || issuer_bits > 16)))
         return CC_ERR_DECODE;
     for (cc_ctx* p : c->peers) {
@@ -959,10 +961,14 @@ static cc_status compute_h_batch(cc_ctx* c, size_t n, size_t q, size_t k, const 
     if (s) return s;
     if (d_h.ensure(n * sb) || d_fail.ensure(4)) return CC_ERR_HIP;
     HIPCK(hipMemsetAsync(d_fail.p, 0, 4, c->stream));
+    // the reference hashes commitment.to_bytes() and the known messages' to_bytes() (canonical)
+    KCK(cck_h_input_canon(sig_group(c->mode), n, len, (int)kn, d_data.as<uint8_t>(), c->stream));
     KCK(cck_hash_to_curve(sig_group(c->mode), n, d_data.as<uint8_t>(), d_off.as<uint64_t>(), d_h.as<uint8_t>(),
                           d_fail.as<uint32_t>(), c->stream));
+    uint32_t fail = 0;
+    HIPCK(hipMemcpyAsync(&fail, d_fail.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCK(hipStreamSynchronize(c->stream));
-    return CC_OK;
+    return fail ? CC_ERR_DECODE : CC_OK;  // as cc_hash_to_curve
 }
 
 cc_status cc_blind_sign_batch(cc_ctx* c, size_t n, size_t q, size_t k, const uint8_t* commitment, const uint8_t* known,

@@ -24,7 +24,7 @@ __host__ __device__ constexpr size_t ft_base_words(int wbits) {
     return (size_t)ft_nwin(wbits) * ft_went(wbits) * (sizeof(Aff<F>) / 4);
 }
 
-// window w of a canonical scalar given as 8 little-endian 32-bit limbs (wbits in [8, 16])
+// window w of a canonical scalar given as 8 little-endian 32-bit limbs (wbits in [8, 22])
 DEV uint32_t ft_digit(const uint32_t k[8], int w, int wbits) {
     if (wbits == 16) return (k[w >> 1] >> (16 * (w & 1))) & 0xffffu;
     if (wbits == 8) return (k[w >> 2] >> (8 * (w & 3))) & 0xffu;

@@ -42,6 +42,37 @@ struct ProofLayout {
 
 }  // namespace
 
+// SignatureRequest::compute_h's input rows (signature.rs:197-206 hashes commitment.to_bytes() ||
+// known_messages[i].to_bytes()): the caller's commitment bytes are decoded and re-encoded (an
+// off-curve or non-canonical encoding becomes what amcl_wrapper's to_bytes of the decoded point
+// gives) and every known message is reduced mod r into its canonical 48-byte encoding, in place.
+// One row (len = SignatureGroup bytes + 48 kn) per lane.
+template <class F>
+__global__ __launch_bounds__(64) void k_h_input_canon(size_t n, size_t len, int kn, uint8_t* __restrict__ data) {
+    const size_t r = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    uint8_t* row = data + r * len;
+    Aff<F> a;
+    const bool fin = dec_pt<F>(a, row);
+    if (sizeof(F) == sizeof(Fp)) g1_encode(row, *reinterpret_cast<Aff<Fp>*>(&a), fin);
+    else g2_encode(row, *reinterpret_cast<Aff<Fp2>*>(&a), fin);
+#pragma unroll 1
+    for (int j = 0; j < kn; j++) {
+        uint8_t* p = row + eb<F>() + 48 * (size_t)j;
+        Fp raw;
+        be48_bytes(raw, p);
+        uint32_t hi = raw.v[8] | raw.v[9] | raw.v[10] | raw.v[11], br = 0;
+#pragma unroll
+        for (int w = 0; w < 8; w++) (void)__builtin_subc(raw.v[w], r_limb(w), br, &br);
+        if (hi != 0 || br == 0) fr_reduce_slow(raw.v);
+#pragma unroll 1
+        for (int b = 0; b < 48; b++) {
+            const int w = (47 - b) >> 2;  // big-endian: byte b holds bits 8 (47 - b)
+            p[b] = w < 8 ? (uint8_t)(raw.v[w] >> (8 * ((47 - b) & 3))) : 0;
+        }
+    }
+}
+
 // scalars for the Straus tasks: canonical 8-limb Fr per (task, base); bases as encodings
 template <class F>
 __global__ __launch_bounds__(64) void k_blind_assemble(size_t n, int q, int k, const uint8_t* __restrict__ cts,
@@ -266,6 +297,15 @@ __global__ __launch_bounds__(64) void k_vss_verify(size_t n, int t, const uint8_
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 extern "C" {
+
+int cck_h_input_canon(int group, size_t n, size_t len, int kn, uint8_t* d_data, hipStream_t st) {
+    if (!n) return 0;
+    if (group == 1)
+        hipLaunchKernelGGL(k_h_input_canon<Fp>, dim3(nblocks(n, 64)), dim3(64), 0, st, n, len, kn, d_data);
+    else
+        hipLaunchKernelGGL(k_h_input_canon<Fp2>, dim3(nblocks(n, 64)), dim3(64), 0, st, n, len, kn, d_data);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 size_t cck_sigreq_proof_bytes(int group, int k) {
     const size_t sb = group == 1 ? 97 : 192;

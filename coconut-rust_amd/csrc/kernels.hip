@@ -554,7 +554,7 @@ int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_o
 int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
                     uint32_t* d_table, hipStream_t st) {
     if (!nbases) return 0;
-    if (wbits < 8 || wbits > 16) return -1;
+    if (wbits < 8 || wbits > 22) return -1;
     size_t t1 = (size_t)nbases * ft_nwin(wbits), t2 = t1 * ((ft_went(wbits) + FILL_RUN - 1) / FILL_RUN);
     if (group == 1) {
         hipLaunchKernelGGL(k_table_pow2<Fp>, dim3(nblocks(t1, 64)), dim3(64), 0, st, nbases, wbits, d_bases, d_inf, d_pw);

@@ -81,7 +81,7 @@ cc_status cc_set_params(cc_ctx* ctx, const uint8_t* g_tilde);
 cc_status cc_set_verkey(cc_ctx* ctx, const uint8_t* X, const uint8_t* Y, size_t q);
 
 /* Window widths of the fixed-base tables built by later cc_set_verkey / cc_set_issuers calls:
- * verkey_bits 0 (chosen by memory), 8 or 16; issuer_bits 0 (chosen by memory) or 8..16.  A forced
+ * verkey_bits 0 (chosen by memory) or 8..22; issuer_bits 0 (chosen by memory) or 8..16.  A forced
  * width that does not fit HBM makes the building call fail.  cc_table_bits reports the widths of the
  * current tables (0: none built). */
 cc_status cc_set_table_bits(cc_ctx* ctx, int verkey_bits, int issuer_bits);

@@ -57,3 +57,24 @@ def test_unblinded_gpu_signature_verifies(ctxs):
     vk = Verkey(_b(case["vk"]["X"]), [_b(v) for v in case["vk"]["Y"]])
     sig = Signature(h[0], s2)
     assert sig.verify([_b(m) for m in r["msgs"]], vk, Params(g=b"", g_tilde=_b(case["g_tilde"])), ctx=ctx)
+
+
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_compute_h_hashes_canonical_encodings(ctxs, mode):
+    """compute_h (signature.rs:197-206) hashes commitment.to_bytes() || known_m.to_bytes(): a known
+    message sent as m + r (a 48-byte value >= r) must give the same h, and so the same blind
+    signature, as the canonical m."""
+    from coconut import blind_sign_batch
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    ctx = ctxs[mode]
+    case = next(c for c in golden(f"issuance_{mode.lower()}.json")["cases"] if c["q"] > c["k"])
+    q, k, rq = case["q"], case["k"], case["requests"]
+    cms = [_b(r["commitment"]) for r in rq]
+    kn = [[_b(m) for m in r["known"]] for r in rq]
+    kn_big = [[(int.from_bytes(m, "big") + R).to_bytes(48, "big") for m in row] for row in kn]
+    cts = [[(_b(a), _b(b)) for a, b in r["ciphertexts"]] for r in rq]
+    x, y = _b(case["x"]), [_b(v) for v in case["y"]]
+    h0, c10, c20 = blind_sign_batch(ctx, q, k, cms, kn, cts, x, y)
+    h1, c11, c21 = blind_sign_batch(ctx, q, k, cms, kn_big, cts, x, y)
+    assert [h.hex() for h in h1] == [h.hex() for h in h0] == [r["h"] for r in rq]
+    assert [c.hex() for c in c21] == [c.hex() for c in c20]
