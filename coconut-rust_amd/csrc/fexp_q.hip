@@ -119,7 +119,7 @@ DEV QR q_pow_x(const QR& src) {
     const auto p1 = mulr(d16, d48);
     const auto p2 = mulr(p1, d57);
     if (is_zero(p2)) return q_pow_x_gs(src);  // quad-uniform (D is the same on both pairs)
-    const auto iv = inv(p2);
+    const auto iv = qinv(p2);
     QR y = qz_expand(c, n57, mulr(iv, p1));    // g^(2^57)
     const auto iv2 = mulr(iv, d57);           // (d16 d48)^-1
     QR acc = rest(q12_mul(qz_expand(s16, n16, mulr(iv2, d48)), qz_expand(s48, n48, mulr(iv2, d16))));
@@ -148,7 +148,7 @@ DEV void qexp_out(size_t i, const QR& res, const uint32_t* flags, uint8_t* verdi
     bool own = (!j && !h ? fp_eq(oa.c, one) : fp_is_zero(oa.c)) && fp_is_zero(ob.c) && fp_is_zero(oc.c);
     const uint32_t fl = flags ? flags[i] : 0u;
     const bool ok = quad_all(own) && (fl & 11u) == 0;  // sigma_1/sigma_2 = O or PoK Schnorr failure
-    if ((__builtin_amdgcn_mbcnt_lo(~0u, 0u) & 3u) == 0) verdicts[i] = ok ? 1 : 0;
+    if ((__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 3u) == 0) verdicts[i] = ok ? 1 : 0;
     if (gt_out) {  // Fp2 k of the AMCL FP12 order at 96 k, half h at + 48 h; component j of a, b, c is k = j, 2 + j, 4 + j
         uint8_t* o = gt_out + i * 576 + 48 * h + 96 * (int)j;
         Fp c;

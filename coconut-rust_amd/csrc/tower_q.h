@@ -48,6 +48,100 @@ DEV bool quad_all(bool own) {
     return o != 0;
 }
 
+// ---------------------------------------------------------------- inversion, one per quad
+// field.h fp_inv_int with the quad's four lanes holding the same input: the divstep iteration's four
+// vectors f, g, d, e sit one per lane (lane & 3 = 0 f, 1 g, 2 d, 3 e; partners f/g and d/e over DPP
+// quad_perm [1,0,3,2]), so a batch's matrix update is ONE signed carry chain a lane (3 mads a limb, the
+// p multiple zero on the f/g lanes) instead of four; the divsteps on the low words (f0, g0 broadcast)
+// run on every lane.
+DEV int32_t qbcast(int32_t x, int src) {
+    switch (src) {
+        case 0: return __builtin_amdgcn_mov_dpp(x, 0x00, 0xF, 0xF, true);
+        case 1: return __builtin_amdgcn_mov_dpp(x, 0x55, 0xF, 0xF, true);
+        case 2: return __builtin_amdgcn_mov_dpp(x, 0xAA, 0xF, 0xF, true);
+        default: return __builtin_amdgcn_mov_dpp(x, 0xFF, 0xF, 0xF, true);
+    }
+}
+DEV void fp_inv_int_quad(Fp& out, const Fp& a) {
+    const uint32_t role = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) & 3u;
+    const bool de = role >= 2, odd = (role & 1u) != 0;
+    S30 X, Y;  // this lane's vector and its partner's
+    {
+        S30 g;
+        s30_from_fp(g, a);
+#pragma unroll
+        for (int i = 0; i < S30N; i++) {
+            const int32_t f = p30_limb(i), d = 0, e = i == 0 ? 1 : 0;
+            const int32_t own = role == 0 ? f : role == 1 ? g.v[i] : role == 2 ? d : e;
+            const int32_t par = role == 0 ? g.v[i] : role == 1 ? f : role == 2 ? e : d;
+            X.v[i] = own;
+            Y.v[i] = par;
+        }
+    }
+    int32_t eta = -1;
+    for (int it = 0; it < 40; it++) {
+        int32_t t[4];
+        eta = divsteps30(eta, (uint32_t)qbcast(X.v[0], 0), (uint32_t)qbcast(X.v[0], 1), t);
+        // f' = t0 f + t1 g, g' = t2 f + t3 g, d' = t0 d + t1 e + p md, e' = t2 d + t3 e + p me (all / 2^30)
+        const int32_t ta = odd ? t[3] : t[0], tb = odd ? t[2] : t[1];
+        int64_t c = smad(tb, Y.v[0], smad(ta, X.v[0], 0));
+        int32_t m = (ta & (X.v[S30N - 1] >> 31)) + (tb & (Y.v[S30N - 1] >> 31));
+        m -= (int32_t)((PINV30 * (uint32_t)c + (uint32_t)m) & (uint32_t)M30);
+        m = de ? m : 0;
+        c = smad(p30_limb(0), m, c);
+        c >>= 30;
+#pragma unroll
+        for (int i = 1; i < S30N; i++) {
+            c = smad(p30_limb(i), m, smad(tb, Y.v[i], smad(ta, X.v[i], c)));
+            X.v[i - 1] = (int32_t)c & M30;
+            c >>= 30;
+        }
+        X.v[S30N - 1] = (int32_t)c;
+        int32_t o = 0;
+#pragma unroll
+        for (int i = 0; i < S30N; i++) {
+            Y.v[i] = __builtin_amdgcn_mov_dpp(X.v[i], 0xB1, 0xF, 0xF, true);
+            o |= X.v[i];
+        }
+        if (qbcast(o, 1) == 0) break;  // g = 0 (quad-uniform)
+    }
+    // f = +-1 (or p when a = 0, where d = 0): x = sign(f) d mod p, d in (-2p, p) (fp_inv_int)
+    const int32_t fsign = qbcast(X.v[S30N - 1], 0);
+    S30 d;
+#pragma unroll
+    for (int i = 0; i < S30N; i++) d.v[i] = qbcast(X.v[i], 2);
+    if (fsign < 0) {
+#pragma unroll
+        for (int i = 0; i < S30N; i++) d.v[i] = -d.v[i];
+        s30_carry(d);
+    }
+    s30_add_kp(d, d.v[S30N - 1] < 0 ? 1 : 0);
+    s30_add_kp(d, d.v[S30N - 1] < 0 ? 1 : 0);
+    S30 tt = d;
+    s30_add_kp(tt, -1);
+    if (tt.v[S30N - 1] >= 0) d = tt;
+    fp_from_s30(out, d);
+}
+// lazy.h inv() for values the four lanes of a quad hold alike
+template <int A, int B>
+DEV auto qinv(const Fq<A, B>& x) {
+    constexpr int32_t C[LN] = {LZ_R3_LIMBS};
+    Fp a = canon(x), ai;
+    fp_inv_int_quad(ai, a);  // (x R')^-1
+    return mul(from_fp(ai), fq_const(C));
+}
+template <int A, int B>
+DEV auto qinv(const F2<A, B>& x) {
+    static_assert(2LL * A * A <= AMAX, "f2 inv: limb bound");
+    int32_t xs[LN];
+#pragma unroll
+    for (int k = 0; k < LN; k++) xs[k] = swp(x.c.v[k]);
+    const W14 n = lz_mont<2>(x.c.v, x.c.v, xs, xs);  // a^2 + b^2 on both lanes
+    const auto ni = qinv(fq<bprod(2LL * B * B)>(n));
+    const auto r = mul(x.c, ni);
+    return conj(F2<AN, decltype(r)::BV>{r});
+}
+
 template <class T>
 struct Two {
     T a, b;
@@ -171,7 +265,7 @@ DEV auto q4_inv(const F2<A, B>& x) {
     const auto sq = sqrr(x);
     const auto psq = qx(sq);
     const auto nrm = norm(qsel(j, sub(psq, xi(sq)), sub(sq, xi(psq))));  // u^2 - xi v^2 on both pairs
-    const auto ni = inv(nrm);
+    const auto ni = qinv(nrm);
     const auto r = mulr(x, ni);
     return qsel(j, neg(r), r);
 }

@@ -74,3 +74,21 @@ def test_reduce_and_squeeze_on_device():
         assert value(r) % P == value(x) % P and abs(value(r)) < 9 * P // 16
         assert all(0 <= t <= M28 for t in r[:-1])
         assert value(s) == value(x) and all(abs(t) < (257 << 20) for t in s)
+
+
+def test_divstep_inversions_on_device():
+    """field.h fp_inv_int (one lane) and tower_q.h fp_inv_int_quad (the four lanes of a quad share one
+    inversion, each lane carrying one of the divstep vectors) against pow(a, p - 2, p), across a whole
+    wave (the upper half-wave's lane ids included) and for a = 0, 1, p - 1."""
+    rnd = random.Random(7)
+    vals = [0, 1, P - 1, 2, P - 2] + [rnd.randrange(1, P) for _ in range(123)]
+    a = [[(v >> (32 * k)) & 0xFFFFFFFF for k in range(12)] + [0, 0] for v in vals]
+    a = [[x - (1 << 32) if x >> 31 else x for x in row] for row in a]
+    quad = [row for row in a for _ in range(4)]  # each quad holds one value
+    words = lambda row: sum((x & 0xFFFFFFFF) << (32 * k) for k, x in enumerate(row[:12]))  # noqa: E731
+    one = _run(4, a)
+    four = _run(5, quad)
+    for k, v in enumerate(vals):
+        want = pow(v, P - 2, P)
+        assert words(one[k]) == want, k
+        assert all(words(four[4 * k + j]) == want for j in range(4)), k
