@@ -124,31 +124,74 @@ DEV W14 lz_mont(const int32_t a[LN], const int32_t b[LN], const int32_t c[LN], c
 }
 
 DEV int32_t swp(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true); }
+// the pair's real / imaginary half on both lanes (DPP quad_perm [0,0,2,2] / [1,1,3,3])
+DEV int32_t bc_re(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xA0, 0xF, 0xF, true); }
+DEV int32_t bc_im(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xF5, 0xF, 0xF, true); }
 using pl::half_id;
 
-// own half of x * y for pair-lane Fp2 values x, y: re  x y + xs (-ys),  im  x ys + xs y
+// Operand preparation under an exec mask: the two halves of a pair need different operations, and a
+// per-limb select (v_cndmask) after computing both costs an instruction a limb more than running each
+// half's operation on its own lanes.  The mask is restored inside the same asm statement, so the
+// compiler never sees a partial exec; lanes that were inactive stay inactive.
+constexpr uint64_t kEvenLanes = 0x5555555555555555ull;  // real halves
+// d <- -d on the real-half lanes, all 14 limbs
+DEV void neg_re14(int32_t d[LN]) {
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_and_b64 exec, exec, %15\n\t"
+        "v_sub_u32 %1, 0, %1\n\tv_sub_u32 %2, 0, %2\n\tv_sub_u32 %3, 0, %3\n\tv_sub_u32 %4, 0, %4\n\t"
+        "v_sub_u32 %5, 0, %5\n\tv_sub_u32 %6, 0, %6\n\tv_sub_u32 %7, 0, %7\n\tv_sub_u32 %8, 0, %8\n\t"
+        "v_sub_u32 %9, 0, %9\n\tv_sub_u32 %10, 0, %10\n\tv_sub_u32 %11, 0, %11\n\tv_sub_u32 %12, 0, %12\n\t"
+        "v_sub_u32 %13, 0, %13\n\tv_sub_u32 %14, 0, %14\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(save), "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3]), "+v"(d[4]), "+v"(d[5]), "+v"(d[6]),
+          "+v"(d[7]), "+v"(d[8]), "+v"(d[9]), "+v"(d[10]), "+v"(d[11]), "+v"(d[12]), "+v"(d[13])
+        : "s"(kEvenLanes));
+}
+// squaring operands for 7 limbs: u holds xs on entry; re lanes u <- x + xs, w <- x - xs; im lanes w <- 2x
+DEV void sqr_ops7(int32_t* u, int32_t* w, const int32_t* x) {
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_and_b64 exec, exec, %22\n\t"
+        "v_sub_u32 %8, %15, %1\n\tv_add_u32 %1, %1, %15\n\t"
+        "v_sub_u32 %9, %16, %2\n\tv_add_u32 %2, %2, %16\n\t"
+        "v_sub_u32 %10, %17, %3\n\tv_add_u32 %3, %3, %17\n\t"
+        "v_sub_u32 %11, %18, %4\n\tv_add_u32 %4, %4, %18\n\t"
+        "v_sub_u32 %12, %19, %5\n\tv_add_u32 %5, %5, %19\n\t"
+        "v_sub_u32 %13, %20, %6\n\tv_add_u32 %6, %6, %20\n\t"
+        "v_sub_u32 %14, %21, %7\n\tv_add_u32 %7, %7, %21\n\t"
+        "s_andn2_b64 exec, %0, %22\n\t"
+        "v_add_u32 %8, %15, %15\n\tv_add_u32 %9, %16, %16\n\tv_add_u32 %10, %17, %17\n\tv_add_u32 %11, %18, %18\n\t"
+        "v_add_u32 %12, %19, %19\n\tv_add_u32 %13, %20, %20\n\tv_add_u32 %14, %21, %21\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(save), "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(u[4]), "+v"(u[5]), "+v"(u[6]),
+          "=&v"(w[0]), "=&v"(w[1]), "=&v"(w[2]), "=&v"(w[3]), "=&v"(w[4]), "=&v"(w[5]), "=&v"(w[6])
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "s"(kEvenLanes));
+}
+
+// own half of x * y for pair-lane Fp2 values x = (a, b), y = (c, d):
+//   re  x c + xs (-d) = a c - b d,  im  x c + xs d = b c + a d
+// (c and d broadcast to both lanes of the pair, d negated on the real-half lane)
 DEV W14 lz_f2_mul_v(const W14& x, const W14& y) {
-    const bool im = half_id() != 0;
     int32_t xs[LN], b[LN], d[LN];
 #pragma unroll
     for (int k = 0; k < LN; k++) {
         xs[k] = swp(x.v[k]);
-        const int32_t ys = swp(y.v[k]);
-        b[k] = im ? ys : y.v[k];
-        d[k] = im ? y.v[k] : -ys;
+        b[k] = bc_re(y.v[k]);
+        d[k] = bc_im(y.v[k]);
     }
+    neg_re14(d);
     return lz_mont<2>(x.v, b, xs, d);
 }
 // own half of x^2: re (x + xs)(x - xs),  im xs (2 x)
 DEV W14 lz_f2_sqr_v(const W14& x) {
-    const bool im = half_id() != 0;
     int32_t u[LN], w[LN];
 #pragma unroll
-    for (int k = 0; k < LN; k++) {
-        const int32_t xs = swp(x.v[k]);
-        u[k] = im ? xs : x.v[k] + xs;
-        w[k] = im ? x.v[k] + x.v[k] : x.v[k] - xs;
-    }
+    for (int k = 0; k < LN; k++) u[k] = swp(x.v[k]);
+    sqr_ops7(u, w, x.v);
+    sqr_ops7(u + 7, w + 7, x.v + 7);
     return lz_mont<1>(u, w, u, w);
 }
 DEV W14 lz_mul_v(const W14& x, const W14& y) { return lz_mont<1>(x.v, y.v, x.v, y.v); }
@@ -460,16 +503,29 @@ DEV F2<AS, B> squeeze(const F2<A, B>& x) { return {squeeze(x.c)}; }
 template <int A, int B>
 DEV F2<AN, 9> reduce(const F2<A, B>& x) { return {reduce(x.c)}; }
 
-// x (1 + i) = (a - b) + (a + b) i: own + (im ? partner : -partner)
+// 7 limbs of s <- x - s on the real-half lanes, x + s on the imaginary-half lanes
+DEV void xi_ops7(int32_t* s, const int32_t* x) {
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_and_b64 exec, exec, %15\n\t"
+        "v_sub_u32 %1, %8, %1\n\tv_sub_u32 %2, %9, %2\n\tv_sub_u32 %3, %10, %3\n\tv_sub_u32 %4, %11, %4\n\t"
+        "v_sub_u32 %5, %12, %5\n\tv_sub_u32 %6, %13, %6\n\tv_sub_u32 %7, %14, %7\n\t"
+        "s_andn2_b64 exec, %0, %15\n\t"
+        "v_add_u32 %1, %8, %1\n\tv_add_u32 %2, %9, %2\n\tv_add_u32 %3, %10, %3\n\tv_add_u32 %4, %11, %4\n\t"
+        "v_add_u32 %5, %12, %5\n\tv_add_u32 %6, %13, %6\n\tv_add_u32 %7, %14, %7\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(save), "+v"(s[0]), "+v"(s[1]), "+v"(s[2]), "+v"(s[3]), "+v"(s[4]), "+v"(s[5]), "+v"(s[6])
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "s"(kEvenLanes));
+}
+// x (1 + i) = (a - b) + (a + b) i: own -+ partner (the partner's half, then one masked op a limb)
 template <int A, int B>
 DEV F2<2 * A, 2 * B> xi(const F2<A, B>& x) {
-    const bool im = half_id() != 0;
     F2<2 * A, 2 * B> r;
 #pragma unroll
-    for (int k = 0; k < LN; k++) {
-        const int32_t s = swp(x.c.v[k]);
-        r.c.v[k] = x.c.v[k] + (im ? s : -s);
-    }
+    for (int k = 0; k < LN; k++) r.c.v[k] = swp(x.c.v[k]);
+    xi_ops7(r.c.v, x.c.v);
+    xi_ops7(r.c.v + 7, x.c.v + 7);
     return r;
 }
 // conj: the imaginary half negated

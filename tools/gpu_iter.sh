@@ -25,4 +25,16 @@ if [ -f coconut-rust_amd/libcoconut_hip_prof.so ]; then
   echo "[iter] fexp phases"
   timeout -k 10 300 python -u tools/fexp_phases.py > "$OUT/fexp_phases.json" 2> "$OUT/fexp_phases.err" || exit 1
 fi
-echo "[iter] done"
+
+# optional: one PMC pass per group in PMC_GROUPS (';'-separated counter lists) over one bench step of the
+# current build, kernel trace only
+if [ -n "${PMC_GROUPS:-}" ]; then
+  IFS=';' read -ra GRPS <<< "$PMC_GROUPS"
+  i=0
+  for grp in "${GRPS[@]}"; do
+    i=$((i+1))
+    echo "[iter] pmc $i: $grp"
+    (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace --pmc $grp -d "$OLDPWD/$OUT/pmc$i" -o pmc --output-format csv -- python3 "$OLDPWD/bench.py" --mode $MODE --steps 1 --warmup 0 --no-cpu-baseline --no-pcie > "$OLDPWD/$OUT/pmc$i.log" 2>&1) || exit 1
+  done
+fi
+echo "[iter] pmc done"
