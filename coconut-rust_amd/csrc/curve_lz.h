@@ -92,5 +92,81 @@ DEV JL jl_add(const JL& p, const JL& q) {
 
 DEV AL jl_neg_aff(const AL& a) { return {a.x, neg(a.y)}; }
 
+// ================================================================ G1, one point per lane
+// The same formulas over the lazy Fp on ONE lane (the G1 fixed-base MSMs of the verify / RLC / PoK
+// preps and of Verkey::aggregate): additions carry-free, squarings on the upper triangle (lazy.h
+// lz_sqr1, 105 product mads against 196), coordinates at rest reduced.
+using FR = Fq<AN, 9>;
+struct JG {
+    FR x, y, z;
+};
+struct AG {
+    Fq<AN, BC> x, y;  // canonical (a table entry)
+};
+
+template <int A1, int B1, int A2, int B2>
+DEV auto mulr1(const Fq<A1, B1>& x, const Fq<A2, B2>& y) {
+    if constexpr ((long long)A1 * A2 <= AMAX) return mul(x, y);
+    else if constexpr (A1 >= A2 && (long long)AS * A2 <= AMAX) return mul(squeeze(x), y);
+    else if constexpr (A2 > A1 && (long long)A1 * AS <= AMAX) return mul(x, squeeze(y));
+    else return mul(squeeze(x), squeeze(y));
+}
+template <int A, int B>
+DEV auto sqrr1(const Fq<A, B>& x) {
+    if constexpr ((long long)A * A <= AMAX1S) return sqr(x);
+    else return sqr(squeeze(x));
+}
+DEV bool r1_is_zero(const FR& x) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int k = 0; k < LN; k++) o |= (uint32_t)x.v[k];
+    return o == 0;
+}
+DEV FR r1_one() {
+    constexpr int32_t O[LN] = {LZ_ONE_LIMBS};
+    return reduce(fq_const(O));
+}
+DEV JG jg_inf() { return {r1_one(), r1_one(), fit<AN, 9>(Fq<AN, 0>{})}; }
+DEV bool jg_is_inf(const JG& p) { return r1_is_zero(p.z); }
+
+// dbl-2009-l (a = 0)
+DEV JG jg_dbl(const JG& p) {
+    const auto A = sqrr1(p.x);
+    const auto B = sqrr1(p.y);
+    const auto C = sqrr1(B);
+    const auto t = sub(sub(sqrr1(add(p.x, B)), A), C);
+    const auto D = squeeze(add(t, t));  // 2 ((X + B)^2 - A - C)
+    const auto E = smul<3>(A);
+    const auto X3 = sub(sqrr1(E), add(D, D));
+    // E (D - X3) - 8 C  (8 C as 2 (4 C) squeezed: 8 normalised limbs would leave int32)
+    const auto Y3 = sub(mulr1(E, sub(D, X3)), smul<2>(squeeze(smul<4>(C))));
+    const auto Z3 = smul<2>(mulr1(p.y, p.z));
+    return {reduce(X3), reduce(Y3), reduce(Z3)};
+}
+
+// madd-2007-bl: p (Jacobian) + q (affine, not the identity)
+DEV JG jg_add_aff(const JG& p, const AG& q) {
+    if (jg_is_inf(p)) return {reduce(q.x), reduce(q.y), r1_one()};
+    const auto z1z1 = sqrr1(p.z);
+    const auto u2 = mulr1(q.x, z1z1);
+    const auto s2 = mulr1(mulr1(q.y, p.z), z1z1);
+    const FR h = reduce(sub(u2, p.x));
+    const FR r0 = reduce(sub(s2, p.y));
+    if (r1_is_zero(h)) return r1_is_zero(r0) ? jg_dbl(p) : jg_inf();
+    const auto rr = add(r0, r0);
+    const auto hh = sqrr1(h);
+    const auto i = smul<4>(hh);
+    const auto j = mulr1(h, i);
+    const auto v = mulr1(p.x, i);
+    const auto X3 = sub(sub(sqrr1(rr), j), add(v, v));
+    const auto Y3 = sub(mulr1(rr, sub(v, X3)), smul<2>(mulr1(p.y, j)));
+    const auto Z3 = sub(sub(sqrr1(add(p.z, h)), z1z1), hh);
+    return {reduce(X3), reduce(Y3), reduce(Z3)};
+}
+
+// storage form (curve.h Jac<Fp>, canonical, R = 2^406) <-> lazy R' form
+DEV JG jg_from(const Jac<Fp>& a) { return {reduce(in_r(a.x)), reduce(in_r(a.y)), reduce(in_r(a.z))}; }
+DEV Jac<Fp> jg_to(const JG& a) { return {out_r(a.x), out_r(a.y), out_r(a.z)}; }
+
 }  // namespace lz
 }  // namespace cc

@@ -12,7 +12,9 @@
 // An entry equal to the identity (only possible for a small-order base) is stored as (0, 0), which
 // lies on neither curve, and skipped.
 #pragma once
+#include <type_traits>
 #include "curve.h"
+#include "curve_lz.h"
 
 namespace cc {
 
@@ -52,21 +54,46 @@ DEV bool ft_is_empty(const Aff<F>& a) {
     return o == 0;
 }
 
-// acc += (k restricted to windows [w0, w1)) * B_j
-template <class F>
-DEV void ft_add(Jac<F>& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j, int w0,
-                int w1) {
-    constexpr int EW = sizeof(Aff<F>) / 4;
+// G1 tables hold their entries in the lazy field's Montgomery form (x R' mod p, R' = 2^392, canonical
+// 12 x 32 words; k_table_fill rescales them), so the lazy G1 mixed addition (curve_lz.h) loads an
+// entry with shifts only.  acc += (k over windows [w0, w1)) * B_j on a lazy accumulator:
+DEV void ft_add_lz(lz::JG& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j, int w0,
+                   int w1) {
+    constexpr int EW = sizeof(Aff<Fp>) / 4;
     const size_t went = ft_went(wbits);
-    const uint32_t* tj = table + (size_t)j * ft_base_words<F>(wbits);
+    const uint32_t* tj = table + (size_t)j * ft_base_words<Fp>(wbits);
 #pragma unroll 1
     for (int w = w0; w < w1; w++) {
         const uint32_t d = ft_digit(k, w, wbits);
         if (!d) continue;
-        Aff<F> e;
-        ft_load<F>(e, tj + ((size_t)w * went + d - 1) * EW);
+        Aff<Fp> e;
+        ft_load<Fp>(e, tj + ((size_t)w * went + d - 1) * EW);
         if (ft_is_empty(e)) continue;
-        jac_add_aff(acc, acc, e);
+        acc = lz::jg_add_aff(acc, lz::AG{lz::from_fp(e.x), lz::from_fp(e.y)});
+    }
+}
+
+// acc += (k restricted to windows [w0, w1)) * B_j
+template <class F>
+DEV void ft_add(Jac<F>& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j, int w0,
+                int w1) {
+    if constexpr (std::is_same<F, Fp>::value) {  // G1: on the lazy field, storage form at the boundary
+        lz::JG a = lz::jg_from(acc);
+        ft_add_lz(a, k, table, wbits, j, w0, w1);
+        acc = lz::jg_to(a);
+    } else {
+        constexpr int EW = sizeof(Aff<F>) / 4;
+        const size_t went = ft_went(wbits);
+        const uint32_t* tj = table + (size_t)j * ft_base_words<F>(wbits);
+#pragma unroll 1
+        for (int w = w0; w < w1; w++) {
+            const uint32_t d = ft_digit(k, w, wbits);
+            if (!d) continue;
+            Aff<F> e;
+            ft_load<F>(e, tj + ((size_t)w * went + d - 1) * EW);
+            if (ft_is_empty(e)) continue;
+            jac_add_aff(acc, acc, e);
+        }
     }
 }
 

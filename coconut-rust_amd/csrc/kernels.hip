@@ -132,9 +132,20 @@ __global__ __launch_bounds__(64) void k_table_pow2(int nbases, int wbits, const 
     st_jac_aos<F>(pw + (size_t)t * (sizeof(Jac<F>) / 4), P);
 }
 
+// x R (storage form) -> x R' (the lazy field's Montgomery form, fixed.h): times 2^392 / R = 2^-14
+DEV void g1_to_lazy_form(Fp& v) {
+    constexpr uint32_t C[NL] = {0x0347fcb8u, 0x19d80000u, 0x6d2002b1u, 0x12e00cdeu, 0xa2090c72u, 0x37669f83u,
+                                0xda0f73e0u, 0x09b09b42u, 0x8f1297bbu, 0xa7c515d9u, 0xfcfa012cu, 0x0577a659u};  // 2^392 mod p
+    Fp c;
+#pragma unroll
+    for (int j = 0; j < NL; j++) c.v[j] = C[j];
+    fp_mul(v, v, c);
+}
+
 // T2: entries d * 2^(wbits w) * B_j for a run of FILL_RUN consecutive digits per thread: the first by
 // double-and-add, the rest by one mixed addition each, then ONE inversion for the whole run
-// (Montgomery's trick) to write them affine.  Identity entries are written as (0, 0).
+// (Montgomery's trick) to write them affine (G1 entries in the lazy field's form, fixed.h).  Identity
+// entries are written as (0, 0).
 constexpr int FILL_RUN = 32;
 template <class F>
 __global__ __launch_bounds__(64) void k_table_fill(int nbases, int wbits, const uint32_t* __restrict__ pw,
@@ -196,10 +207,12 @@ __global__ __launch_bounds__(64) void k_table_fill(int nbases, int wbits, const 
         uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
         for (int c = 0; c < PW; c++) vw[c] = o[c];
         T::mul(v, v, zi2);
+        if constexpr (std::is_same<F, Fp>::value) g1_to_lazy_form(v);
         for (int c = 0; c < PW; c++) o[c] = vw[c];
         T::mul(zi2, zi2, zi);
         for (int c = 0; c < PW; c++) vw[c] = o[PW + c];
         T::mul(v, v, zi2);
+        if constexpr (std::is_same<F, Fp>::value) g1_to_lazy_form(v);
         for (int c = 0; c < PW; c++) o[PW + c] = vw[c];
     }
 }

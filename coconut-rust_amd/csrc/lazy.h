@@ -123,6 +123,33 @@ DEV W14 lz_mont(const int32_t a[LN], const int32_t b[LN], const int32_t c[LN], c
     return r;
 }
 
+// a^2 / R' mod p for a one-lane value: product scanning over the upper triangle only (column k:
+// sum over i < j of (2 a_i) a_j, plus a_{k/2}^2), 105 product mads instead of 196.  Column bound: at
+// most 7 doubled cross terms and one square, 15 A^2 2^40 in all, so A^2 <= 498,000 (AMAX1S).
+constexpr long long AMAX1S = 498000;
+DEV W14 lz_sqr1(const int32_t a[LN]) {
+    int32_t d[LN], m[LN];
+#pragma unroll
+    for (int i = 0; i < LN; i++) d[i] = a[i] + a[i];
+    W14 r;
+    int64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * LN - 1; k++) {
+        int64_t acc2 = 0;
+#pragma unroll
+        for (int i = 0; i < LN; i++) {
+            const int j = k - i;
+            if (j <= i || j >= LN) continue;
+            acc2 += (int64_t)d[i] * a[j];
+        }
+        if ((k & 1) == 0 && k / 2 < LN) acc2 += (int64_t)a[k / 2] * a[k / 2];
+        acc += acc2;
+        lz_redc_col(k, acc, m, r.v);
+    }
+    r.v[LN - 1] = (int32_t)acc;
+    return r;
+}
+
 DEV int32_t swp(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, true); }
 // the pair's real / imaginary half on both lanes (DPP quad_perm [0,0,2,2] / [1,1,3,3])
 DEV int32_t bc_re(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0xA0, 0xF, 0xF, true); }
@@ -249,6 +276,12 @@ DEV W14 lz_f2_mul_c(const W14& x, const W14& y) { return lz_f2_mul_call(LZ_E14(x
 DEV W14 lz_f2_sqr_c(const W14& x) { return lz_f2_sqr_call(LZ_E14(x)); }
 DEV W14 lz_mul_c(const W14& x, const W14& y) { return lz_mul_call(LZ_E14(x), LZ_E14(y)); }
 #endif
+// one-lane squaring (not in the pair-lane kernels' inlined build: only the G1 code uses it)
+static __device__ __noinline__ W14 lz_sqr1_call(LZ_L14(a)) {
+    const int32_t A[LN] = {LZ_V14(a)};
+    return lz_sqr1(A);
+}
+DEV W14 lz_sqr1_c(const W14& x) { return lz_sqr1_call(LZ_E14(x)); }
 
 template <int A, int B>
 DEV W14 w14(const Fq<A, B>& x) {
@@ -577,6 +610,12 @@ template <int A1, int B1, int A2, int B2>
 DEV Fq<AN, bprod((long long)B1 * B2)> mul(const Fq<A1, B1>& x, const Fq<A2, B2>& y) {
     static_assert((long long)A1 * A2 <= AMAX, "fp mul: limb bound");
     return fq<bprod((long long)B1 * B2)>(lz_mul_c(w14(x), w14(y)));
+}
+// one-lane x^2 (upper-triangle product scanning)
+template <int A, int B>
+DEV Fq<AN, bprod((long long)B * B)> sqr(const Fq<A, B>& x) {
+    static_assert((long long)A * A <= AMAX1S, "fp sqr: limb bound");
+    return fq<bprod((long long)B * B)>(lz_sqr1_c(w14(x)));
 }
 
 // pair-uniform predicates (both halves agree)
