@@ -140,7 +140,7 @@ DEV auto f12_mul_line(const F12<A, B>& f, const L0& l0, const L2& l2, const L3& 
     const auto la = mk4(l0, l3);
     const auto t0 = mul(f.a, la);                                  // a A
     const auto t2 = mul_f2(f.c, l2);                               // c C
-    const auto s = mul(norm(add(f.a, f.c)), mk4(norm(add(l0, l2)), l3));  // (a + c)(A + C)
+    const auto s = mul(add(f.a, f.c), mk4(add(l0, l2), l3));              // (a + c)(A + C), squeezed by mulr
     const auto rc = sub(sub(s, t0), t2);                           // c A + a C
     const auto ra = add(t0, mul_s(mul_f2(f.b, l2)));               // a A + s (b C)
     const auto rb = add(mul(f.b, la), mul_s(t2));                  // b A + s (c C)
@@ -271,9 +271,9 @@ DEV auto line_dbl(G2P<BX, BY, BZ>& T) {
     const auto a = mulr(T.x, T.y);
     const auto b = sqrr(T.y);
     const auto c = sqrr(T.z);
-    const auto e3 = norm(smul<3>(norm(xi(c))));       // 3 xi C
+    const auto e3 = norm(smul<3>(xi(c)));             // 3 xi C
     const auto e = smul<4>(e3);                        // E = 12 xi C
-    const auto f = norm(smul<4>(norm(smul<3>(e3))));  // F = 3 E
+    const auto f = dbl(norm(smul<6>(e3)));            // F = 3 E = 2 (6 e3)
     const auto ln = mk_line(norm(sub(e, b)), norm(smul<3>(sqrr(T.x))), norm(neg(sub(sub(sqrr(add(T.y, T.z)), b), c))));
     const auto h = neg(ln.l3);                         // H (squeezed)
     const auto t = sqrr(norm(e));

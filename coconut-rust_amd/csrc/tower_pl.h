@@ -87,18 +87,34 @@ DEV uint32_t four_p29(int k) {
 // operands are converted to radix 2^29 once and the partner's converted limbs fetched by DPP.
 //   re: a c + b (4p - d) = x y + xs (4p - ys);   im: b c + a d = x ys + xs y
 // a c + b (4p - d) < 12 p^2 < p R, so the Montgomery result is < 2p and one subtraction makes it canonical.
+// 7 limbs of d <- 4p - d on the real-half lanes (limbs k0..k0+6 of four_p29), under an exec mask as
+// lazy.h neg_re14: the imaginary-half lanes keep d
+#define CC_4P_OPS7(k0)                                                                                        \
+    asm volatile("s_mov_b64 %0, exec\n\t"                                                                     \
+                 "s_and_b64 exec, exec, %8\n\t"                                                               \
+                 "v_sub_u32 %1, %9, %1\n\tv_sub_u32 %2, %10, %2\n\tv_sub_u32 %3, %11, %3\n\t"                \
+                 "v_sub_u32 %4, %12, %4\n\tv_sub_u32 %5, %13, %5\n\tv_sub_u32 %6, %14, %6\n\t"               \
+                 "v_sub_u32 %7, %15, %7\n\t"                                                                  \
+                 "s_mov_b64 exec, %0"                                                                         \
+                 : "=&s"(save), "+v"(d[k0]), "+v"(d[k0 + 1]), "+v"(d[k0 + 2]), "+v"(d[k0 + 3]),               \
+                   "+v"(d[k0 + 4]), "+v"(d[k0 + 5]), "+v"(d[k0 + 6])                                          \
+                 : "s"(0x5555555555555555ull), "s"(four_p29(k0)), "s"(four_p29(k0 + 1)),                      \
+                   "s"(four_p29(k0 + 2)), "s"(four_p29(k0 + 3)), "s"(four_p29(k0 + 4)), "s"(four_p29(k0 + 5)), \
+                   "s"(four_p29(k0 + 6)))
 DEV Fp f2_mul_half(const Fp& x, const Fp& y) {
-    const bool im = half_id() != 0;
     uint32_t a[L29], y29[L29], b[L29], c[L29], d[L29];
     to29(a, x);
     to29(y29, y);
 #pragma unroll
     for (int k = 0; k < L29; k++) {
         c[k] = swp(a[k]);
-        const uint32_t ys = swp(y29[k]);
-        b[k] = im ? ys : y29[k];
-        d[k] = im ? y29[k] : four_p29(k) - ys;
+        // the pair's real half of y on both lanes (b), its imaginary half (d), 4p - d on the real lane
+        b[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)y29[k], 0xA0, 0xF, 0xF, true);
+        d[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)y29[k], 0xF5, 0xF, 0xF, true);
     }
+    uint64_t save;
+    CC_4P_OPS7(0);
+    CC_4P_OPS7(7);
     return mul2_29(a, b, c, d);
 }
 // 2p, 32-bit limbs
