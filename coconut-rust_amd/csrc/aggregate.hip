@@ -502,6 +502,7 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_split(size_t n, int q, int 
         const uint8_t* rp = resp + i * (size_t)(q - r + 1) * 48;
         const int nwin = ft_nwin(wbits);
         Fr k;
+        lz::JG la = lz::jg_inf();  // the table terms on the lazy field (fixed.h ft_add_lz)
         if (!roleB) {
             {
                 Aff<FS_> a;
@@ -513,7 +514,7 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_split(size_t n, int q, int 
                 for (int c = 0; c < 4; c++) st_fp(S, S_Q2 + c, i, pa[c]);
             }
             fr_from_be48(k, rp);
-            if (!binf[q]) ft_add<FO>(acc, k.v, table, wbits, q, 0, nwin);  // table base q = g~
+            if (!binf[q]) ft_add_lz(la, k.v, table, wbits, q, 0, nwin);  // table base q = g~
         }
         // hidden responses: role A the first `split`, role B the rest
         int slot = 1, hid = 0;
@@ -525,36 +526,38 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_split(size_t n, int q, int 
             hid++;
             if (mine) {
                 fr_from_be48(k, rp + (size_t)slot * 48);
-                if (!binf[h]) ft_add<FO>(acc, k.v, table, wbits, h, 0, nwin);
+                if (!binf[h]) ft_add_lz(la, k.v, table, wbits, h, 0, nwin);
             }
             slot++;
         }
+        acc = lz::jg_to(la);
         if (!roleB) {
             // J * chal in fixed 4-bit windows (k_prep_pok)
             fr_from_be48(k, chal + i * 48);
             if (Jok) {
-                auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * JW + w) * n + i]; };
-                Jac<FO> t;
-                jac_from_aff(t, Ja);
+                // on the lazy field (curve_lz.h); the table of d J, d = 1..15, in the scratch as lazy points
+                constexpr int LW = sizeof(lz::JG) / 4;
+                auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * LW + w) * n + i]; };
+                const lz::AG Jl{lz::fit<lz::AN, lz::BC>(lz::reduce(lz::in_r(Ja.x))), lz::fit<lz::AN, lz::BC>(lz::reduce(lz::in_r(Ja.y)))};
+                lz::JG t = lz::jg_add_aff(lz::jg_inf(), Jl);
 #pragma unroll 1
                 for (int d = 1; d <= 15; d++) {
-                    if (d > 1) jac_add_aff(t, t, Ja);
+                    if (d > 1) t = lz::jg_add_aff(t, Jl);
                     const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
-                    for (int w = 0; w < JW; w++) tab(d, w) = tw[w];
+                    for (int w = 0; w < LW; w++) tab(d, w) = tw[w];
                 }
-                Jac<FO> sacc;
-                jac_set_inf(sacc);
+                lz::JG sacc = lz::jg_inf();
 #pragma unroll 1
                 for (int win = 63; win >= 0; win--) {
-                    for (int b = 0; b < 4; b++) jac_dbl(sacc, sacc);
+                    for (int b = 0; b < 4; b++) sacc = lz::jg_dbl(sacc);
                     const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
                     if (d) {
                         uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
-                        for (int w = 0; w < JW; w++) tw[w] = tab((int)d, w);
-                        jac_add(sacc, sacc, t);
+                        for (int w = 0; w < LW; w++) tw[w] = tab((int)d, w);
+                        sacc = lz::jg_add(sacc, t);
                     }
                 }
-                jac_add(acc, acc, sacc);
+                jac_add(acc, acc, lz::jg_to(sacc));
             }
         } else {
             Aff<FO> Ta;
@@ -572,12 +575,14 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_split(size_t n, int q, int 
                 jac_from_aff(jp, x);
             }
             if (Jok) jac_add_aff(jp, jp, Ja);
+            lz::JG lj = lz::jg_from(jp);
             for (int z = 0; z < r; z++) {
                 Fr m;
                 fr_from_be48(m, rev_msgs + ((size_t)i * r + z) * 48);
                 const int h = (int)rev_idx[z];
-                if (!binf[h]) ft_add<FO>(jp, m.v, table, wbits, h, 0, nwin);
+                if (!binf[h]) ft_add_lz(lj, m.v, table, wbits, h, 0, nwin);
             }
+            jp = lz::jg_to(lj);
             if (jac_is_inf(jp)) fl |= 4u;
             Fp t;
             fp_mul(t, jp.x, jp.z);
@@ -629,24 +634,34 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
     if (task >= n * (size_t)(q + 1)) return;  // uniform over the lane group
     const size_t cred = task / (q + 1);
     const int j = (int)(task % (q + 1));
-    Jac<F> acc;
-    jac_set_inf(acc);
     int bad = 0;
+    // this lane's share of the t terms into accum (a lazy G1 accumulator, or a storage-form one)
+    auto lane_terms = [&](auto& accum, auto&& add_term) {
 #pragma unroll 1
-    for (size_t k = lane; k < t; k += L) {
-        const uint64_t id = ids[cred * len + k];
-        int lo = 0, hi = n_iss;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (iss_ids[mid] < id) lo = mid + 1; else hi = mid;
+        for (size_t k = lane; k < t; k += L) {
+            const uint64_t id = ids[cred * len + k];
+            int lo = 0, hi = n_iss;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (iss_ids[mid] < id) lo = mid + 1; else hi = mid;
+            }
+            if (lo >= n_iss || iss_ids[lo] != id) {  // no issuer verkey for this id
+                bad = 1;
+                continue;
+            }
+            const int b = lo * (q + 1) + j;
+            if (binf[b]) continue;
+            add_term(accum, l + (cred * t + k) * 8, b);
         }
-        if (lo >= n_iss || iss_ids[lo] != id) {  // no issuer verkey for this id
-            bad = 1;
-            continue;
-        }
-        const int b = lo * (q + 1) + j;
-        if (binf[b]) continue;
-        ft_add<F>(acc, l + (cred * t + k) * 8, table, wbits, b, 0, ft_nwin(wbits));
+    };
+    Jac<F> acc;
+    if constexpr (std::is_same<F, Fp>::value) {  // G1: the whole lane sum on the lazy field
+        lz::JG a = lz::jg_inf();
+        lane_terms(a, [&](lz::JG& x, const uint32_t* kk, int b) { ft_add_lz(x, kk, table, wbits, b, 0, ft_nwin(wbits)); });
+        acc = lz::jg_to(a);
+    } else {
+        jac_set_inf(acc);
+        lane_terms(acc, [&](Jac<F>& x, const uint32_t* kk, int b) { ft_add<F>(x, kk, table, wbits, b, 0, ft_nwin(wbits)); });
     }
     lane_group_sum<F, L>(acc);
 #pragma unroll

@@ -355,11 +355,11 @@ static cc_status subgroup_host(cc_ctx* c, int group, size_t n, const uint8_t* by
     return CC_OK;
 }
 
-// Shared-verkey tables: 16-bit windows (half the additions of 8-bit ones; 100 / 200 MB per G1 / G2
-// base) when the q + 2 bases' tables fit half the free HBM (at most 64 GiB), else 8-bit windows
-// (32 x 255 entries, 0.8 / 1.6 MB a base); a failed 16-bit allocation falls back to 8 bits.
-// cc_set_table_bits forces a width in [8, 22] (ceil(256 / w) windows of 2^w - 1 entries: 20 bits = 13
-// windows, 1.3 / 2.6 GB a G1 / G2 base).  On failure the caller leaves the context without a verkey.
+// Shared-verkey tables: the widest of 22 / 20 / 16-bit windows whose q + 2 bases' tables fit 40 % of the
+// free HBM (at most 96 GiB of the 288): 22 bits = 12 windows of 4,194,303 entries, 4.8 / 9.7 GB a G1 / G2
+// base, 12 mixed additions per scalar against 16 at 16 bits (100 / 200 MB a base); else 8-bit windows
+// (32 x 255 entries, 0.8 / 1.6 MB a base); a failed wide allocation falls back to 8 bits.
+// cc_set_table_bits forces a width in [8, 22].  On failure the caller leaves the context without a verkey.
 static cc_status rebuild_tables(cc_ctx* c) {
     // bases for the fixed-base tables: Y~[0..q), g~ (PoK Schnorr base), X~ (RLC) -> q + 2 bases
     int og = oth_group(c->mode);
@@ -371,9 +371,14 @@ static cc_status rebuild_tables(cc_ctx* c) {
     c->table.release();
     const double fr = (double)free_hbm();
     if (!wb) {
-        const double want = (double)nb * (double)tab_words(og, 16) * 4.0;
-        const double cap = std::min(0.5 * fr, 64.0 * (double)(1ull << 30));
-        wb = want <= cap ? 16 : 8;
+        // the widest of 22 / 20 / 16 bits whose tables fit 40 % of the free HBM, at most 96 GiB
+        const double cap = std::min(0.4 * fr, 96.0 * (double)(1ull << 30));
+        wb = 8;
+        for (int w : {22, 20, 16})
+            if ((double)nb * (double)tab_words(og, w) * 4.0 <= cap) {
+                wb = w;
+                break;
+            }
     }
     // a forced width is refused up front when it exceeds the free HBM: hipMalloc does not reliably fail
     // for sizes above it (the runtime may over-commit), and a build kernel writing such a table would not

@@ -164,6 +164,29 @@ DEV JG jg_add_aff(const JG& p, const AG& q) {
     return {reduce(X3), reduce(Y3), reduce(Z3)};
 }
 
+// add-2007-bl: general Jacobian addition with the exceptional cases
+DEV JG jg_add(const JG& p, const JG& q) {
+    if (jg_is_inf(p)) return q;
+    if (jg_is_inf(q)) return p;
+    const auto z1z1 = sqrr1(p.z);
+    const auto z2z2 = sqrr1(q.z);
+    const auto u1 = mulr1(p.x, z2z2);
+    const auto u2 = mulr1(q.x, z1z1);
+    const auto s1 = mulr1(mulr1(p.y, q.z), z2z2);
+    const auto s2 = mulr1(mulr1(q.y, p.z), z1z1);
+    const FR h = reduce(sub(u2, u1));
+    const FR r0 = reduce(sub(s2, s1));
+    if (r1_is_zero(h)) return r1_is_zero(r0) ? jg_dbl(p) : jg_inf();
+    const auto rr = add(r0, r0);
+    const auto i = sqrr1(add(h, h));
+    const auto j = mulr1(h, i);
+    const auto v = mulr1(u1, i);
+    const auto X3 = sub(sub(sqrr1(rr), j), add(v, v));
+    const auto Y3 = sub(mulr1(rr, sub(v, X3)), smul<2>(mulr1(s1, j)));
+    const auto Z3 = mulr1(sub(sub(sqrr1(add(p.z, q.z)), z1z1), z2z2), h);
+    return {reduce(X3), reduce(Y3), reduce(Z3)};
+}
+
 // storage form (curve.h Jac<Fp>, canonical, R = 2^406) <-> lazy R' form
 DEV JG jg_from(const Jac<Fp>& a) { return {reduce(in_r(a.x)), reduce(in_r(a.y)), reduce(in_r(a.z))}; }
 DEV Jac<Fp> jg_to(const JG& a) { return {out_r(a.x), out_r(a.y), out_r(a.z)}; }

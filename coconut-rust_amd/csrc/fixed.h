@@ -3,10 +3,10 @@
 // The verifier's MSMs (multi_scalar_mul_var_time over X~, Y~_j, g~) have FIXED
 // bases per verkey, so cc_set_verkey precomputes, per base B, nwin = ceil(256 / wbits) windows of the
 // 2^wbits - 1 affine multiples d * 2^(wbits w) * B (AoS, Montgomery).  A scalar multiplication is then
-// nwin mixed additions and no doublings.  The shared-verkey tables use wbits = 16 (16 windows: half
-// the additions of 8-bit windows; 100 MB per G1 base, 200 MB per G2 base — the tables live in HBM and
-// every lookup is one random 96/192-byte read, which the ~8 TB/s HBM serves far faster than the
-// VALU-bound additions consume them); the issuer tables (hundreds of bases) take the widest window
+// nwin mixed additions and no doublings.  The shared-verkey tables use the widest of wbits = 22 / 20 /
+// 16 that fits the HBM budget (capi.cpp rebuild_tables; 22 bits: 12 windows, 4.8 GB per G1 base — the
+// tables live in HBM and every lookup is one random 96/192-byte read, which the ~8 TB/s HBM serves far
+// faster than the VALU-bound additions consume them); the issuer tables (hundreds of bases) take the widest window
 // in {16, 13, 12, 10, 8} whose tables fit a memory budget (cc_set_issuers), the one-off
 // cc_fixed_base_mul wbits = 8.
 // An entry equal to the identity (only possible for a small-order base) is stored as (0, 0), which

@@ -218,6 +218,29 @@ __global__ __launch_bounds__(64) void k_table_fill(int nbases, int wbits, const 
 }
 
 // ================================================================ MSM helpers
+// acc += sum_j (m_j over windows [w0, w1)) Y~_j; G1 sums stay on the lazy field between the terms
+template <class F>
+DEV void msm_fixed_terms(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t* __restrict__ table, int wbits,
+                         const uint32_t* __restrict__ binf, int w0, int w1) {
+    if constexpr (std::is_same<F, Fp>::value) {
+        lz::JG a = lz::jg_from(acc);
+        for (int j = 0; j < q; j++) {
+            if (binf[j]) continue;  // uniform across the batch (shared verkey)
+            Fr m;
+            fr_from_be48(m, msgs + (size_t)j * 48);
+            ft_add_lz(a, m.v, table, wbits, j, w0, w1);
+        }
+        acc = lz::jg_to(a);
+    } else {
+        for (int j = 0; j < q; j++) {
+            if (binf[j]) continue;
+            Fr m;
+            fr_from_be48(m, msgs + (size_t)j * 48);
+            ft_add<F>(acc, m.v, table, wbits, j, w0, w1);
+        }
+    }
+}
+
 // fixed-base: acc = X~ + sum_j m_j Y~_j using the window tables
 template <class F>
 DEV void msm_fixed(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t* __restrict__ Xaff, uint32_t Xinf,
@@ -229,12 +252,7 @@ DEV void msm_fixed(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t* __re
         ld_aff_aos<F>(x, Xaff);
         jac_from_aff(acc, x);
     }
-    for (int j = 0; j < q; j++) {
-        if (binf[j]) continue;  // uniform across the batch (shared verkey)
-        Fr m;
-        fr_from_be48(m, msgs + (size_t)j * 48);
-        ft_add<F>(acc, m.v, table, wbits, j, 0, ft_nwin(wbits));
-    }
+    msm_fixed_terms<F>(acc, msgs, q, table, wbits, binf, 0, ft_nwin(wbits));
 }
 
 // fixed-base over windows [w0, w1) only, X~ included on request (the lane-pair split of msm_fixed)
@@ -249,12 +267,7 @@ DEV void msm_fixed_part(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t*
         ld_aff_aos<F>(x, Xaff);
         jac_from_aff(acc, x);
     }
-    for (int j = 0; j < q; j++) {
-        if (binf[j]) continue;  // uniform across the batch (shared verkey)
-        Fr m;
-        fr_from_be48(m, msgs + (size_t)j * 48);
-        ft_add<F>(acc, m.v, table, wbits, j, w0, w1);
-    }
+    msm_fixed_terms<F>(acc, msgs, q, table, wbits, binf, w0, w1);
 }
 
 // variable-base (per-credential verkey): interleaved double-and-add over the q+1 bases.

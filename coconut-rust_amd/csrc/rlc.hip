@@ -124,18 +124,18 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, int q, uint6
     uint32_t kk[NR], d[NR], w4[4];
     for (int k = 0; k < 8; k++) kk[k] = key[k];
     rlc_delta_signed(d, w4, kk, base_index + i);
-    Jac<Fp> acc;
-    jac_set_inf(acc);
+    lz::JG a = lz::jg_inf();  // the sum on the lazy field (fixed.h ft_add_lz)
     const int nwin = ft_nwin(wbits);
-    if (!binf[q + 1]) ft_add<Fp>(acc, d, table, wbits, q + 1, 0, nwin);  // delta X~
+    if (!binf[q + 1]) ft_add_lz(a, d, table, wbits, q + 1, 0, nwin);  // delta X~
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
         fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
         uint32_t dm[NR];
         fr_mul_canon(dm, d, m.v);
-        ft_add<Fp>(acc, dm, table, wbits, j, 0, nwin);
+        ft_add_lz(a, dm, table, wbits, j, 0, nwin);
     }
+    const Jac<Fp> acc = lz::jg_to(a);
     if (jac_is_inf(acc)) flags[i] |= 4u;
     st_eval(S, S_P1, i, acc);
 }

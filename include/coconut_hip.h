@@ -75,8 +75,9 @@ cc_status cc_ctx_mode(const cc_ctx* ctx, int* mode_out);
 cc_status cc_set_params(cc_ctx* ctx, const uint8_t* g_tilde);
 
 /* Shared verkey (X~, Y~[q]) for cc_verify_batch with vk == NULL: builds fixed-base tables on the
- * device (one-time cost, reported separately from batch throughput): 16-bit windows when the q + 2
- * bases' tables fit half the free HBM (at most 64 GiB), else 8-bit windows.  On any failure the
+ * device (one-time cost, reported separately from batch throughput): the widest of 22 / 20 / 16-bit
+ * windows whose q + 2 bases' tables fit 40 % of the free HBM (at most 96 GiB), else 8-bit windows.
+ * On any failure the
  * context is left WITHOUT a verkey (verify / RLC / PoK calls then return CC_ERR_STATE). */
 cc_status cc_set_verkey(cc_ctx* ctx, const uint8_t* X, const uint8_t* Y, size_t q);
 

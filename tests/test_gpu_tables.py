@@ -6,7 +6,7 @@ cc_device_error):
   the oracle's verdicts and GT bytes with either width;
 * issuer tables at every width the budget can pick (8, 10, 12, 13, 16): the golden Verkey::aggregate
   cases;
-* a verkey too large for 16-bit tables (q = 2,048 in SigG1: 410 GB) falls back to 8 bits and verifies;
+* a verkey too large for wide tables (q = 2,048 in SigG1: 410 GB at 16 bits) falls back to 8 bits and verifies;
   forcing 16 bits there fails and leaves the context WITHOUT a verkey (CC_ERR_STATE afterwards);
 * Lagrange with t > 3,968 (ids past the 64 KiB LDS staging, read from global memory): Shamir-shared
   signatures and verkeys aggregate to the master values (signature.rs:554-559 identity);

@@ -17,7 +17,7 @@ for m in $MODES; do
     [ $v = prev ] && lib=$(pwd)/coconut-rust_amd/libcoconut_hip_prev.so
     [ -f "$lib" ] || continue
     echo "[abm] bench $m $v"
-    COCONUT_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --mode $m --steps 5 --warmup 1 --no-cpu-baseline > "$OUT/${m}_$v.json" 2> "$OUT/${m}_$v.err" || exit 1
+    COCONUT_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --mode $m --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/${m}_$v.json" 2> "$OUT/${m}_$v.err" || exit 1
   done
 done
 echo "[abm] done"
