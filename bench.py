@@ -606,7 +606,7 @@ def main():
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) rate")
     ap.add_argument("--vk-bits", type=int, default=0,
                     help="verkey table window width (cc_set_table_bits; 0 = the library's choice)")
-    ap.add_argument("--mode", choices=["verify", "verify-g1", "rlc", "aggregate", "pok", "stub"], default="verify")
+    ap.add_argument("--mode", choices=["verify", "verify-g1", "rlc", "aggregate", "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
     args = ap.parse_args()
     if args.backend:
         BACKEND = args.backend
@@ -625,7 +625,7 @@ def main():
         return bench_verify(args, 1)
     if args.mode == "rlc":
         return bench_rlc(args)
-    if args.mode == "aggregate":
+    if args.mode in ("aggregate", "aggregate-g1"):
         from bench_modes import bench_aggregate
         return bench_aggregate(args)
     from bench_modes import bench_pok

@@ -148,9 +148,10 @@ def bench_aggregate(args):
     world, rank, local, dist = _dist_setup()
     dev = torch.device("cuda", local)
     n = args.n or 10000
-    ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
+    sigm = 1 if args.mode.endswith("-g1") else 0  # aggregate-g1: SigG1 (sigma in G1, issuer keys in G2)
+    ctx = coconut.Context(local, coconut.GroupMode.SIG_G1 if sigm else coconut.GroupMode.SIG_G2)
     t_set = time.perf_counter()
-    b = make_aggregate_batch(ctx, 0, n, seed=4000 + rank)
+    b = make_aggregate_batch(ctx, sigm, n, seed=4000 + rank)
     gen_s = time.perf_counter() - t_set
     t_iss = time.perf_counter()
     ctx.set_issuers(b["iss"], b["X"], b["Y"], b["q"])
@@ -188,7 +189,8 @@ def bench_aggregate(args):
     if rank == 0:
         peak = peak_mad_per_s()
         sig_ms, vk_ms = phase[1], phase[2]
-        counts = opcounts("aggregate_sigg2_t67")
+        # the op-count fixture covers SigG2; SigG1 lines report times only
+        counts = opcounts("aggregate_sigg2_t67") if not sigm else {"straus_sigma2": 0, "fixed_verkey": 0}
         k_sig = counts["straus_sigma2"] * MADS_PER_M * n / (sig_ms * 1e-3)
         k_vk = counts["fixed_verkey"] * MADS_PER_M * n / (vk_ms * 1e-3)
         dom, ach = ("signature_msm", k_sig) if sig_ms >= vk_ms else ("verkey_msm", k_vk)
@@ -201,7 +203,8 @@ def bench_aggregate(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "u32 (Fp 12x32-bit Montgomery limbs, integer-only)",
             "data": "synthetic (seeded Shamir-shared issuer keys; random 67-subsets; outputs checked = x g~, y_j g~, "
                     "(x + sum y m) h)",
-            "config": {"workload": f"config4: {n:,} credentials per GPU, t=67 of n=100 issuers, msg_count={q}, SigG2",
+            "config": {"workload": f"config4: {n:,} credentials per GPU, t=67 of n=100 issuers, msg_count={q}, "
+                                   + ("SigG1" if sigm else "SigG2"),
                        "credentials_per_gpu": n, "threshold": t, "issuers": 100,
                        "parallelism": f"shard-by-credential x{world}"},
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 3),
@@ -217,7 +220,9 @@ def bench_aggregate(args):
             "rocprof_kernels": rk,
             "setup": {"issuer_tables_ms": round(iss_ms, 1), "synthetic_data_s": round(gen_s, 2)},
         }
-        if not args.no_cpu_baseline and world == 1:
+        if sigm:
+            out["roofline"] = None  # no SigG1 op-count fixture (tests/fixtures/opcount.json)
+        if not args.no_cpu_baseline and world == 1 and not sigm:
             out["cpu_baseline"] = cpu_aggregate(b)
         print(json.dumps(out), flush=True)
     if dist:
@@ -260,9 +265,10 @@ def bench_pok(args):
     world, rank, local, dist = _dist_setup()
     dev = torch.device("cuda", local)
     n = args.n or 65536
-    ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
+    sigm = 1 if args.mode.endswith("-g1") else 0  # pok-g1: SigG1 (sigma in G1, Schnorr MSM in G2)
+    ctx = coconut.Context(local, coconut.GroupMode.SIG_G1 if sigm else coconut.GroupMode.SIG_G2)
     t0 = time.perf_counter()
-    b = make_pok_batch(ctx, 0, n, seed=5000 + rank)
+    b = make_pok_batch(ctx, sigm, n, seed=5000 + rank)
     gen_s = time.perf_counter() - t0
     ctx.set_params(b["g_tilde"])
     if args.vk_bits:
@@ -291,7 +297,7 @@ def bench_pok(args):
     if rank == 0:
         from bench import kernel_table, cpu_info, kernel_pmc_report
         peak = peak_mad_per_s()
-        counts = opcounts("pok_sigg2_q32_r8")
+        counts = opcounts("pok_sigg2_q32_r8")  # SigG2 op counts; a SigG1 line's fractions are not meaningful
         kt = kernel_table(phase_ms, n, counts, 2 * 192 + 2 * 97 + (nresp + 1 + r) * 48, peak, "k_prep_pok", "pok")
         dom = max(kt, key=lambda k: kt[k]["ms"])
         out = {
@@ -301,7 +307,7 @@ def bench_pok(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "int32/u32 (pairing kernels: 14 signed 28-bit-radix limbs, lazy; elsewhere 12x32-bit Montgomery; integer-only)",
             "data": "synthetic (seeded; proofs with known discrete logs built on the GPU; 1/16 bad response)",
             "config": {"workload": f"config5: {n:,} PoKOfSignatureProof::verify per GPU, q=32, revealed "
-                                   f"{b['revealed']}, SigG2", "proofs_per_gpu": n,
+                                   f"{b['revealed']}, " + ("SigG1" if sigm else "SigG2"), "proofs_per_gpu": n,
                        "parallelism": f"shard-by-proof x{world}"},
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
@@ -311,7 +317,9 @@ def bench_pok(args):
             "rocprof_kernels": kernel_pmc_report("pok"),
             "setup": {"synthetic_data_s": round(gen_s, 2), "verkey_table_bits": ctx.table_bits()[0]},
         }
-        if not args.no_cpu_baseline and world == 1:
+        if sigm:
+            out["roofline"] = None  # no SigG1 op-count fixture
+        if not args.no_cpu_baseline and world == 1 and not sigm:
             oc = __import__("bench")._oracle()
             k = 24
             ver = []

@@ -677,76 +677,133 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
     encode_pt<F>(o, r, fin);
 }
 
+// SigG1 (G2 issuer keys): the same task on lane PAIRS (curve_pl.h: one point per pair, each lane one
+// half of every Fp2 coordinate, the storage-form table add pl::ft_add_g2), L lanes = L / 2 pairs a task.
+// The one-lane G2 form needed all 512 VGPRs (one wave per SIMD); the pair form fits two.
+template <int L>
+__global__ __launch_bounds__(256, 2) void k_vk_agg_fixed_g2pl(size_t n, size_t len, size_t t, int q,
+                                                            const uint64_t* __restrict__ ids,
+                                                            const uint32_t* __restrict__ l,
+                                                            const uint64_t* __restrict__ iss_ids, int n_iss,
+                                                            const uint32_t* __restrict__ table, int wbits,
+                                                            const uint32_t* __restrict__ binf,
+                                                            uint8_t* __restrict__ outX, uint8_t* __restrict__ outY,
+                                                            uint32_t* __restrict__ err) {
+    constexpr int NPR = L / 2;
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t task = g / L;
+    const int lane = (int)(g % L), pair = lane >> 1, h = lane & 1;
+    if (task >= n * (size_t)(q + 1)) return;  // uniform over the lane group
+    const size_t cred = task / (q + 1);
+    const int j = (int)(task % (q + 1));
+    Jac<pl::Fp2> acc;
+    jac_set_inf(acc);
+    int bad = 0;
+#pragma unroll 1
+    for (size_t k = pair; k < t; k += NPR) {  // pair-uniform
+        const uint64_t id = ids[cred * len + k];
+        int lo = 0, hi = n_iss;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (iss_ids[mid] < id) lo = mid + 1; else hi = mid;
+        }
+        if (lo >= n_iss || iss_ids[lo] != id) {  // no issuer verkey for this id
+            bad = 1;
+            continue;
+        }
+        const int b = lo * (q + 1) + j;
+        if (binf[b]) continue;
+        pl::ft_add_g2(acc, l + (cred * t + k) * 8, table, wbits, b, 0, ft_nwin(wbits));
+    }
+    pl::pair_group_sum<L>(acc);
+#pragma unroll
+    for (int o = 1; o < L; o <<= 1) bad |= __shfl_xor(bad, o, L);
+    if (pair) return;  // pair 0 writes
+    if (bad) {
+        if (!h) atomicOr(err, 1u);  // CC_DEVERR_UNKNOWN_ID
+        jac_set_inf(acc);
+    }
+    Aff<pl::Fp2> r;
+    const bool fin = jac_to_aff(r, acc);
+    Aff<Fp2> o;  // both halves on lane h = 0 for the encoding
+    const Fp xs = pl::swp(r.x.c), ys = pl::swp(r.y.c);
+    o.x.a = h ? xs : r.x.c;
+    o.x.b = h ? r.x.c : xs;
+    o.y.a = h ? ys : r.y.c;
+    o.y.b = h ? r.y.c : ys;
+    uint8_t* out = j == 0 ? outX + cred * 192 : outY + (cred * q + (j - 1)) * 192;
+    if (!h) g2_encode(out, o, fin);
+}
+
 // ================================================================ PoK verify prep
 // Prep layout (soa.h: Q1 0..3 | Q2 4..7 | P1 8..10 | P2 11..12) and flag bits as kernels.hip,
 // plus flag bit3 = Schnorr check failed.
 
-// FS_: SignatureGroup field, FO: OtherGroup field; MINB blocks a CU (2 for SigG2: its G1 Schnorr MSM
-// fits 2 waves/SIMD, ~10 registers over the bound otherwise ran it at one wave/SIMD)
-template <class FS_, class FO, int MINB>
-__global__ __launch_bounds__(256, MINB) void k_prep_pok(size_t n, int q, int r, const uint8_t* __restrict__ s1b,
-                                                  const uint8_t* __restrict__ s2b, const uint8_t* __restrict__ Jb,
-                                                  const uint8_t* __restrict__ Tb, const uint8_t* __restrict__ resp,
-                                                  const uint8_t* __restrict__ chal,
-                                                  const uint8_t* __restrict__ rev_msgs,
-                                                  const uint32_t* __restrict__ rev_idx,
-                                                  const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                                                  const uint32_t* __restrict__ table, int wbits,
-                                                  const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep,
-                                                  uint32_t* __restrict__ flags, uint32_t* __restrict__ jtab) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    constexpr bool kSigG2 = sizeof(FS_) == sizeof(Fp2);
-    constexpr int SB = ebytes<FS_>(), OB = ebytes<FO>();
+// SigG1 PoK prep (sigma' in G1, the Schnorr MSM and J' in G2), one proof per lane PAIR (curve_pl.h): lane h
+// decodes sigma'_{h+1} (G1), the G2 sums run on the pair-lane Fp2 (pl::ft_add_g2 over the verkey tables,
+// chal J in fixed 4-bit windows from a per-lane table of d J, d = 1..15, in jtab), the pair writes J' as
+// pair 0's Q.  The one-lane form needed all 512 VGPRs and spilled (one wave per SIMD).
+__global__ __launch_bounds__(256, 2) void k_prep_pok_g1pl(size_t n, int q, int r, const uint8_t* __restrict__ s1b,
+                                                        const uint8_t* __restrict__ s2b,
+                                                        const uint8_t* __restrict__ Jb,
+                                                        const uint8_t* __restrict__ Tb,
+                                                        const uint8_t* __restrict__ resp,
+                                                        const uint8_t* __restrict__ chal,
+                                                        const uint8_t* __restrict__ rev_msgs,
+                                                        const uint32_t* __restrict__ rev_idx,
+                                                        const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                        const uint32_t* __restrict__ table, int wbits,
+                                                        const uint32_t* __restrict__ binf,
+                                                        uint32_t* __restrict__ prep, uint32_t* __restrict__ flags,
+                                                        uint32_t* __restrict__ jtab) {
+    using G2 = pl::Fp2;
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t i = g >> 1;
+    const int h = (int)(g & 1);
+    if (i >= n) return;  // pair-uniform
     Soa S{prep, n};
     uint32_t fl = 0;
-    // sigma'
-    {
-        Aff<FS_> a;
-        if (!decode_pt<FS_>(a, s1b + i * SB)) fl |= 1u;
-        const Fp* pa = reinterpret_cast<const Fp*>(&a);
-        if (kSigG2) {
-            for (int c = 0; c < 4; c++) st_fp(S, S_Q1 + c, i, pa[c]);
-        } else {
-            for (int c = 0; c < 2; c++) st_fp(S, S_P1 + c, i, pa[c]);
-        }
-        if (!decode_pt<FS_>(a, s2b + i * SB)) fl |= 2u;
-        FT<FS_>::neg(a.y, a.y);
-        if (kSigG2) {
-            for (int c = 0; c < 4; c++) st_fp(S, S_Q2 + c, i, pa[c]);
-        } else {
-            for (int c = 0; c < 2; c++) st_fp(S, S_P2 + c, i, pa[c]);
-        }
+    {  // sigma'_1 on lane 0 (P1), -sigma'_2 on lane 1 (P2)
+        Aff<Fp> a;
+        if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
+        if (h) fp_neg(a.y, a.y);
+        const int slot = h ? S_P2 : S_P1;
+        st_fp(S, slot, i, a.x);
+        st_fp(S, slot + 1, i, a.y);
     }
-    // Schnorr: acc = g~ * resp[0] + sum_hidden Y~_h * resp[k] + J * chal - T  ==  O ?
-    Aff<FO> Ja;
-    const bool Jok = decode_pt<FO>(Ja, Jb + i * OB);
-    Jac<FO> acc;
+    fl |= pl::swp(fl);
+    // a G2 point as this lane's halves (both lanes decode it)
+    auto own = [&](Aff<G2>& o, const Aff<Fp2>& a) {
+        o.x.c = h ? a.x.b : a.x.a;
+        o.y.c = h ? a.y.b : a.y.a;
+    };
+    Aff<Fp2> Jf;
+    const bool Jok = pl::pair_all(g2_decode(Jf, Jb + i * 192));
+    Aff<G2> Ja;
+    own(Ja, Jf);
+    // Schnorr: acc = g~ resp[0] + sum_hidden Y~_h resp[k] + J chal - T == O ?
+    Jac<G2> acc;
     jac_set_inf(acc);
     {
         Fr k;
         const uint8_t* rp = resp + i * (size_t)(q - r + 1) * 48;
         fr_from_be48(k, rp);
         const int nwin = ft_nwin(wbits);
-        if (!binf[q]) ft_add<FO>(acc, k.v, table, wbits, q, 0, nwin);  // table base q = g~
+        if (!binf[q]) pl::ft_add_g2(acc, k.v, table, wbits, q, 0, nwin);  // table base q = g~
         int slot = 1;
-        for (int h = 0; h < q; h++) {
+        for (int hh = 0; hh < q; hh++) {
             bool revealed = false;
-            for (int z = 0; z < r; z++) revealed |= rev_idx[z] == (uint32_t)h;
+            for (int z = 0; z < r; z++) revealed |= rev_idx[z] == (uint32_t)hh;
             if (revealed) continue;
             fr_from_be48(k, rp + (size_t)slot * 48);
             slot++;
-            if (!binf[h]) ft_add<FO>(acc, k.v, table, wbits, h, 0, nwin);
+            if (!binf[hh]) pl::ft_add_g2(acc, k.v, table, wbits, hh, 0, nwin);
         }
-        // J * chal (variable base), fixed 4-bit windows: a per-lane table d J (d = 1..15, Jacobian, SoA
-        // in jtab) and 64 windows of 4 doublings + one addition.  The bitwise double-and-add it
-        // replaces ran an addition at nearly every bit in SIMT (some lane of the wave has the bit set):
-        // 255 + 255 group operations against 255 + 64 + 14 here.
         fr_from_be48(k, chal + i * 48);
         if (Jok) {
-            constexpr int JW = sizeof(Jac<FO>) / 4;
-            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * JW + w) * n + i]; };
-            Jac<FO> t;
+            constexpr int JW = sizeof(Jac<G2>) / 4;
+            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * JW + w) * 2 * n + g]; };
+            Jac<G2> t;
             jac_from_aff(t, Ja);
 #pragma unroll 1
             for (int d = 1; d <= 15; d++) {
@@ -754,61 +811,53 @@ __global__ __launch_bounds__(256, MINB) void k_prep_pok(size_t n, int q, int r, 
                 const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
                 for (int w = 0; w < JW; w++) tab(d, w) = tw[w];
             }
-            Jac<FO> s;
-            jac_set_inf(s);
+            Jac<G2> sacc;
+            jac_set_inf(sacc);
 #pragma unroll 1
             for (int win = 63; win >= 0; win--) {
-                for (int b = 0; b < 4; b++) jac_dbl(s, s);
+                for (int b = 0; b < 4; b++) jac_dbl(sacc, sacc);
                 const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
                 if (d) {
                     uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
                     for (int w = 0; w < JW; w++) tw[w] = tab((int)d, w);
-                    jac_add(s, s, t);
+                    jac_add(sacc, sacc, t);
                 }
             }
-            jac_add(acc, acc, s);
+            jac_add(acc, acc, sacc);
         }
-        Aff<FO> Ta;
-        if (decode_pt<FO>(Ta, Tb + i * OB)) {
-            FT<FO>::neg(Ta.y, Ta.y);
+        Aff<Fp2> Tf;
+        if (pl::pair_all(g2_decode(Tf, Tb + i * 192))) {
+            Aff<G2> Ta;
+            own(Ta, Tf);
+            FT<G2>::neg(Ta.y, Ta.y);
             jac_add_aff(acc, acc, Ta);
         }
         if (!jac_is_inf(acc)) fl |= 8u;
     }
     // J' = X~ + J + sum_revealed Y~_i m_i
-    Jac<FO> jp;
+    Jac<G2> jp;
     if (Xinf) {
         jac_set_inf(jp);
     } else {
-        Aff<FO> x;
-        ld_aff_aos<FO>(x, Xaff);
+        Aff<G2> x;
+        for (int c = 0; c < NL; c++) {
+            x.x.c.v[c] = Xaff[NL * h + c];
+            x.y.c.v[c] = Xaff[2 * NL + NL * h + c];
+        }
         jac_from_aff(jp, x);
     }
     if (Jok) jac_add_aff(jp, jp, Ja);
     for (int z = 0; z < r; z++) {
         Fr m;
         fr_from_be48(m, rev_msgs + ((size_t)i * r + z) * 48);
-        int h = (int)rev_idx[z];
-        if (!binf[h]) ft_add<FO>(jp, m.v, table, wbits, h, 0, ft_nwin(wbits));
+        const int hh = (int)rev_idx[z];
+        if (!binf[hh]) pl::ft_add_g2(jp, m.v, table, wbits, hh, 0, ft_nwin(wbits));
     }
-    if (jac_is_inf(jp)) fl |= 4u;
-    if (kSigG2) {
-        // P1 = J' (G1) in line-evaluation form (X Z, Y, Z^3)
-        const Jac<Fp>& g = *reinterpret_cast<const Jac<Fp>*>(&jp);
-        Fp t;
-        fp_mul(t, g.x, g.z);
-        st_fp(S, S_P1, i, t);
-        st_fp(S, S_P1 + 1, i, g.y);
-        fp_sqr(t, g.z);
-        fp_mul(t, t, g.z);
-        st_fp(S, S_P1 + 2, i, t);
-    } else {
-        Aff<FO> a;
-        jac_to_aff(a, jp);
-        const Fp* pa = reinterpret_cast<const Fp*>(&a);
-        for (int c = 0; c < 4; c++) st_fp(S, S_Q1 + c, i, pa[c]);
-    }
-    flags[i] = fl;
+    Aff<G2> a;
+    if (!jac_to_aff(a, jp)) fl |= 4u;
+    pl::st_f2(S, S_Q1, i, a.x);
+    pl::st_f2(S, S_Q1 + 2, i, a.y);
+    if (!h) flags[i] = fl;
 }
 
 // ================================================================ fixed-base scalar multiplication
@@ -897,8 +946,8 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
         hipLaunchKernelGGL((k_vk_agg_fixed<Fp, L>), g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss, d_table,
                            wbits, d_binf, d_outX, d_outY, d_err);
     else
-        hipLaunchKernelGGL((k_vk_agg_fixed<Fp2, 4>), dim3(nblocks(ntask * 4, 256)), b, 0, st, n, len, t, q, d_ids,
-                           d_l, d_iss_ids, n_iss, d_table, wbits, d_binf, d_outX, d_outY, d_err);  // G2 keys: 4 lanes
+        hipLaunchKernelGGL((k_vk_agg_fixed_g2pl<L>), g, b, 0, st, n, len, t, q, d_ids, d_l, d_iss_ids, n_iss,
+                           d_table, wbits, d_binf, d_outX, d_outY, d_err);  // G2 keys: 4 lane pairs a task
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -919,8 +968,8 @@ int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const ui
                            d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf,
                            d_prep, d_flags, d_jtab);
     } else
-        hipLaunchKernelGGL((k_prep_pok<Fp, Fp2, 1>), g, b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal,
-                           d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags, d_jtab);
+        hipLaunchKernelGGL(k_prep_pok_g1pl, dim3(nblocks(2 * n, 256)), b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp,
+                           d_chal, d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags, d_jtab);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

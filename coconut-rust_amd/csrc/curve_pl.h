@@ -64,6 +64,22 @@ DEV bool g2_in_subgroup(const Aff<Fp2>& q) {
     return jac_is_inf(t);
 }
 
+// the same test on the lazy pair-lane field (curve_lz.h): [|x|] Q by double-and-add over |x|, plus psi(Q)
+// (formed in the storage form, two Fp2 products), is the identity
+DEV bool g2_in_subgroup_lz(const Aff<Fp2>& q) {
+    const lz::AL a{lz::reduce(lz::in_r2(q.x)), lz::reduce(lz::in_r2(q.y))};
+    lz::JL t = lz::jl_from_aff(a);
+#pragma unroll 1
+    for (int b = 62; b >= 0; b--) {
+        t = lz::jl_dbl(t);
+        if ((X_ABS >> b) & 1ull) t = lz::jl_add_aff(t, a);
+    }
+    Aff<Fp2> ps;
+    g2_psi(ps, q);
+    t = lz::jl_add_aff(t, lz::AL{lz::reduce(lz::in_r2(ps.x)), lz::reduce(lz::in_r2(ps.y))});
+    return lz::jl_is_inf(t);
+}
+
 // The Miller loop's twist point ends as T = [|x|] Q (homogeneous projective: x = X/Z, y = Y/Z; the
 // loop walks |x|'s addition chain), so Q is in G2 iff psi(Q) == [x] Q = -T: X = psi_x Z, Y = -psi_y Z,
 // Z != 0 (eprint 2021/1130 §4, the test of g2_in_subgroup at the cost of two Fp2 multiplications).

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t b
     Aff<pl::Fp2> p;
     p.x = pl::f2_from_lane(a.x, 1);
     p.y = pl::f2_from_lane(a.y, 1);
-    if (!(fl & 2u) && !pl::g2_in_subgroup(p)) fl |= 32u;
+    if (!(fl & 2u) && !pl::g2_in_subgroup_lz(p)) fl |= 32u;
     uint32_t kk[NR], d[NR], w4[4];
     for (int k = 0; k < 8; k++) kk[k] = key[k];
     rlc_delta_signed(d, w4, kk, base_index + i);
