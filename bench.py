@@ -492,13 +492,25 @@ def bench_rlc(args):
     d_s1, d_s2, d_m = to_dev(batch["s1"], dev), to_dev(batch["s2"], dev), to_dev(batch["msgs"], dev)
     eng = DeviceEngine(ctx, n, q, d_s1, d_s2, d_m, base_index=rank * n)
 
-    def step():
+    # batches are pipelined: batch i's single final exponentiation (one wave, latency-bound) runs on the
+    # engine's finish stream while batch i+1's partial runs (DeviceEngine.finish_async)
+    def run(k_steps, phase=None):
+        ok = True
         part = eng.partial()
-        allp, k = gather_partials(part)
-        return eng.finish(allp, k)
+        if phase is not None:
+            phase += np.array(ctx.last_timing())
+        for s in range(k_steps):
+            allp, k = gather_partials(part)
+            decision = eng.finish_async(allp, k)
+            if s + 1 < k_steps:
+                part = eng.partial()
+                if phase is not None:
+                    phase += np.array(ctx.last_timing())
+            ok &= decision()
+        return ok
 
-    for _ in range(args.warmup):
-        assert step()
+    if args.warmup:
+        assert run(args.warmup)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -506,10 +518,7 @@ def bench_rlc(args):
     ctx.timing(True)
     phase = np.zeros(3)
     t0 = time.perf_counter()
-    ok = True
-    for _ in range(args.steps):
-        ok &= step()
-        phase += np.array(ctx.last_timing())
+    ok = run(args.steps, phase)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()

@@ -87,8 +87,14 @@ class DeviceEngine:
         # which is not ordered against torch's default stream
         self.stream = stream if stream is not None else torch.cuda.Stream(self.dev)
         self._sh = ctypes.c_void_p(self.stream.cuda_stream)
-        self.part = torch.empty(PARTIAL_WORDS, dtype=torch.int32, device=self.dev)
-        self.accept = torch.zeros(1, dtype=torch.uint8, device=self.dev)
+        # two partial / accept buffers: a pipelined caller's finish of batch i (finish_async, on its own
+        # stream) may still read one while the next partial writes the other
+        self._parts = [torch.empty(PARTIAL_WORDS, dtype=torch.int32, device=self.dev) for _ in range(2)]
+        self._accepts = [torch.zeros(1, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        self._slot = 0
+        self.part = self._parts[0]
+        self.accept = self._accepts[0]
+        self._fin_stream = None
         self.verdicts = torch.zeros(n, dtype=torch.uint8, device=self.dev)
 
     def _enter(self):
@@ -106,6 +112,8 @@ class DeviceEngine:
 
     def partial(self):
         seed = self.seed if self.seed is not None else os.urandom(32)
+        self._slot ^= 1
+        self.part = self._parts[self._slot]
         self._enter()
         self._check(self.lib.cc_rlc_partial_device(self.ctx.h, self.n, self.q, self.base_index, seed,
                                                    ctypes.c_void_p(self.d_s1.data_ptr()),
@@ -126,6 +134,30 @@ class DeviceEngine:
         if not sync:
             return None
         return bool(self.accept.item())
+
+    def finish_async(self, allp, k: int):
+        """cc_rlc_finish_device on the engine's second stream, NOT ordered before later work on the
+        engine's main stream: the next batch's partial() can overlap this batch's final exponentiation.
+        Returns a callable that waits for the decision and returns it."""
+        import torch
+        if self._fin_stream is None:
+            self._fin_stream = torch.cuda.Stream(self.dev)
+        fs = self._fin_stream
+        allp = allp.contiguous()
+        fs.wait_stream(torch.cuda.current_stream(self.dev))  # the gathered partials are ready
+        fs.wait_stream(self.stream)
+        allp.record_stream(fs)
+        acc = self._accepts[self._slot]
+        self._check(self.lib.cc_rlc_finish_device(self.ctx.h, k, ctypes.c_void_p(allp.data_ptr()),
+                                                  ctypes.c_void_p(acc.data_ptr()), None,
+                                                  ctypes.c_void_p(fs.cuda_stream)), "cc_rlc_finish_device")
+        ev = torch.cuda.Event()
+        ev.record(fs)
+
+        def result() -> bool:
+            ev.synchronize()
+            return bool(acc.item())
+        return result
 
     def per_credential(self) -> np.ndarray:
         self._enter()

@@ -146,6 +146,7 @@ struct cc_ctx {
     DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, vkbinf, msgs_canon, lag;
     // RLC batch mode: ChaCha20 key, identity flag word, partial / gathered partials, verdict
     DevBuf rlc_key, rlc_any, rlc_part, rlc_flag, rlc_accept;
+    DevBuf fin_f, fin_scratch;  // cc_rlc_finish_device's own buffers
     // RLC g~-side fold (fold.hip): fold points, delta digits, sort/partials workspace, the 1,024
     // pseudo-credentials' prep SoA (bucket sums + the fixed points P_w,d = (256^w d) g~) and flags
     DevBuf rlc_pts, rlc_dig, rlc_work, rlc_prep2, rlc_finf, rlc_flags2;
@@ -295,7 +296,7 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag,
-                      &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->pok_idx, &c->rlc_gath,
+                      &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->fin_f, &c->fin_scratch, &c->pok_idx, &c->rlc_gath,
                       &c->rlc_pts, &c->rlc_dig, &c->rlc_work, &c->rlc_prep2, &c->rlc_finf, &c->rlc_flags2,
                       &c->iss_ids, &c->iss_aff, &c->iss_inf, &c->iss_table, &c->agg_scratch, &c->dev_err};
     for (auto* b : bufs) b->release();
@@ -672,14 +673,16 @@ cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_parti
     c = primary(c);  // a device set forwards to its first device
     if (!c || !nparts || !d_partials || !d_accept) return CC_ERR_DECODE;
     HIPCK(hipSetDevice(c->device));
-    cc_status s = ensure_work(c, 1);
-    if (s) return s;
-    if (c->rlc_flag.ensure(4)) return CC_ERR_HIP;
+    // the finish owns its buffers (combined product, the one-element fexp's scratch, flag) and touches no
+    // other context state, so it is NOT ordered against the context's stream: on a caller stream it may
+    // overlap the next batch's cc_rlc_partial_device (the caller orders d_partials itself)
+    if (c->rlc_flag.ensure(4) || c->fin_f.ensure(12 * 12 * 4) || c->fin_scratch.ensure(2 * 72 * 12 * 4))
+        return CC_ERR_HIP;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    StreamOrder order(c, st);
-    KCK(cck_rlc_combine(nparts, d_partials, c->fbuf.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), st));
+    KCK(cck_rlc_combine(nparts, d_partials, c->fin_f.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), st));
     // one final exponentiation; flags[0] bit0 (a sigma was the identity somewhere) forces a reject
-    KCK(cck_fexp(1, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), d_accept, d_gt, st));
+    KCK(cck_fexp(1, c->fin_f.as<uint32_t>(), c->fin_scratch.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), d_accept,
+                 d_gt, st));
     return CC_OK;
 }
 

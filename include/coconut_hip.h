@@ -119,8 +119,11 @@ cc_status cc_verify_batch_device(cc_ctx* ctx, size_t n, size_t q, const uint8_t*
  *                          per-credential verdict is 1); 0 means "fall back to per-credential
  *                          verification" (a bad or identity credential somewhere).  d_gt optional
  *                          (576 B, GT of the combined product).
- * Both are asynchronous on `stream` (NULL: the context stream).  cc_verify_batch(..., rlc = 1)
- * runs the single-GPU form with a fresh seed from /dev/urandom and falls back by itself. */
+ * Both are asynchronous on `stream` (NULL: the context stream).  The partial is ordered against the
+ * context's other work; the finish owns its buffers and is NOT, so on a second stream it may overlap
+ * the next batch's partial (the caller orders d_partials before it, and two finishes of one context
+ * one after the other).  cc_verify_batch(..., rlc = 1) runs the single-GPU form with a fresh seed
+ * from /dev/urandom and falls back by itself. */
 cc_status cc_rlc_partial_device(cc_ctx* ctx, size_t n, size_t q, uint64_t base_index, const uint8_t* seed32,
                                 const uint8_t* d_sigma1, const uint8_t* d_sigma2, const uint8_t* d_msgs,
                                 uint32_t* d_partial, void* stream);
