@@ -516,7 +516,9 @@ def decode(g, enc):
     return a if g.on_curve(a) else None
 
 
-VK_WBITS = 16  # shared-verkey tables (fixed.h; capi.cpp verkey_table_bits)
+VK_WBITS = 22  # shared-verkey tables (fixed.h; capi.cpp rebuild_tables: the widest of 22 / 20 / 16 bits whose
+# tables fit the HBM budget -- 22 for configs 2 and 3 (8 / 18 G1 bases), 20 for config 5 (34 bases); main()
+# sets it per config)
 
 
 def fixed_table_mul_add(g, acc, k, base_aff, w0, w1, wbits=8):
@@ -554,7 +556,7 @@ def verify_sigg2(cred, vk_aff, gtil_aff, q):
     # lane pair: windows 0..15 (with X) on the even lane, 16..31 on the odd lane, then one jac_add
     lo = (X[0], X[1], 1) if X else G1.inf()
     hi = G1.inf()
-    nw = 256 // VK_WBITS
+    nw = -(-256 // VK_WBITS)
     for j in range(q):
         lo = fixed_table_mul_add(G1, lo, msgs[j], Ys[j], 0, nw // 2, VK_WBITS)
         hi = fixed_table_mul_add(G1, hi, msgs[j], Ys[j], nw // 2, nw, VK_WBITS)
@@ -587,7 +589,7 @@ def verify_sigg1(cred, vk_aff, gtil_aff, q):
     X, Ys = vk_aff
     acc = (X[0], X[1], F2_ONE) if X else G2.inf()
     for j in range(q):
-        acc = fixed_table_mul_add(G2, acc, msgs[j], Ys[j], 0, 256 // VK_WBITS, VK_WBITS)
+        acc = fixed_table_mul_add(G2, acc, msgs[j], Ys[j], 0, -(-256 // VK_WBITS), VK_WBITS)
     pr = G2.to_aff(acc)
     counts["prep"] = C.take()
     # pair 0: (pr, sigma_1); pair 1: (g~ [precomputed lines: no line cost], -sigma_2)
@@ -760,7 +762,7 @@ def pok_sigg2(d, p, vk_aff, gtil):
     Ja = decode(G1, bytes.fromhex(p["J"]))
     resp = [int(h, 16) % R for h in p["responses"]]
     chal = int(p["chal"], 16) % R
-    nw = 256 // VK_WBITS
+    nw = -(-256 // VK_WBITS)
     acc = fixed_table_mul_add(G1, G1.inf(), resp[0], gtil, 0, nw, VK_WBITS)
     slot = 1
     for h in range(q):
@@ -836,7 +838,7 @@ def rlc_sigg2(cred, vk_aff, gtil_aff, q, rnd):
     X, Ys = vk_aff
     delta = rnd.getrandbits(128) - (1 << 127)
     d = delta % R
-    nw = 256 // VK_WBITS
+    nw = -(-256 // VK_WBITS)
     acc = fixed_table_mul_add(G1, G1.inf(), d, X, 0, nw, VK_WBITS)
     for j in range(q):
         acc = fixed_table_mul_add(G1, acc, d * msgs[j] % R, Ys[j], 0, nw, VK_WBITS)
@@ -884,6 +886,7 @@ def run_fixture(d, limit=None):
 
 
 def main():
+    global VK_WBITS
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {"unit": "M = one 381-bit Montgomery multiplication = 288 algorithmic 32x32->64 mads",
            "mads_per_M": 288,
@@ -913,6 +916,7 @@ def main():
                 "tests/golden/aggregate_g2_t67_subsets.json, outputs checked against the fixture"}
     with open(os.path.join(root, "tests", "golden", "pok_g2_q32.json")) as f:
         d = json.load(f)
+    VK_WBITS = 20  # q = 32: 34 bases, 22-bit tables would exceed the 96 GiB budget
     vk, gt = vk_from_fixture(d)
     rows = []
     for p in d["proofs"]:
@@ -927,6 +931,7 @@ def main():
         "note": "valid proofs of tests/golden/pok_g2_q32.json (verdicts of every kind checked)"}
     with open(os.path.join(root, "tests", "golden", "verify_g2_q16.json")) as f:
         d = json.load(f)
+    VK_WBITS = 22
     vk, gt = vk_from_fixture(d)
     rnd = random.Random(3)
     rows = [rlc_sigg2(c, vk, gt, d["q"], rnd) for c in d["creds"] if c["kind"] == "valid"]
