@@ -14,7 +14,7 @@ echo "[final] smoke"
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
 echo "[final] bench"
 timeout -k 10 600 python bench.py --steps 10 --warmup 2 > "$OUT/bench.json" 2> "$OUT/bench.err"
-for m in verify-g1 rlc aggregate pok; do
+for m in verify-g1 rlc aggregate pok aggregate-g1 pok-g1; do
   echo "[final] bench $m"
   timeout -k 10 600 python bench.py --mode $m --steps 5 --warmup 1 > "$OUT/bench_$m.json" 2> "$OUT/bench_$m.err"
 done
