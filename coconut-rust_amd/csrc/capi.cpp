@@ -1230,16 +1230,26 @@ cc_status cc_aggregate_credential_batch_device(cc_ctx* c, size_t n, size_t len, 
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_lagrange(n, len, t, d_ids, c->lag.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    // the two MSMs share only the Lagrange coefficients: Signature::aggregate first on the caller's
+    // stream (its launch is sized to one round of wave slots, cck_msm_straus), Verkey::aggregate on the
+    // side stream behind it, filling the slots the Straus launch leaves and its tail
+    hipStream_t side = c->side ? c->side : st;
+    if (side != st) HIPCK(hipEventRecord(c->ev_fork, st));  // the coefficients are ready
     KCK(cck_msm_straus(sg, n, t, d_s2, len * sb, 0, sb, c->lag.as<uint32_t>(), 1, c->agg_scratch.as<uint32_t>(),
                        d_out_s2, st));
-    HIPCK(hipMemcpy2DAsync(d_out_s1, sb, d_s1, len * sb, sb, n, hipMemcpyDeviceToDevice, st));
-    if (c->timing) (void)hipEventRecord(c->ev[2], st);
+    if (side != st) HIPCK(hipStreamWaitEvent(side, c->ev_fork, 0));
     KCK(cck_vk_agg_fixed(oth_group(c->mode), n, len, t, (int)c->iss_q, d_ids, c->lag.as<uint32_t>(),
                          c->iss_ids.as<uint64_t>(), (int)c->iss_n, c->iss_table.as<uint32_t>(), c->iss_wbits,
-                         c->iss_inf.as<uint32_t>(), d_outX, d_outY, c->dev_err.as<uint32_t>(), st));
+                         c->iss_inf.as<uint32_t>(), d_outX, d_outY, c->dev_err.as<uint32_t>(), side));
+    HIPCK(hipMemcpy2DAsync(d_out_s1, sb, d_s1, len * sb, sb, n, hipMemcpyDeviceToDevice, st));
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
+    if (side != st) {
+        HIPCK(hipEventRecord(c->ev_join, side));
+        HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));
+    }
     if (c->timing) {
-        (void)hipEventRecord(c->ev[3], st);
-        collect_timing(c);
+        (void)hipEventRecord(c->ev[3], st);  // phases: Lagrange, Signature::aggregate (sharing the GPU), the
+        collect_timing(c);                   // rest of Verkey::aggregate after it
     }
     return CC_OK;
 }
