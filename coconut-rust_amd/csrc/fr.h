@@ -13,8 +13,6 @@ namespace cc {
 constexpr int NR = 8;
 #define CC_RR2 0xf3f29c6du, 0xc999e990u, 0x87925c23u, 0x2b6cedcbu, 0x7254398fu, 0x05d31496u, 0x9f59ff11u, 0x0748d9d9u
 #define CC_RONE 0xfffffffeu, 0x00000001u, 0x00034802u, 0x5884b7fau, 0xecbc4ff5u, 0x998c4fefu, 0xacc5056fu, 0x1824b159u
-__constant__ static const uint32_t kRm2[NR] = {0xffffffffu, 0xfffffffeu, 0xfffe5bfeu, 0x53bda402u,
-                                               0x09a1d805u, 0x3339d808u, 0x299d7d48u, 0x73eda753u};
 
 struct Fm {
     uint32_t v[NR];
@@ -90,13 +88,128 @@ DEV Fm fm_one() {
     return a;
 }
 
-DEV Fm fm_inv(const Fm& a) {
-    Fm acc = a;
-    for (int bit = 254 - 1; bit >= 0; bit--) {  // r - 2 has its top bit at 254
-        acc = fm_mul_v(acc, acc);
-        if ((kRm2[bit >> 5] >> (bit & 31)) & 1u) acc = fm_mul_v(acc, a);
+// ---------------------------------------------------------------- inversion mod r
+// Bernstein-Yang divsteps as field.h fp_inv_int, for the 255-bit r: 9 signed radix-2^30 limbs, batches of
+// 30 divsteps (field.h divsteps30) with the 2 x 2 matrix applied by signed 32 x 32 mads; r = 1 mod 2^30,
+// so the exact-division multiple of r is the low 30 bits of -(c + m) directly.  ~25 batches against the
+// ~384 Montgomery products of the Fermat ladder it replaces.
+constexpr int R30N = 9;
+struct R30 {
+    int32_t v[R30N];
+};
+DEV int32_t r30_limb(int i) {
+    constexpr int32_t L[R30N] = {0x1, 0x3ffffffc, 0x3fe5bfef, 0x2f6900bf, 0x21d80553,
+                                 0x27602026, 0x17d48333, 0x29d4ca67, 0x73ed};
+    return L[i];
+}
+DEV void r30_update_fg(R30& f, R30& g, const int32_t t[4]) {
+    int64_t cf = smad(t[1], g.v[0], smad(t[0], f.v[0], 0));
+    int64_t cg = smad(t[3], g.v[0], smad(t[2], f.v[0], 0));
+    cf >>= 30;
+    cg >>= 30;
+#pragma unroll
+    for (int i = 1; i < R30N; i++) {
+        cf = smad(t[1], g.v[i], smad(t[0], f.v[i], cf));
+        cg = smad(t[3], g.v[i], smad(t[2], f.v[i], cg));
+        f.v[i - 1] = (int32_t)cf & M30;
+        g.v[i - 1] = (int32_t)cg & M30;
+        cf >>= 30;
+        cg >>= 30;
     }
-    return acc;
+    f.v[R30N - 1] = (int32_t)cf;
+    g.v[R30N - 1] = (int32_t)cg;
+}
+// [d, e] <- (t [d, e] + r [md, me]) / 2^30, d and e kept in (-2r, r)
+DEV void r30_update_de(R30& d, R30& e, const int32_t t[4]) {
+    const int32_t sd = d.v[R30N - 1] >> 31, se = e.v[R30N - 1] >> 31;
+    int32_t md = (t[0] & sd) + (t[1] & se);
+    int32_t me = (t[2] & sd) + (t[3] & se);
+    int64_t cd = smad(t[1], e.v[0], smad(t[0], d.v[0], 0));
+    int64_t ce = smad(t[3], e.v[0], smad(t[2], d.v[0], 0));
+    md -= (int32_t)(((uint32_t)cd + (uint32_t)md) & (uint32_t)M30);  // r^-1 = 1 mod 2^30
+    me -= (int32_t)(((uint32_t)ce + (uint32_t)me) & (uint32_t)M30);
+    cd = smad(r30_limb(0), md, cd);
+    ce = smad(r30_limb(0), me, ce);
+    cd >>= 30;
+    ce >>= 30;
+#pragma unroll
+    for (int i = 1; i < R30N; i++) {
+        cd = smad(r30_limb(i), md, smad(t[1], e.v[i], smad(t[0], d.v[i], cd)));
+        ce = smad(r30_limb(i), me, smad(t[3], e.v[i], smad(t[2], d.v[i], ce)));
+        d.v[i - 1] = (int32_t)cd & M30;
+        e.v[i - 1] = (int32_t)ce & M30;
+        cd >>= 30;
+        ce >>= 30;
+    }
+    d.v[R30N - 1] = (int32_t)cd;
+    e.v[R30N - 1] = (int32_t)ce;
+}
+DEV void r30_carry(R30& a) {
+#pragma unroll
+    for (int i = 0; i < R30N - 1; i++) {
+        a.v[i + 1] += a.v[i] >> 30;
+        a.v[i] &= M30;
+    }
+}
+DEV void r30_add_kr(R30& a, int32_t k) {
+#pragma unroll
+    for (int i = 0; i < R30N; i++) a.v[i] += k * r30_limb(i);
+    r30_carry(a);
+}
+// a^-1 mod r as a plain integer (a < r; 0 -> 0)
+DEV void fr_inv_int(uint32_t out[NR], const uint32_t a[NR]) {
+    R30 d, e, f, g;
+#pragma unroll
+    for (int i = 0; i < R30N; i++) {
+        d.v[i] = 0;
+        e.v[i] = 0;
+        f.v[i] = r30_limb(i);
+        const int w = (30 * i) >> 5, sh = (30 * i) & 31;
+        const uint64_t pair = (uint64_t)a[w] | ((w + 1 < NR ? (uint64_t)a[w + 1] : 0ull) << 32);
+        g.v[i] = (int32_t)((uint32_t)(pair >> sh) & (uint32_t)M30);
+    }
+    e.v[0] = 1;
+    int32_t eta = -1;
+    for (int it = 0; it < 30; it++) {  // Bernstein-Yang bound for 255-bit inputs: < 740 divsteps
+        int32_t t[4];
+        eta = divsteps30(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+        r30_update_de(d, e, t);
+        r30_update_fg(f, g, t);
+        int32_t o = 0;
+#pragma unroll
+        for (int i = 0; i < R30N; i++) o |= g.v[i];
+        if (o == 0) break;
+    }
+    // f = +-1 (or r when a = 0, where d = 0): x = sign(f) d mod r, d in (-2r, r)
+    if (f.v[R30N - 1] < 0) {
+#pragma unroll
+        for (int i = 0; i < R30N; i++) d.v[i] = -d.v[i];
+        r30_carry(d);
+    }
+    r30_add_kr(d, d.v[R30N - 1] < 0 ? 1 : 0);
+    r30_add_kr(d, d.v[R30N - 1] < 0 ? 1 : 0);
+    R30 tt = d;
+    r30_add_kr(tt, -1);
+    if (tt.v[R30N - 1] >= 0) d = tt;
+#pragma unroll
+    for (int j = 0; j < NR; j++) {
+        const int i = (32 * j) / 30, sh = (32 * j) % 30;
+        uint64_t x = (uint64_t)(uint32_t)d.v[i] >> sh;
+        if (i + 1 < R30N) x |= (uint64_t)(uint32_t)d.v[i + 1] << (30 - sh);
+        if (i + 2 < R30N) x |= (uint64_t)(uint32_t)d.v[i + 2] << (60 - sh);
+        out[j] = (uint32_t)x;
+    }
+}
+
+// a^-1 in Montgomery form (a in Montgomery form): (a R)^-1 times R^3 R^-1 = a^-1 R; 0 -> 0
+DEV Fm fm_inv(const Fm& a) {
+    constexpr uint32_t R3[NR] = {0x439b73afu, 0xc62c1807u, 0x8cf06990u, 0x1b3e0d18u,
+                                 0xc7b5f418u, 0x73d13c71u, 0xc8db33e9u, 0x6e2a5bb9u};  // R^3 mod r
+    Fm x, r3;
+    fr_inv_int(x.v, a.v);
+#pragma unroll
+    for (int j = 0; j < NR; j++) r3.v[j] = R3[j];
+    return fm_mul_v(x, r3);
 }
 
 DEV Fm fm_to_canon(const Fm& a) {

@@ -150,6 +150,60 @@ def test_safegcd_inversion():
         assert (x == 0 and r == 0) or r * x % P == 1
 
 
+# ---- the same schedule mod r (fr.h fr_inv_int: 9 limbs, r = 1 mod 2^30 so r^-1 mod 2^30 = 1)
+RN = 9
+R30 = [(B.R >> (30 * i)) & M30 for i in range(RN)]
+
+
+def _apply_r(a, b, t0, t1, md=None):
+    c = t0 * a[0] + t1 * b[0] + (R30[0] * md if md is not None else 0)
+    assert c % (1 << 30) == 0
+    c >>= 30
+    out = []
+    for i in range(1, RN):
+        c += t0 * a[i] + t1 * b[i] + (R30[i] * md if md is not None else 0)
+        assert -(1 << 63) <= c < (1 << 63)
+        out.append(_i32(c) & M30)
+        c >>= 30
+    return out + [_i32(c)]
+
+
+def _md_r(t0, t1, d, e):
+    m = _i32((t0 if d[-1] < 0 else 0) + (t1 if e[-1] < 0 else 0))
+    cd = t0 * d[0] + t1 * e[0]
+    return _i32(m - (_u32(_u32(cd) + _u32(m)) & M30))
+
+
+def safegcd_inv_r(x):
+    val = lambda a: sum(a[i] << (30 * i) for i in range(RN))  # noqa: E731
+    d, e, f, g = [0] * RN, [1] + [0] * (RN - 1), R30[:], [(x >> (30 * i)) & M30 for i in range(RN)]
+    eta, batches = -1, 0
+    for _ in range(30):
+        batches += 1
+        eta, t = _divsteps(eta, f[0], g[0])
+        md, me = _md_r(t[0], t[1], d, e), _md_r(t[2], t[3], d, e)
+        d, e = _apply_r(d, e, t[0], t[1], md), _apply_r(d, e, t[2], t[3], me)
+        f, g = _apply_r(f, g, t[0], t[1]), _apply_r(f, g, t[2], t[3])
+        assert -2 * B.R < val(d) < B.R and -2 * B.R < val(e) < B.R
+        if not any(g):
+            break
+    assert not any(g), "the loop bound of fr_inv_int must suffice"
+    D = -val(d) if val(f) < 0 else val(d)
+    return D % B.R, batches
+
+
+def test_safegcd_inversion_mod_r():
+    """fr.h fr_inv_int (the Lagrange kernel's inversion) restated: exact inverses mod r, intermediates in
+    the signed 64-bit accumulators, d and e in (-2r, r), and g = 0 within the kernel's 30 batches."""
+    rnd = random.Random(12)
+    worst = 0
+    for x in [0, 1, 2, B.R - 1, B.R - 2, (1 << 254) + 5] + [rnd.randrange(B.R) for _ in range(300)]:
+        r, nb = safegcd_inv_r(x)
+        worst = max(worst, nb)
+        assert (x == 0 and r == 0) or r * x % B.R == 1
+    assert worst <= 30
+
+
 # ---- RLC signed-digit coefficient (fr.h rlc_delta_signed) restated word by word
 R_ORDER = B.R
 
