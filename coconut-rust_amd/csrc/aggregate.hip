@@ -887,7 +887,8 @@ extern "C" {
 
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st) {
     if (!n || !t) return 0;
-    constexpr int lt = 4;  // tasks per lane: 3.96 / 3.62 / 4.10 ms for 2 / 4 / 8 at config 4
+    constexpr int lt = 2;  // tasks per lane: with the divstep inversion 1.82 / 2.01 ms for 2 / 4 at config 4
+                           // (the Fermat ladder measured 3.96 / 3.62 / 4.10 for 2 / 4 / 8)
     // ids of the credentials one block's 64 x lt tasks touch: at most 64 lt / t + 2 rows of t; past
     // 64 KiB (t > 3,968) the ids are read from global memory
     const size_t lds = (64 * (size_t)lt + 2 * t) * 8;
