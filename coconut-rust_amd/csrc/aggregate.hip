@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256) void k_vk_agg_fixed(size_t n, size_t len, size
         acc = lz::jg_to(a);
     } else {
         jac_set_inf(acc);
-        lane_terms(acc, [&](Jac<F>& x, const uint32_t* kk, int b) { ft_add<F>(x, kk, table, wbits, b, 0, ft_nwin(wbits)); });
+        lane_terms(acc, [&](Jac<F>& x, const uint32_t* kk, int b) { ft_add<F>(x, kk, table, wbits, b, 0, ft_nwin(wbits), true); });
     }
     lane_group_sum<F, L>(acc);
 #pragma unroll
@@ -696,8 +696,7 @@ __global__ __launch_bounds__(256, 2) void k_vk_agg_fixed_g2pl(size_t n, size_t l
     if (task >= n * (size_t)(q + 1)) return;  // uniform over the lane group
     const size_t cred = task / (q + 1);
     const int j = (int)(task % (q + 1));
-    Jac<pl::Fp2> acc;
-    jac_set_inf(acc);
+    lz::JL la = lz::jl_inf();  // the pair's share on the lazy pair-lane field
     int bad = 0;
 #pragma unroll 1
     for (size_t k = pair; k < t; k += NPR) {  // pair-uniform
@@ -713,8 +712,9 @@ __global__ __launch_bounds__(256, 2) void k_vk_agg_fixed_g2pl(size_t n, size_t l
         }
         const int b = lo * (q + 1) + j;
         if (binf[b]) continue;
-        pl::ft_add_g2(acc, l + (cred * t + k) * 8, table, wbits, b, 0, ft_nwin(wbits));
+        pl::ft_add_g2_lz(la, l + (cred * t + k) * 8, table, wbits, b, 0, ft_nwin(wbits));
     }
+    Jac<pl::Fp2> acc = pl::jl_to_pl(la);
     pl::pair_group_sum<L>(acc);
 #pragma unroll
     for (int o = 1; o < L; o <<= 1) bad |= __shfl_xor(bad, o, L);
@@ -789,7 +789,8 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_g1pl(size_t n, int q, int r
         const uint8_t* rp = resp + i * (size_t)(q - r + 1) * 48;
         fr_from_be48(k, rp);
         const int nwin = ft_nwin(wbits);
-        if (!binf[q]) pl::ft_add_g2(acc, k.v, table, wbits, q, 0, nwin);  // table base q = g~
+        lz::JL la = lz::jl_inf();  // the table terms on the lazy pair-lane field
+        if (!binf[q]) pl::ft_add_g2_lz(la, k.v, table, wbits, q, 0, nwin);  // table base q = g~
         int slot = 1;
         for (int hh = 0; hh < q; hh++) {
             bool revealed = false;
@@ -797,8 +798,9 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_g1pl(size_t n, int q, int r
             if (revealed) continue;
             fr_from_be48(k, rp + (size_t)slot * 48);
             slot++;
-            if (!binf[hh]) pl::ft_add_g2(acc, k.v, table, wbits, hh, 0, nwin);
+            if (!binf[hh]) pl::ft_add_g2_lz(la, k.v, table, wbits, hh, 0, nwin);
         }
+        acc = pl::jl_to_pl(la);
         fr_from_be48(k, chal + i * 48);
         if (Jok) {
             constexpr int JW = sizeof(Jac<G2>) / 4;
@@ -847,12 +849,14 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_g1pl(size_t n, int q, int r
         jac_from_aff(jp, x);
     }
     if (Jok) jac_add_aff(jp, jp, Ja);
+    lz::JL lj = pl::jl_from_pl(jp);
     for (int z = 0; z < r; z++) {
         Fr m;
         fr_from_be48(m, rev_msgs + ((size_t)i * r + z) * 48);
         const int hh = (int)rev_idx[z];
-        if (!binf[hh]) pl::ft_add_g2(jp, m.v, table, wbits, hh, 0, ft_nwin(wbits));
+        if (!binf[hh]) pl::ft_add_g2_lz(lj, m.v, table, wbits, hh, 0, ft_nwin(wbits));
     }
+    jp = pl::jl_to_pl(lj);
     Aff<G2> a;
     if (!jac_to_aff(a, jp)) fl |= 4u;
     pl::st_f2(S, S_Q1, i, a.x);

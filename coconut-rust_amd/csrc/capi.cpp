@@ -18,7 +18,7 @@
 extern "C" {
 int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_out, uint32_t* d_inf, hipStream_t st);
 int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
-                    uint32_t* d_table, hipStream_t st);
+                    uint32_t* d_table, int lazy_g2, hipStream_t st);
 int cck_gtilde_lines(const uint32_t* d_gtilde_aff, uint32_t* d_lines, hipStream_t st);
 int cck_subgroup(int group, size_t n, const uint8_t* d_bytes, uint8_t* d_status, hipStream_t st);
 int cck_hash_to_curve(int group, size_t n, const uint8_t* d_data, const uint64_t* d_offsets, uint8_t* d_out,
@@ -402,7 +402,7 @@ static cc_status rebuild_tables(cc_ctx* c) {
     DevBuf pw;
     if (pw.ensure((size_t)nb * tab_nwin(c->wbits) * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
     KCK(cck_build_table(og, nb, c->wbits, c->vk_aff.as<uint32_t>() + aw, c->table_inf.as<uint32_t>(), pw.as<uint32_t>(),
-                        c->table.as<uint32_t>(), c->stream));
+                        c->table.as<uint32_t>(), 1, c->stream));
     HIPCK(hipStreamSynchronize(c->stream));
     pw.release();
     return CC_OK;
@@ -779,7 +779,8 @@ cc_status cc_fixed_base_mul(cc_ctx* c, int group, const uint8_t* base, size_t n,
     if (s) return s;
     uint32_t binf = 0;
     HIPCK(hipMemcpy(&binf, inf.p, 4, hipMemcpyDeviceToHost));
-    KCK(cck_build_table(group, 1, 8, aff.as<uint32_t>(), inf.as<uint32_t>(), pw.as<uint32_t>(), table.as<uint32_t>(), st));
+    KCK(cck_build_table(group, 1, 8, aff.as<uint32_t>(), inf.as<uint32_t>(), pw.as<uint32_t>(), table.as<uint32_t>(), 0,
+                        st));
     HIPCK(hipMemcpyAsync(ks.p, scalars, n * 48, hipMemcpyHostToDevice, st));
     KCK(cck_fixed_mul(group, n, ks.as<uint8_t>(), table.as<uint32_t>(), binf, o.as<uint8_t>(), st));
     HIPCK(hipMemcpyAsync(out, o.p, n * eb, hipMemcpyDeviceToHost, st));
@@ -1157,7 +1158,7 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
     DevBuf pw;
     if (pw.ensure(nb * tab_nwin(wb) * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
     KCK(cck_build_table(og, (int)nb, wb, c->iss_aff.as<uint32_t>(), c->iss_inf.as<uint32_t>(), pw.as<uint32_t>(),
-                        c->iss_table.as<uint32_t>(), c->stream));
+                        c->iss_table.as<uint32_t>(), 1, c->stream));
     HIPCK(hipStreamSynchronize(c->stream));
     pw.release();
     c->iss_n = n_iss;

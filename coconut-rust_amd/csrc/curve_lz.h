@@ -67,6 +67,26 @@ DEV JL jl_add_aff(const JL& p, const AL& q) {
     return {reduce(X3), reduce(Y3), reduce(Z3)};
 }
 
+// madd-2007-bl with a canonical affine point (a table entry in the lazy Montgomery form, fixed.h)
+DEV JL jl_add_aff_c(const JL& p, const F2<AN, BC>& qx, const F2<AN, BC>& qy) {
+    if (jl_is_inf(p)) return {reduce(qx), reduce(qy), r_one()};
+    const auto z1z1 = sqrr(p.z);
+    const auto u2 = mulr(qx, z1z1);
+    const auto s2 = mulr(mulr(qy, p.z), z1z1);
+    const F2R h = reduce(sub(u2, p.x));
+    const F2R r0 = reduce(sub(s2, p.y));
+    if (rz_is_zero(h)) return rz_is_zero(r0) ? jl_dbl(p) : jl_inf();
+    const auto rr = dbl(r0);
+    const auto hh = sqrr(h);
+    const auto i = smul<4>(hh);
+    const auto j = mulr(h, i);
+    const auto v = mulr(p.x, i);
+    const auto X3 = sub(sub(sqrr(rr), j), dbl(v));
+    const auto Y3 = sub(mulr(rr, sub(v, X3)), dbl(mulr(p.y, j)));
+    const auto Z3 = sub(sub(sqrr(add(p.z, h)), z1z1), hh);
+    return {reduce(X3), reduce(Y3), reduce(Z3)};
+}
+
 // add-2007-bl: general Jacobian addition with the exceptional cases
 DEV JL jl_add(const JL& p, const JL& q) {
     if (jl_is_inf(p)) return q;

@@ -93,10 +93,11 @@ DEV bool miller_t_in_subgroup(const G2Proj& T, const Aff<Fp2>& q) {
     return !f2_is_zero(T.z) && f2_eq(a, T.x) && f2_eq(b, T.y);
 }
 
-// fixed.h ft_add on the pair-lane Fp2: acc += (k over windows [w0, w1)) * B_j from a G2 window table
-// (AoS entries x.a | x.b | y.a | y.b, 12 words each): each lane loads its own halves.
-DEV void ft_add_g2(Jac<Fp2>& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j, int w0,
-                   int w1) {
+// fixed.h ft_add on the pair-lane Fp2 over a G2 window table in the lazy Montgomery form (AoS entries
+// x.a | x.b | y.a | y.b, 12 words each; the verkey and issuer tables, k_table_fill): each lane loads its
+// own halves, the sum runs on the lazy pair-lane field (curve_lz.h)
+DEV void ft_add_g2_lz(lz::JL& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j,
+                      int w0, int w1) {
     constexpr int EW = sizeof(cc::Aff<cc::Fp2>) / 4;
     const int h = (int)half_id();
     const size_t went = ft_went(wbits);
@@ -106,19 +107,23 @@ DEV void ft_add_g2(Jac<Fp2>& acc, const uint32_t k[8], const uint32_t* __restric
         const uint32_t d = ft_digit(k, w, wbits);  // pair-uniform: both lanes hold the same scalar
         if (!d) continue;
         const uint32_t* e = tj + ((size_t)w * went + d - 1) * EW;
-        Aff<Fp2> a;
+        Fp x, y;
         uint32_t o = 0;
 #pragma unroll
         for (int c = 0; c < NL; c++) {
-            a.x.c.v[c] = e[NL * h + c];
-            a.y.c.v[c] = e[2 * NL + NL * h + c];
-            o |= a.x.c.v[c] | a.y.c.v[c];
+            x.v[c] = e[NL * h + c];
+            y.v[c] = e[2 * NL + NL * h + c];
+            o |= x.v[c] | y.v[c];
         }
         if (pair_all(o == 0)) continue;  // (0, 0): an identity entry
-        jac_add_aff(acc, acc, a);
+        acc = lz::jl_add_aff_c(acc, lz::F2<lz::AN, lz::BC>{lz::from_fp(x)}, lz::F2<lz::AN, lz::BC>{lz::from_fp(y)});
     }
 }
-
+// storage-form (canonical, R = 2^406) pair-lane Jacobian points <-> the lazy field's (curve_lz.h)
+DEV lz::JL jl_from_pl(const Jac<Fp2>& a) {
+    return {lz::reduce(lz::in_r2(a.x)), lz::reduce(lz::in_r2(a.y)), lz::reduce(lz::in_r2(a.z))};
+}
+DEV Jac<Fp2> jl_to_pl(const lz::JL& a) { return {lz::out_r2(a.x), lz::out_r2(a.y), lz::out_r2(a.z)}; }
 // curve.h lane_group_sum for lane-pair points: the sum over the L / 2 pairs of L consecutive lanes
 // (L a power of two <= 64), butterfly at lane distances L/2 .. 2 so halves stay with halves; every
 // pair ends with the same sum.

@@ -73,10 +73,25 @@ DEV void ft_add_lz(lz::JG& acc, const uint32_t k[8], const uint32_t* __restrict_
     }
 }
 
-// acc += (k restricted to windows [w0, w1)) * B_j
+// a G2 entry of a lazy-form table back to the storage form (one-lane consumers of the verkey tables:
+// the RLC fold's fixed points in SigG1 mode): x R' -> x R, times 2^14 = R^2 / R' (fp_mul by 2^420 mod p)
+DEV void g2_entry_from_lazy_form(Aff<Fp2>& e) {
+    constexpr uint32_t C[NL] = {0x8e9f9aecu, 0x977080eau, 0x16d8fe47u, 0x26e7d667u, 0xfb088639u, 0xaca5f496u,
+                                0x7416d1f5u, 0xbca6d4cfu, 0xb5b6168du, 0xdaab0ee4u, 0x403d5566u, 0x14820974u};
+    Fp c;
+#pragma unroll
+    for (int i = 0; i < NL; i++) c.v[i] = C[i];
+    fp_mul(e.x.a, e.x.a, c);
+    fp_mul(e.x.b, e.x.b, c);
+    fp_mul(e.y.a, e.y.a, c);
+    fp_mul(e.y.b, e.y.b, c);
+}
+
+// acc += (k restricted to windows [w0, w1)) * B_j; lazy_g2: a G2 table in the lazy form (the verkey and
+// issuer tables; cc_fixed_base_mul's tables are in the storage form)
 template <class F>
 DEV void ft_add(Jac<F>& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j, int w0,
-                int w1) {
+                int w1, bool lazy_g2 = false) {
     if constexpr (std::is_same<F, Fp>::value) {  // G1: on the lazy field, storage form at the boundary
         lz::JG a = lz::jg_from(acc);
         ft_add_lz(a, k, table, wbits, j, w0, w1);
@@ -92,6 +107,8 @@ DEV void ft_add(Jac<F>& acc, const uint32_t k[8], const uint32_t* __restrict__ t
             Aff<F> e;
             ft_load<F>(e, tj + ((size_t)w * went + d - 1) * EW);
             if (ft_is_empty(e)) continue;
+            if constexpr (std::is_same<F, Fp2>::value)
+                if (lazy_g2) g2_entry_from_lazy_form(e);
             jac_add_aff(acc, acc, e);
         }
     }

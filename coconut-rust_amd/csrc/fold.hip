@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void k_fold_fixed(int q, const uint32_t* __res
     s[w >> 2] = (uint32_t)d << (8 * (w & 3));
     Jac<G> acc;
     jac_set_inf(acc);
-    if (!binf[q]) ft_add<G>(acc, s, table, wbits, q, 0, ft_nwin(wbits));
+    if (!binf[q]) ft_add<G>(acc, s, table, wbits, q, 0, ft_nwin(wbits), true);  // the verkey table: lazy form
     Aff<G> a;
     const bool fin = jac_to_aff(a, acc);
     fixed_inf[b] = fin ? 0 : 1;

@@ -141,6 +141,14 @@ DEV void g1_to_lazy_form(Fp& v) {
     for (int j = 0; j < NL; j++) c.v[j] = C[j];
     fp_mul(v, v, c);
 }
+// table entries: G1 always in the lazy form; G2 when the table's consumers are the pair-lane lazy sums
+// (verkey and issuer tables; cc_fixed_base_mul's one-lane tables stay in the storage form)
+DEV void to_lazy_form(Fp& v, int) { g1_to_lazy_form(v); }
+DEV void to_lazy_form(Fp2& v, int lazy_g2) {
+    if (!lazy_g2) return;
+    g1_to_lazy_form(v.a);
+    g1_to_lazy_form(v.b);
+}
 
 // T2: entries d * 2^(wbits w) * B_j for a run of FILL_RUN consecutive digits per thread: the first by
 // double-and-add, the rest by one mixed addition each, then ONE inversion for the whole run
@@ -149,7 +157,7 @@ DEV void g1_to_lazy_form(Fp& v) {
 constexpr int FILL_RUN = 32;
 template <class F>
 __global__ __launch_bounds__(64) void k_table_fill(int nbases, int wbits, const uint32_t* __restrict__ pw,
-                                                   uint32_t* __restrict__ table) {
+                                                   uint32_t* __restrict__ table, int lazy_g2) {
     using T = FT<F>;
     constexpr int EW = sizeof(Aff<F>) / 4, PW = sizeof(F) / 4;
     const int nwin = ft_nwin(wbits);
@@ -207,12 +215,12 @@ __global__ __launch_bounds__(64) void k_table_fill(int nbases, int wbits, const 
         uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
         for (int c = 0; c < PW; c++) vw[c] = o[c];
         T::mul(v, v, zi2);
-        if constexpr (std::is_same<F, Fp>::value) g1_to_lazy_form(v);
+        to_lazy_form(v, lazy_g2);
         for (int c = 0; c < PW; c++) o[c] = vw[c];
         T::mul(zi2, zi2, zi);
         for (int c = 0; c < PW; c++) vw[c] = o[PW + c];
         T::mul(v, v, zi2);
-        if constexpr (std::is_same<F, Fp>::value) g1_to_lazy_form(v);
+        to_lazy_form(v, lazy_g2);
         for (int c = 0; c < PW; c++) o[PW + c] = vw[c];
     }
 }
@@ -236,7 +244,7 @@ DEV void msm_fixed_terms(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t
             if (binf[j]) continue;
             Fr m;
             fr_from_be48(m, msgs + (size_t)j * 48);
-            ft_add<F>(acc, m.v, table, wbits, j, w0, w1);
+            ft_add<F>(acc, m.v, table, wbits, j, w0, w1, true);  // the verkey table
         }
     }
 }
@@ -507,12 +515,14 @@ __global__ __launch_bounds__(256, 2) void k_prep_sigg1_pair(size_t n, int q, con
         }
         jac_from_aff(acc, x);
     }
+    lz::JL la = pl::jl_from_pl(acc);  // the sum on the lazy pair-lane field
     for (int j = 0; j < q; j++) {
         if (binf_fixed[j]) continue;  // uniform across the batch (shared verkey)
         Fr m;
         fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
-        pl::ft_add_g2(acc, m.v, table, wbits, j, 0, ft_nwin(wbits));
+        pl::ft_add_g2_lz(la, m.v, table, wbits, j, 0, ft_nwin(wbits));
     }
+    acc = pl::jl_to_pl(la);
     Aff<pl::Fp2> a;
     if (!jac_to_aff(a, acc)) fl |= 4u;
     pl::st_f2(S, S_Q1, i, a.x);
@@ -578,16 +588,17 @@ int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_o
 
 // table: nbases * ft_base_words(wbits) words (fixed.h); pw scratch: nbases * ft_nwin(wbits) Jacobian points
 int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
-                    uint32_t* d_table, hipStream_t st) {
+                    uint32_t* d_table, int lazy_g2, hipStream_t st) {
     if (!nbases) return 0;
     if (wbits < 8 || wbits > 22) return -1;
     size_t t1 = (size_t)nbases * ft_nwin(wbits), t2 = t1 * ((ft_went(wbits) + FILL_RUN - 1) / FILL_RUN);
     if (group == 1) {
         hipLaunchKernelGGL(k_table_pow2<Fp>, dim3(nblocks(t1, 64)), dim3(64), 0, st, nbases, wbits, d_bases, d_inf, d_pw);
-        hipLaunchKernelGGL(k_table_fill<Fp>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, wbits, d_pw, d_table);
+        hipLaunchKernelGGL(k_table_fill<Fp>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, wbits, d_pw, d_table, 1);
     } else {
         hipLaunchKernelGGL(k_table_pow2<Fp2>, dim3(nblocks(t1, 64)), dim3(64), 0, st, nbases, wbits, d_bases, d_inf, d_pw);
-        hipLaunchKernelGGL(k_table_fill<Fp2>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, wbits, d_pw, d_table);
+        hipLaunchKernelGGL(k_table_fill<Fp2>, dim3(nblocks(t2, 64)), dim3(64), 0, st, nbases, wbits, d_pw, d_table,
+                           lazy_g2);
     }
     CC_CHECK(hipGetLastError());
     return 0;

@@ -192,18 +192,18 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg1(size_t n, int q, uint6
     uint32_t kk[NR], d[NR], w4[4];
     for (int k = 0; k < 8; k++) kk[k] = key[k];
     rlc_delta_signed(d, w4, kk, base_index + i);
-    Jac<pl::Fp2> acc;
-    jac_set_inf(acc);
+    lz::JL la = lz::jl_inf();  // the sum on the lazy pair-lane field (curve_pl.h ft_add_g2_lz)
     const int nwin = ft_nwin(wbits);
-    if (!binf[q + 1]) pl::ft_add_g2(acc, d, table, wbits, q + 1, 0, nwin);
+    if (!binf[q + 1]) pl::ft_add_g2_lz(la, d, table, wbits, q + 1, 0, nwin);
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
         fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
         uint32_t dm[NR];
         fr_mul_canon(dm, d, m.v);
-        pl::ft_add_g2(acc, dm, table, wbits, j, 0, nwin);
+        pl::ft_add_g2_lz(la, dm, table, wbits, j, 0, nwin);
     }
+    const Jac<pl::Fp2> acc = pl::jl_to_pl(la);
     Aff<pl::Fp2> a2;
     const bool fin = jac_to_aff(a2, acc);
     pl::st_f2(S, S_Q1, i, a2.x);
