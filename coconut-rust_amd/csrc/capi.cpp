@@ -40,13 +40,14 @@ int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* 
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
-int cck_miller_lz_g2(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+int cck_miller_lz_g2(int np, int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
-int cck_miller_lz_g1(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+int cck_miller_lz_g1(int np, int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
 size_t cck_fold_words(int mode, size_t n);
+int cck_fold_pseudo();
 int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok,
              int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
              uint32_t* d_flags2, hipStream_t st);
@@ -147,10 +148,10 @@ struct cc_ctx {
     // RLC batch mode: ChaCha20 key, identity flag word, partial / gathered partials, verdict
     DevBuf rlc_key, rlc_any, rlc_part, rlc_flag, rlc_accept;
     DevBuf fin_f, fin_scratch;  // cc_rlc_finish_device's own buffers
-    // RLC g~-side fold (fold.hip): fold points, delta digits, sort/partials workspace, the 1,024
-    // pseudo-credentials' prep SoA (bucket sums + the fixed points P_w,d = (256^w d) g~) and flags
+    // RLC g~-side fold (fold.hip): fold points, delta digits, sort/partials/bucket workspace, the 16
+    // pseudo-credentials' prep SoA (window sums + the fixed points P_w = (256^w) g~) and flags
     DevBuf rlc_pts, rlc_dig, rlc_work, rlc_prep2, rlc_finf, rlc_flags2;
-    bool rlc_fixed_ok = false;  // P_w,d in rlc_prep2 match the current tables
+    bool rlc_fixed_ok = false;  // P_w in rlc_prep2 match the current tables
     DevBuf pok_idx;  // revealed indices of the last PoK batch
     // issuer table (cc_set_issuers): sorted ids, decoded verkeys, per-base 8-bit window tables
     size_t iss_n = 0, iss_q = 0;
@@ -166,10 +167,13 @@ struct cc_ctx {
     float last_ms[3] = {0, 0, 0};
     // orders a caller-supplied stream against the context stream (StreamOrder below)
     hipEvent_t ev_order = nullptr;
-    // RLC fold side stream: the fold and its pseudo-credentials' Miller launch run concurrently with
-    // the credentials' Miller launch (ev_fork after prep, ev_join after the pseudo Miller)
+    // side stream (high priority): Verkey::aggregate beside Signature::aggregate (ev_fork / ev_join)
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // RLC partial: the fold's window pairs' Miller launch (one wave, ~6 ms of latency) on one CU of
+    // its own (cu_one) while the delta MSM runs on the others (cu_rest); ev_msm after the MSM
+    hipStream_t cu_one = nullptr, cu_rest = nullptr;
+    hipEvent_t ev_msm = nullptr;
     // device set (cc_ctx_create_multi): one single-device context per GPU and one RCCL communicator
     // per GPU (ncclCommInitAll, this process drives every device); empty for a single-device context
     std::vector<cc_ctx*> peers;
@@ -200,21 +204,26 @@ struct StreamOrder {
 };
 
 // mode 0 (SigG2): d_const = g~ affine G1 (24 words); mode 1 (SigG1): g~ Miller lines (68 x 72 words).
-// np = 1: pair 0 only (RLC credentials; their second pairs are folded, fold.hip).  Pairing kernels
-// run one credential per lane pair (tower_pl.h).  Miller values go to SoA elements [foff, foff + n)
-// of stride fstride (default: n, 0).
+// Pairing kernels run one credential per lane pair (tower_pl.h).  Miller values go to SoA elements
+// [foff, foff + n) of stride fstride (default: n, 0).
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
-                      uint32_t* d_f, hipStream_t st, int np = 2, size_t fstride = 0, size_t foff = 0,
-                      uint32_t* d_qcheck = nullptr) {
-    if (!fstride) fstride = n;
-    return mode == 0 ? cck_miller_lz_g2(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, d_qcheck, st)
-                     : cck_miller_lz_g1(0, np, n, d_prep, d_flags, d_const, d_f, fstride, foff, nullptr, st);
+                      uint32_t* d_f, hipStream_t st) {
+    return mode == 0 ? cck_miller_lz_g2(2, 0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st)
+                     : cck_miller_lz_g1(2, 0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st);
+}
+// the RLC credentials: pair 0 only (their second pairs are folded, fold.hip), two credentials per
+// lane pair through the shared-squaring loop: (n + 1) / 2 Miller values, each the product of two
+// credentials' (the RLC multiplies them all), to SoA elements [0, (n + 1) / 2) of stride fstride
+static int cck_miller_twin(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
+                           size_t fstride, uint32_t* d_qcheck, hipStream_t st) {
+    return mode == 0 ? cck_miller_lz_g2(1, 1, n, d_prep, d_flags, nullptr, d_f, fstride, 0, d_qcheck, st)
+                     : cck_miller_lz_g1(1, 1, n, d_prep, d_flags, nullptr, d_f, fstride, 0, nullptr, st);
 }
 // the RLC fold's pseudo-credentials: one (Q, P) pair per lane pair, Q affine G2 and P in evaluation
 // form, both per lane (either group mode: the SigG2 instantiation reads exactly that)
 static int cck_miller_pairs(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
                             size_t fstride, size_t foff, hipStream_t st) {
-    return cck_miller_lz_g2(0, 1, n, d_prep, d_flags, nullptr, d_f, fstride, foff, nullptr, st);
+    return cck_miller_lz_g2(1, 0, n, d_prep, d_flags, nullptr, d_f, fstride, foff, nullptr, st);
 }
 
 static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }
@@ -269,12 +278,22 @@ cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
     (void)hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->ev_msm, hipEventDisableTiming);
     {
-        // high priority: the pseudo-credential Miller launch (64 waves) must get its slots before the
-        // credentials' launch fills the chip (a Miller wave holds its slot for the whole loop)
+        // high priority: a launch on the side stream gets its wave slots before a full launch on the
+        // context stream fills the chip
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
         if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess) c->side = nullptr;
+        // CU-masked pair for the RLC partial: CU 0 alone, and every other CU
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 1) {
+            const uint32_t words = (uint32_t)((ncu + 31) / 32);
+            std::vector<uint32_t> one(words, 0u), rest(words, 0u);
+            for (int k = 0; k < ncu; k++) (k ? rest : one)[k / 32] |= 1u << (k % 32);
+            if (hipExtStreamCreateWithCUMask(&c->cu_one, words, one.data()) != hipSuccess) c->cu_one = nullptr;
+            if (hipExtStreamCreateWithCUMask(&c->cu_rest, words, rest.data()) != hipSuccess) c->cu_rest = nullptr;
+        }
     }
     *out = c;
     return CC_OK;
@@ -305,7 +324,10 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_msm) (void)hipEventDestroy(c->ev_msm);
     if (c->side) (void)hipStreamDestroy(c->side);
+    if (c->cu_one) (void)hipStreamDestroy(c->cu_one);
+    if (c->cu_rest) (void)hipStreamDestroy(c->cu_rest);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return CC_OK;
@@ -607,8 +629,9 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     }
     cc_status s = ensure_work(c, n);
     if (s) return s;
-    constexpr size_t NPS = 2048;  // fold pseudo-credentials (one per bucket, one pair each)
-    const size_t N = n + NPS;     // Miller values: n credentials, then the pseudo-credentials
+    const size_t NPS = (size_t)cck_fold_pseudo();  // fold pseudo-credentials (one per window, one pair each)
+    const size_t M = (n + 1) / 2;  // the credentials' Miller values (two credentials each)
+    const size_t N = M + NPS;      // Miller values: the credentials', then the pseudo-credentials'
     if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4) || c->fbuf.ensure(N * 144 * 4) ||
         c->scratch.ensure(((N + 1) / 2) * 144 * 4 + n * 12 * 4 * 72) || c->rlc_pts.ensure(n * 48 * 4) ||
         c->rlc_dig.ensure(16 * n) || c->rlc_work.ensure(cck_fold_words(c->mode, n) * 4) ||
@@ -619,45 +642,50 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     HIPCK(hipMemcpyAsync(c->rlc_key.p, c->rlc_key_host, 32, hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
-    auto prep_part = [&](int part) {
+    auto prep_part = [&](int part, hipStream_t s) {
         return cck_prep_rlc(c->mode, part, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
                             c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
                             c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), c->rlc_pts.as<uint32_t>(),
-                            c->rlc_dig.as<int8_t>(), st);
+                            c->rlc_dig.as<int8_t>(), s);
     };
-    KCK(prep_part(0));  // decode, subgroup checks, the fold's inputs
+    KCK(prep_part(0, st));  // decode, subgroup checks, the fold's inputs
     if (!c->vk_subgroup) {
         // a verkey / g~ point outside the subgroup: the linear-combination argument does not hold,
         // so the batch is never accepted here and the caller verifies per credential (exact)
         static const uint32_t one = 1;
         HIPCK(hipMemcpyAsync(c->rlc_any.p, &one, 4, hipMemcpyHostToDevice, st));
     }
-    // The second pairs become 2,048 bucket pairs (fold.hip).  The fold's short kernels run alone
-    // (behind a full launch each would wait milliseconds for a free slot); the buckets' Miller launch
-    // (64 waves, latency bound alone) then runs on the high-priority side stream under the delta MSM
-    // and pair 0 of every credential on st.  Both Miller launches write disjoint ranges of fbuf
-    // (stride N).
+    // The second pairs become 16 window pairs (fold.hip).  The fold's short kernels run alone
+    // (behind a full launch each would wait milliseconds for a free slot).  Then the windows' Miller
+    // launch (one wave: ~6 ms of latency, about the delta MSM's time) runs on CU 0 alone while the
+    // delta MSM runs on the other CUs, and pair 0 of every credential (two per lane pair: 2,048
+    // waves, exactly the chip's wave slots) starts once both are done — a wave still holding a slot
+    // would push one of its waves into a second round.  Both Miller launches write disjoint ranges
+    // of fbuf (stride N).
     KCK(cck_fold(c->mode, n, c->rlc_dig.as<int8_t>(), c->rlc_pts.as<uint32_t>(), c->rlc_work.as<uint32_t>(),
                  c->rlc_fixed_ok ? 1 : 0, (int)q, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(),
                  c->rlc_prep2.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_flags2.as<uint32_t>(), st));
     c->rlc_fixed_ok = true;
-    hipStream_t side = c->side ? c->side : st;
-    if (side != st) {
+    const bool split = c->cu_one && c->cu_rest;
+    hipStream_t s_one = split ? c->cu_one : st, s_rest = split ? c->cu_rest : st;
+    if (split) {
         HIPCK(hipEventRecord(c->ev_fork, st));
-        HIPCK(hipStreamWaitEvent(side, c->ev_fork, 0));
+        HIPCK(hipStreamWaitEvent(s_one, c->ev_fork, 0));
+        HIPCK(hipStreamWaitEvent(s_rest, c->ev_fork, 0));
     }
-    KCK(cck_miller_pairs(NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(), c->fbuf.as<uint32_t>(), N, n,
-                         side));
-    KCK(prep_part(1));  // delta X~ + sum (delta m_j) Y~_j
-    if (c->timing) (void)hipEventRecord(c->ev[1], st);
-    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
-    // SigG2: sigma_1's subgroup test comes from this loop's T (a failure raises rlc_any: fallback)
-    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st, 1, N,
-                   0, c->mode == 0 ? c->rlc_any.as<uint32_t>() : nullptr));
-    if (side != st) {
-        HIPCK(hipEventRecord(c->ev_join, side));
+    KCK(cck_miller_pairs(NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(), c->fbuf.as<uint32_t>(), N, M,
+                         s_one));
+    KCK(prep_part(1, s_rest));  // delta X~ + sum (delta m_j) Y~_j
+    if (split) {
+        HIPCK(hipEventRecord(c->ev_msm, s_rest));
+        HIPCK(hipEventRecord(c->ev_join, s_one));
+        HIPCK(hipStreamWaitEvent(st, c->ev_msm, 0));
         HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));
     }
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    // SigG2: sigma_1's subgroup test comes from this loop's T (a failure raises rlc_any: fallback)
+    KCK(cck_miller_twin(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), c->fbuf.as<uint32_t>(), N,
+                        c->mode == 0 ? c->rlc_any.as<uint32_t>() : nullptr, st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_rlc_reduce(N, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,
                        st));

@@ -5,27 +5,30 @@
 //     prod_i e(-sigma_2,i, delta_i g~) = e(sum_i delta_i (-sigma_2,i), g~).
 // delta_i is drawn as 16 signed base-256 digits d_w,i in [-128, 127] (fr.h rlc_delta_signed), so
 //     sum_i delta_i X_i = sum_w sum_{d=1..128} (256^w d) B_w,d,   B_w,d = sum_{i: |d_w,i| = d} sign X_i
-// and instead of ONE sequential Horner combination (128 doublings of one point: ~2k dependent Fp
-// multiplications on one lane, milliseconds of latency) the scalars 256^w d move to the OTHER pairing
-// argument, whose points P_w,d = (256^w d) g~ are fixed per verkey:
-//     prod = prod_{w,d} e(B_w,d, P_w,d)       (2,048 one-pair pseudo-credentials)
-// The per-credential Miller loop keeps pair 0 only (NP = 1: ~40 % fewer multiplications); the fold
-// costs ~16 mixed additions per credential (one per window) and a 2,048-lane-pair Miller launch that
-// the host runs on a second stream, concurrently with the credentials' Miller launch (alone it
-// would be latency-bound: 64 waves on 1,024 SIMDs).
+// and instead of ONE sequential Horner combination over all 16 windows (~2k dependent Fp
+// multiplications on one lane, milliseconds of latency) each window is combined on its own wave and
+// the window weights 256^w move to the OTHER pairing argument, whose points P_w = (256^w) g~ are fixed
+// per verkey:
+//     prod = prod_w e(S_w, P_w),   S_w = sum_{d=1..128} d B_w,d      (16 one-pair pseudo-credentials)
+// S_w is a bucket-method sum spread over the wave's lanes (k_fold_window): lane t takes the CK
+// digits d = CK t + k + 1 and forms U_t = sum_k (k + 1) B and T_t = sum_k B by running sums, then
+// U_t + [CK t] T_t; a butterfly adds the lanes.  The per-credential Miller loop keeps pair 0 only and
+// runs two credentials per shared-squaring loop (miller_lz.hip kTwin); the fold costs ~16 mixed
+// additions per credential (one per window) and ~30 point operations per window lane.
 //
 //   k_fold_count / k_fold_scan / k_fold_scatter : counting sort of the (w, i) digits into 2,048
 //                                                 bucket lists, each padded to FS-entry chunks
 //   k_fold_sum<F>                               : one lane per chunk: mixed additions of its points
-//   k_fold_reduce<F>                            : one wave per bucket: chunk partials, butterfly, affine
-//   k_fold_sum_g2pl / k_fold_reduce_g2pl        : the same for G2 buckets (SigG2) on the pair-lane
-//                                                 Fp2 (curve_pl.h): one LANE PAIR per chunk / 32 pairs
-//                                                 per bucket, 2 waves/SIMD where the one-lane G2
-//                                                 forms need 448-512 registers (1 wave/SIMD)
-//   k_fold_fixed<F>                             : the fixed points P_w,d (once per verkey)
-// X_i = -sigma_2,i (AoS affine, written by the RLC prep); B_w,d lands in the pseudo-credentials' prep
-// SoA (soa.h slots, stride FB; bucket b = pseudo-credential b, pair 0) as the Q side (SigG2: B in G2)
-// or the P side (SigG1: B in G1), P_w,d on the other side.
+//   k_fold_reduce<F>                            : one wave per bucket: chunk partials, butterfly
+//   k_fold_window<F>                            : one wave per window: S_w, affine
+//   k_fold_sum_g2pl / k_fold_reduce_g2pl /      : the same for G2 buckets (SigG2) on the pair-lane
+//   k_fold_window_g2pl                            Fp2 (curve_pl.h): one LANE PAIR per chunk / 32 pairs
+//                                                 per bucket or window, 2 waves/SIMD where the one-lane
+//                                                 G2 forms need 448-512 registers (1 wave/SIMD)
+//   k_fold_fixed<F>                             : the fixed points P_w (once per verkey)
+// X_i = -sigma_2,i (AoS affine, written by the RLC prep); S_w lands in the pseudo-credentials' prep
+// SoA (soa.h slots, stride FW; window w = pseudo-credential w, pair 0) as the Q side (SigG2: S in G2)
+// or the P side (SigG1: S in G1), P_w on the other side.
 #include "codec.h"
 #include "curve_pl.h"
 #include "fixed.h"
@@ -162,12 +165,11 @@ __global__ __launch_bounds__(256) void k_fold_sum(size_t maxchunks, const uint32
     st_jac_aos<F>(part + c * JW, acc);
 }
 
-// one wave per bucket: lane-strided sum of the bucket's chunk partials, butterfly across the wave,
-// affine; written as pseudo-credential b.  kBisQ: B is the Q side (SigG2).
-template <class F, bool kBisQ>
+// one wave per bucket: lane-strided sum of the bucket's chunk partials, butterfly across the wave;
+// the Jacobian sum B_b goes to bkt (AoS, JW words a bucket)
+template <class F>
 __global__ __launch_bounds__(64) void k_fold_reduce(const uint32_t* __restrict__ off, const uint32_t* __restrict__ part,
-                                                    const uint8_t* __restrict__ fixed_inf, uint32_t* __restrict__ prep2,
-                                                    uint32_t* __restrict__ flags2) {
+                                                    uint32_t* __restrict__ bkt) {
     constexpr int JW = sizeof(Jac<F>) / 4;
     const int b = blockIdx.x;
     const uint32_t c0 = off[b] / FS, c1 = off[b + 1] / FS;
@@ -180,13 +182,50 @@ __global__ __launch_bounds__(64) void k_fold_reduce(const uint32_t* __restrict__
         jac_add(acc, acc, p);
     }
     lane_group_sum<F, 64>(acc);
+    if (threadIdx.x == 0) st_jac_aos<F>(bkt + (size_t)b * JW, acc);
+}
+
+// lane t's share of S_w = sum_d d B_d over the digits d = CK t + k + 1 (k < CK): U + [CK t] T with
+// U = sum_k (k + 1) B, T = sum_k B (running sums from the top digit down); ld(k, B) loads B.  t < 64.
+template <class F, int CK, class Ld>
+DEV Jac<F> window_share(int t, Ld ld) {
+    Jac<F> run, u, v;
+    jac_set_inf(run);
+    jac_set_inf(u);
+#pragma unroll 1
+    for (int k = CK - 1; k >= 0; k--) {
+        Jac<F> b;
+        ld(k, b);
+        jac_add(run, run, b);
+        jac_add(u, u, run);
+    }
+    jac_set_inf(v);
+#pragma unroll 1
+    for (int s = 5; s >= 0; s--) {  // [t] T, then [CK] of it
+        jac_dbl(v, v);
+        if ((t >> s) & 1) jac_add(v, v, run);
+    }
+#pragma unroll 1
+    for (int c = 1; c < CK; c <<= 1) jac_dbl(v, v);
+    jac_add(u, u, v);
+    return u;
+}
+
+// one wave per window (one lane per CK = 2 digits): S_w, affine, as pseudo-credential w (P side:
+// SigG1, S in G1); flags2[w]: skip the pair (S_w = O or P_w = O)
+__global__ __launch_bounds__(64) void k_fold_window(const uint32_t* __restrict__ bkt, const uint8_t* __restrict__ fixed_inf,
+                                                    uint32_t* __restrict__ prep2, uint32_t* __restrict__ flags2) {
+    constexpr int JW = sizeof(Jac<Fp>) / 4, CK = FD / 64;
+    const int w = blockIdx.x, t = threadIdx.x;
+    Jac<Fp> acc = window_share<Fp, CK>(t, [&](int k, Jac<Fp>& b) {
+        ld_jac_aos<Fp>(b, bkt + (size_t)(w * FD + CK * t + k) * JW);
+    });
+    lane_group_sum<Fp, 64>(acc);
     if (threadIdx.x != 0) return;
-    Aff<F> a;
+    Aff<Fp> a;
     const bool fin = jac_to_aff(a, acc);
-    const Soa S{prep2, FB};
-    if constexpr (kBisQ) st_as_q(S, b, a);
-    else st_as_p(S, b, a);
-    flags2[b] = (!fin || fixed_inf[b]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
+    st_as_p(Soa{prep2, FW}, w, a);
+    flags2[w] = (!fin || fixed_inf[w]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
 }
 
 // k_fold_sum for G2 points on the pair-lane Fp2: one lane pair per chunk, each lane adds its halves.
@@ -215,11 +254,10 @@ __global__ __launch_bounds__(256, 2) void k_fold_sum_g2pl(size_t maxchunks, cons
     st_jac_aos<pl::Fp2>(part + c * JW + h * HW, acc);
 }
 
-// k_fold_reduce<Fp2, true> on the pair-lane Fp2: one wave (32 lane pairs) per bucket
+// k_fold_reduce<Fp2> on the pair-lane Fp2: one wave (32 lane pairs) per bucket; bkt as part
 __global__ __launch_bounds__(64, 2) void k_fold_reduce_g2pl(const uint32_t* __restrict__ off,
                                                            const uint32_t* __restrict__ part,
-                                                           const uint8_t* __restrict__ fixed_inf,
-                                                           uint32_t* __restrict__ prep2, uint32_t* __restrict__ flags2) {
+                                                           uint32_t* __restrict__ bkt) {
     constexpr int JW = sizeof(Jac<Fp2>) / 4, HW = sizeof(Jac<pl::Fp2>) / 4;
     const int b = blockIdx.x;
     const int h = (int)pl::half_id();
@@ -233,40 +271,54 @@ __global__ __launch_bounds__(64, 2) void k_fold_reduce_g2pl(const uint32_t* __re
         jac_add(acc, acc, p);
     }
     pl::pair_group_sum<64>(acc);
+    if (threadIdx.x < 2) st_jac_aos<pl::Fp2>(bkt + (size_t)b * JW + h * HW, acc);
+}
+
+// k_fold_window for G2 buckets on the pair-lane Fp2 (one lane pair per CK = 4 digits), S_w as the
+// Q side (SigG2)
+__global__ __launch_bounds__(64, 2) void k_fold_window_g2pl(const uint32_t* __restrict__ bkt,
+                                                           const uint8_t* __restrict__ fixed_inf,
+                                                           uint32_t* __restrict__ prep2, uint32_t* __restrict__ flags2) {
+    constexpr int JW = sizeof(Jac<Fp2>) / 4, HW = sizeof(Jac<pl::Fp2>) / 4, CK = FD / 32;
+    const int w = blockIdx.x, t = threadIdx.x >> 1;  // pair-uniform
+    const int h = (int)pl::half_id();
+    Jac<pl::Fp2> acc = window_share<pl::Fp2, CK>(t, [&](int k, Jac<pl::Fp2>& b) {
+        ld_jac_aos<pl::Fp2>(b, bkt + (size_t)(w * FD + CK * t + k) * JW + h * HW);
+    });
+    pl::pair_group_sum<64>(acc);
     if (threadIdx.x >= 2) return;
     Aff<pl::Fp2> a;
     const bool fin = jac_to_aff(a, acc);
-    const Soa S{prep2, FB};
-    pl::st_f2(S, S_Q1, b, a.x);
-    pl::st_f2(S, S_Q1 + 2, b, a.y);
-    if (!h) flags2[b] = (!fin || fixed_inf[b]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
+    const Soa S{prep2, FW};
+    pl::st_f2(S, S_Q1, w, a.x);
+    pl::st_f2(S, S_Q1 + 2, w, a.y);
+    if (!h) flags2[w] = (!fin || fixed_inf[w]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
 }
 
-// P_w,d = (256^w d) g~ from g~'s fixed-base table (base index q of the verkey tables); G is g~'s field
+// P_w = (256^w) g~ from g~'s fixed-base table (base index q of the verkey tables); G is g~'s field
 template <class G>
-__global__ __launch_bounds__(256) void k_fold_fixed(int q, const uint32_t* __restrict__ table, int wbits,
-                                                    const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep2,
-                                                    uint8_t* __restrict__ fixed_inf) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= FB) return;
-    const int w = b / FD, d = b % FD + 1;
+__global__ __launch_bounds__(64) void k_fold_fixed(int q, const uint32_t* __restrict__ table, int wbits,
+                                                   const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep2,
+                                                   uint8_t* __restrict__ fixed_inf) {
+    const int w = threadIdx.x;
+    if (w >= FW) return;
     uint32_t s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    s[w >> 2] = (uint32_t)d << (8 * (w & 3));
+    s[w >> 2] = 1u << (8 * (w & 3));
     Jac<G> acc;
     jac_set_inf(acc);
     if (!binf[q]) ft_add<G>(acc, s, table, wbits, q, 0, ft_nwin(wbits), true);  // the verkey table: lazy form
     Aff<G> a;
     const bool fin = jac_to_aff(a, acc);
-    fixed_inf[b] = fin ? 0 : 1;
-    const Soa S{prep2, FB};
-    if constexpr (sizeof(G) == sizeof(Fp)) st_as_p(S, b, a);  // SigG2: g~ in G1
-    else st_as_q(S, b, a);                                     // SigG1: g~ in G2
+    fixed_inf[w] = fin ? 0 : 1;
+    const Soa S{prep2, FW};
+    if constexpr (sizeof(G) == sizeof(Fp)) st_as_p(S, w, a);  // SigG2: g~ in G1
+    else st_as_q(S, w, a);                                     // SigG1: g~ in G2
 }
 
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 // work-buffer layout (32-bit words): cnt FB | off FB+1 | cur FB (+3) | list maxchunks*FS |
-// part maxchunks*JW (16-byte aligned)
+// part maxchunks*JW (16-byte aligned) | bkt FB*JW
 static size_t fold_maxchunks(size_t n) { return (FW * n + (size_t)FB * (FS - 1)) / FS + 1; }
 
 extern "C" {
@@ -274,13 +326,15 @@ extern "C" {
 size_t cck_fold_words(int mode, size_t n) {
     const size_t jw = mode == 0 ? sizeof(Jac<Fp2>) / 4 : sizeof(Jac<Fp>) / 4;
     const size_t mc = fold_maxchunks(n);
-    return 3 * (size_t)FB + 1 + 3 + mc * FS + mc * jw + 4;
+    return 3 * (size_t)FB + 1 + 3 + mc * FS + mc * jw + 4 + (size_t)FB * jw;
 }
 
+int cck_fold_pseudo() { return FW; }
+
 // mode 0 (SigG2): X_i in G2 (AoS affine, 48 words), g~ in G1; mode 1: X_i in G1 (24 words), g~ in G2.
-// d_dig: [FW][n] int8 digits (0 for credentials to leave out).  fixed_ok = 0 recomputes P_w,d into
-// d_prep2 and their identity flags into d_finf (FB bytes); both persist between calls.
-// d_prep2: PREP_SLOTS x FB SoA; d_flags2: FB words (pair-0 skip flags of the pseudo-credentials).
+// d_dig: [FW][n] int8 digits (0 for credentials to leave out).  fixed_ok = 0 recomputes P_w into
+// d_prep2 and their identity flags into d_finf (FW bytes); both persist between calls.
+// d_prep2: PREP_SLOTS x FW SoA; d_flags2: FW words (pair-0 skip flags of the pseudo-credentials).
 int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok, int q,
              const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
              uint32_t* d_flags2, hipStream_t st) {
@@ -292,13 +346,12 @@ int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uin
     uint8_t* finf = d_finf;
     uint32_t* list = cur + FB + 3;
     uint32_t* part = reinterpret_cast<uint32_t*>(((uintptr_t)(list + mc * FS) + 15) & ~(uintptr_t)15);
+    uint32_t* bkt = part + mc * (mode == 0 ? sizeof(Jac<Fp2>) / 4 : sizeof(Jac<Fp>) / 4);
     if (!fixed_ok) {
         if (mode == 0)
-            hipLaunchKernelGGL(k_fold_fixed<Fp>, dim3(FB / 256), dim3(256), 0, st, q, d_table, wbits, d_binf, d_prep2,
-                               finf);
+            hipLaunchKernelGGL(k_fold_fixed<Fp>, dim3(1), dim3(64), 0, st, q, d_table, wbits, d_binf, d_prep2, finf);
         else
-            hipLaunchKernelGGL(k_fold_fixed<Fp2>, dim3(FB / 256), dim3(256), 0, st, q, d_table, wbits, d_binf,
-                               d_prep2, finf);
+            hipLaunchKernelGGL(k_fold_fixed<Fp2>, dim3(1), dim3(64), 0, st, q, d_table, wbits, d_binf, d_prep2, finf);
     }
     if (hipMemsetAsync(cnt, 0, FB * 4, st) != hipSuccess || hipMemsetAsync(list, 0xff, mc * FS * 4, st) != hipSuccess)
         return -1;
@@ -308,10 +361,12 @@ int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uin
     hipLaunchKernelGGL(k_fold_scatter, gw, dim3(256), 0, st, n, d_dig, cur, list);
     if (mode == 0) {
         hipLaunchKernelGGL(k_fold_sum_g2pl, dim3(nblocks(2 * mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
-        hipLaunchKernelGGL(k_fold_reduce_g2pl, dim3(FB), dim3(64), 0, st, off, part, finf, d_prep2, d_flags2);
+        hipLaunchKernelGGL(k_fold_reduce_g2pl, dim3(FB), dim3(64), 0, st, off, part, bkt);
+        hipLaunchKernelGGL(k_fold_window_g2pl, dim3(FW), dim3(64), 0, st, bkt, finf, d_prep2, d_flags2);
     } else {
         hipLaunchKernelGGL(k_fold_sum<Fp>, dim3(nblocks(mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
-        hipLaunchKernelGGL((k_fold_reduce<Fp, false>), dim3(FB), dim3(64), 0, st, off, part, finf, d_prep2, d_flags2);
+        hipLaunchKernelGGL(k_fold_reduce<Fp>, dim3(FB), dim3(64), 0, st, off, part, bkt);
+        hipLaunchKernelGGL(k_fold_window, dim3(FW), dim3(64), 0, st, bkt, finf, d_prep2, d_flags2);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

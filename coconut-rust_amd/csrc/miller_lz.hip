@@ -4,10 +4,13 @@
 // inputs and outputs); one credential per PAIR of adjacent lanes as there.
 //
 //   SigG2: pair 0 = (sigma_1, pr) with pr in Jacobian-evaluation form (XZ, Y, Z^3);
-//          pair 1 = (-sigma_2, g~): g~ affine constant, or per lane (lane2: the RLC fold's
-//          pseudo-credentials, fold.hip).
+//          pair 1 = (-sigma_2, g~): g~ affine constant.
 //   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2).
-//   RLC mode runs pair 0 alone (NP = 1).
+//   RLC mode keeps pair 0 of every credential (its second pairs are folded, fold.hip) and runs TWO
+//   credentials through the 2-pair loop (kTwin): the RLC only needs the product of the credentials'
+//   Miller values, and the shared squaring halves the Fp12 work per credential (5,696 Fp
+//   multiplications against 6,800 for a loop of its own).  The fold's 16 window pairs run one pair
+//   per loop (NP = 1).
 //
 // Representation boundary: the prep SoA holds canonical 12 x 32 values in R = 2^406 form.  The twist
 // points are moved to R' form once (in_r: T's start and the addition steps' Q).  The G1 evaluation
@@ -39,7 +42,6 @@ using Tw = G2P<BX, BY, BZ>;
 using F12S = F12<AS, BF>;
 using F2L = F2<AS, BL>;
 using LineS = Line<F2L, F2L, F2L>;
-constexpr int TW = 3 * LN;  // words of a parked Tw (this lane's halves)
 
 template <class L>
 DEV LineS fit_line(const L& l) { return {fit<AS, BL>(l.l0), fit<AS, BL>(l.l2), fit<AS, BL>(l.l3)}; }
@@ -146,38 +148,63 @@ static __device__ __noinline__ void miller_add(StepState* st, const uint32_t* pr
     st->f = eval_mul(f, ln, ps, i, skip);
 }
 
+// sigma_1's G2 subgroup test from the loop's final T (curve_pl.h miller_t_in_subgroup): out of line,
+// so its registers do not add to the loop's
+static __device__ __noinline__ void t_check(const Tw* T, const uint32_t* prep, size_t n, int qslot, size_t i,
+                                            uint32_t* qcheck) {
+    pl::G2Proj Tp;
+    Tp.x = out_r2(T->x);
+    Tp.y = out_r2(T->y);
+    Tp.z = out_r2(T->z);
+    const Soa S{const_cast<uint32_t*>(prep), n};
+    Aff<pl::Fp2> q;
+    pl::ld_f2(q.x, S, qslot, i);
+    pl::ld_f2(q.y, S, qslot + 2, i);
+    if (!pl::miller_t_in_subgroup(Tp, q) && !half_id()) atomicOr(qcheck, 1u);
+}
+
 }  // namespace
 
 // prep: SoA slots of soa.h; flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 pr = O, bit4 pair-1 P = O
-// cst: SigG2 -> g~ affine (24 words, used when !kLane2); SigG1 -> g~ lines (68 x 72 words)
-// NP = 1: pair 0 only (RLC mode).  The Miller value of credential i goes to fout as SoA element
-// foff + i of stride fstride.  qcheck (NP = 1, SigG2): pair 0's Q (sigma_1) gets the G2 subgroup test
-// from the loop's own T (curve_pl.h miller_t_in_subgroup); a failure sets *qcheck.
-template <int SIG, bool kLane2, int NP>
+// cst: SigG2 -> g~ affine (24 words); SigG1 -> g~ lines (68 x 72 words); unused by NP = 1 and kTwin
+// NP = 1: pair 0 only (the RLC fold's window pairs).  The Miller value of credential i goes to fout as
+// SoA element foff + i of stride fstride.  kTwin (NP = 2, RLC credentials): the one pair of credentials
+// 2j and 2j + 1, laid out as pairs 0 and 1 of element j (rlc.hip twin_slot; the second skipped when n
+// is odd); their product goes to element foff + j.  qcheck (one pair per credential, SigG2): each
+// credential's Q (sigma_1) gets the G2 subgroup test from the loop's own T (curve_pl.h
+// miller_t_in_subgroup); a failure sets *qcheck.
+template <int SIG, int NP, bool kTwin = false>
 __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __restrict__ prep,
                                                const uint32_t* __restrict__ flags, const uint32_t* __restrict__ cst,
                                                uint32_t* __restrict__ fout, size_t fstride, size_t foff,
                                                uint32_t* __restrict__ qcheck) {
+    static_assert(!kTwin || NP == 2, "twin: two credentials' pairs");
     __shared__ int32_t lds[NP == 2 ? 2 * TP : 1][MB];
-    const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // credential of this lane pair
-    if (i >= n) return;  // pair-uniform
+    const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // lane pair: credential (twin: pair)
+    if (i >= (kTwin ? (n + 1) / 2 : n)) return;  // pair-uniform
     constexpr bool kSigG2 = SIG == 2;
-    const uint32_t fl = flags[i];
-    const bool skip0 = (fl & 5u) != 0, skip1 = (fl & 18u) != 0;
+    // twin: credentials 2 i and 2 i + 1 have their pairs at element i of the pair-0 and pair-1 slots
+    // (rlc.hip twin_slot); with n odd the last pair 1 is skipped (its element was never written)
+    const uint32_t fl = flags[kTwin ? 2 * i : i];
+    const bool skip0 = (fl & 5u) != 0;
+    const bool skip1 = kTwin ? (2 * i + 1 >= n || (flags[2 * i + 1] & 5u) != 0) : (fl & 18u) != 0;
     PSrc ps0, ps1;
-    if (kSigG2) {
+    if (kTwin) {
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, kSigG2};
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kSigG2};
+    } else if (kSigG2) {
         ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, true};
-        ps1 = kLane2 ? PSrc{prep + (size_t)S_P2 * NL * n, n, 1, true} : PSrc{cst, 1, 0, false};
+        ps1 = PSrc{cst, 1, 0, false};
     } else {
         ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, false};
-        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kLane2};
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, false};
     }
     const Soa S{const_cast<uint32_t*>(prep), n};
     // NP = 1: T stays in registers; NP = 2: both T's parked in LDS between their uses
     Tw T;
     {
         F2<AN, 17> qx, qy;
-        if (kSigG2 && NP == 2) {  // pair 1's T = -sigma_2
+        if ((kSigG2 || kTwin) && NP == 2) {  // pair 1's T: -sigma_2 (twin: the second credential's Q)
             ld_q(qx, qy, S, S_Q2, i);
             park(lds, 1, t_from(qx, qy));
         }
@@ -194,7 +221,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
 #pragma unroll 1
         for (int k = 0; k < NP; k++) {
             LineS ln;
-            if (!kSigG2 && k == 1) {
+            if (!kSigG2 && !kTwin && k == 1) {
                 ln = ld_line(gl);
                 gl += 72;
             } else {
@@ -209,7 +236,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
         if ((X_ABS >> b) & 1ull) {
 #pragma unroll 1
             for (int k = 0; k < NP; k++) {
-                const bool const_line = !kSigG2 && k == 1;
+                const bool const_line = !kSigG2 && !kTwin && k == 1;
                 StepState st;
                 st.f = f;
                 if (!const_line) st.T = NP == 2 ? unpark(lds, k) : T;
@@ -222,15 +249,13 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
             }
         }
     }
-    if (NP == 1 && kSigG2 && qcheck && !skip0) {
-        pl::G2Proj Tp;
-        Tp.x = out_r2(T.x);
-        Tp.y = out_r2(T.y);
-        Tp.z = out_r2(T.z);
-        Aff<pl::Fp2> q;
-        pl::ld_f2(q.x, S, S_Q1, i);
-        pl::ld_f2(q.y, S, S_Q1 + 2, i);
-        if (!pl::miller_t_in_subgroup(Tp, q) && !half_id()) atomicOr(qcheck, 1u);
+    if ((NP == 1 || kTwin) && kSigG2 && qcheck) {
+#pragma unroll 1
+        for (int k = 0; k < NP; k++) {
+            if (k ? skip1 : skip0) continue;  // pair-uniform
+            const Tw Tk = NP == 2 ? unpark(lds, k) : T;
+            t_check(&Tk, prep, n, k ? S_Q2 : S_Q1, i, qcheck);
+        }
     }
     f = f12_conj(f);
     const Soa O{fout, fstride};
@@ -248,24 +273,26 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
 #define CC_MILLER_LAUNCH cck_miller_lz_g1
 #endif
 
-// lane2: per-lane second-pair P; np: pairs per credential (1 or 2); the Miller values go to SoA
-// elements [foff, foff + n) of stride fstride (>= foff + n); d_qcheck (np = 1, SigG2, or null): the
-// sigma_1 subgroup test from the loop's T
-extern "C" int CC_MILLER_LAUNCH(int lane2, int np, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+// np: pairs per credential (1 or 2); twin (np = 1): two credentials per lane pair, one Miller value
+// (their product) per two credentials.  The m Miller values (m = n, twin: ceil(n / 2)) go to SoA
+// elements [foff, foff + m) of stride fstride (>= foff + m); d_qcheck (np = 1 or twin, SigG2, or
+// null): the sigma_1 subgroup test from the loop's T
+extern "C" int CC_MILLER_LAUNCH(int np, int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                                 const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff,
                                 uint32_t* d_qcheck, hipStream_t st) {
     if (!n) return 0;
-    if (fstride < foff + n || (np != 1 && np != 2)) return -1;
+    const size_t m = twin ? (n + 1) / 2 : n;
+    if (fstride < foff + m || (np != 1 && np != 2) || (twin && np != 1)) return -1;
     constexpr int MB = cc::lz::MB;
-    dim3 g((unsigned)((2 * n + MB - 1) / MB)), b(MB);
-    if (np == 1)
-        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, false, 1>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+    dim3 g((unsigned)((2 * m + MB - 1) / MB)), b(MB);
+    if (twin)
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, 2, true>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
                            fstride, foff, d_qcheck);
-    else if (lane2)
-        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, true, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
-                           fstride, foff, d_qcheck);
+    else if (np == 1)
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, 1>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f, fstride,
+                           foff, d_qcheck);
     else
-        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, false, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
-                           fstride, foff, d_qcheck);
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f, fstride,
+                           foff, d_qcheck);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -7,12 +7,12 @@
 //     prod_i e(delta_i pr_i, sigma_1,i) * e(g~, -delta_i sigma_2,i) == 1        (SigG1)
 //
 // with independent delta_i (ChaCha20 keyed by a fresh host seed, 16 signed base-256 digits: fr.h
-// rlc_delta_signed): the second pairs share g~ and are folded into 2,048 bucket pairs (fold.hip), so
-// each credential runs a ONE-pair Miller loop; then the product of all Miller values and ONE final
-// exponentiation per batch (or, over several GPUs, one per gathered set of per-GPU partial products).
-// A forged credential passes with probability <= 2^-127.  If the batch fails, or any sigma is the identity (which the per-credential
-// semantics reject), the caller falls back to per-credential verification, so verdicts always equal
-// the reference's.
+// rlc_delta_signed): the second pairs share g~ and are folded into 16 window pairs (fold.hip), so
+// each credential keeps ONE pair (two credentials per shared-squaring Miller loop); then the product
+// of all Miller values and ONE final exponentiation per batch (or, over several GPUs, one per
+// gathered set of per-GPU partial products).  A forged credential passes with probability <= 2^-127.
+// If the batch fails, or any sigma is the identity (which the per-credential semantics reject), the
+// caller falls back to per-credential verification, so verdicts always equal the reference's.
 //
 //   k_rlc_check_* / k_rlc_msm_*        : decode, subgroup checks and the fold's inputs (-sigma_2,
 //                                         delta's digits); the delta-scaled fixed-base MSM
@@ -44,11 +44,16 @@ DEV void st_eval(const Soa& S, int slot, size_t i, const Jac<Fp>& P) {
     st_fp(S, slot + 2, i, t);
 }
 
+// The RLC keeps one pair per credential and runs two credentials per Miller loop (miller_lz.hip
+// kTwin): credential i's pair goes to SoA element i / 2 of the verify layout's pair-0 slots (even i)
+// or pair-1 slots (odd i), so the loop loads both pairs exactly as a verify loop does (coalesced).
+DEV int twin_slot(int s0, int s1, size_t i) { return (i & 1) ? s1 : s0; }
+
 }  // namespace
 
 // Tables: bases [Y~_0 .. Y~_{q-1}, g~, X~] (indices 0..q-1, q, q+1) of cc_set_verkey.
 // flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 delta pr = O, bit5 sigma outside the subgroup.
-// Per credential: pair 0 of the Miller loop (sigma_1 with delta pr, SoA slots of soa.h), the fold
+// Per credential: its Miller pair (sigma_1 with delta pr, SoA slots of soa.h, twin_slot), the fold
 // point X_i = -sigma_2,i (AoS affine, pts) and delta's 16 signed digits (dig[w * n + i]; all zero when
 // sigma_2 is the identity, which fails the batch anyway).  delta X~ runs over all windows: delta is
 // used mod r (fr.h rlc_delta_signed).
@@ -85,9 +90,9 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t b
     uint32_t fl = 0;
     Aff<Fp2> a;
     if (!g2_decode(a, (h ? s2b : s1b) + i * 192)) fl |= h ? 2u : 1u;
-    if (!h) {
-        st_f2(S, S_Q1, i, a.x);
-        st_f2(S, S_Q1 + 2, i, a.y);
+    if (!h) {  // pair 0's Q in the twin layout (twin_slot)
+        st_f2(S, twin_slot(S_Q1, S_Q2, i), i >> 1, a.x);
+        st_f2(S, twin_slot(S_Q1, S_Q2, i) + 2, i >> 1, a.y);
     } else {
         Aff<Fp2> m = a;
         f2_neg(m.y, m.y);
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, int q, uint6
     }
     const Jac<Fp> acc = lz::jg_to(a);
     if (jac_is_inf(acc)) flags[i] |= 4u;
-    st_eval(S, S_P1, i, acc);
+    st_eval(S, twin_slot(S_P1, S_P2, i), i >> 1, acc);
 }
 
 // one credential per lane pair: lane h decodes and subgroup-checks sigma_{h+1} (one-lane G1)
@@ -158,8 +163,8 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, uint64_t b
     if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
     else if (!g1_in_subgroup(a)) fl |= 32u;
     if (!h) {
-        st_fp(S, S_P1, i, a.x);
-        st_fp(S, S_P1 + 1, i, a.y);
+        st_fp(S, twin_slot(S_P1, S_P2, i), i >> 1, a.x);
+        st_fp(S, twin_slot(S_P1, S_P2, i) + 1, i >> 1, a.y);
     } else {
         fp_neg(a.y, a.y);
         st_aff_aos<Fp>(pts + i * (sizeof(Aff<Fp>) / 4), a);
@@ -206,8 +211,8 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg1(size_t n, int q, uint6
     const Jac<pl::Fp2> acc = pl::jl_to_pl(la);
     Aff<pl::Fp2> a2;
     const bool fin = jac_to_aff(a2, acc);
-    pl::st_f2(S, S_Q1, i, a2.x);
-    pl::st_f2(S, S_Q1 + 2, i, a2.y);
+    pl::st_f2(S, twin_slot(S_Q1, S_Q2, i), i >> 1, a2.x);
+    pl::st_f2(S, twin_slot(S_Q1, S_Q2, i) + 2, i >> 1, a2.y);
     if (!fin && !pl::half_id()) flags[i] |= 4u;
 }
 

@@ -149,6 +149,45 @@ def test_config4_fused_entry_one_lagrange(ctxs):
         assert [oy[j * ob:(j + 1) * ob].hex() for j in range(d["q"])] == case["out_Y"]
 
 
+def test_config4_fused_entry_sigg1_and_unknown_id(ctxs):
+    """SigG1 (sigma in G1, issuer keys in G2: the pair-lane issuer-table kernel on the side stream, running
+    alongside the G1 Straus): the fused entry's four outputs equal construction on 1,000 credentials, and an
+    id without an issuer key raises the device error word through the same entry."""
+    import torch
+    import bench_modes
+    from coconut import _lib
+    ctx = ctxs["G1"]
+    n = 1000
+    b = bench_modes.make_aggregate_batch(ctx, 1, n, seed=46)
+    ctx.set_issuers(b["iss"], b["X"], b["Y"], b["q"])
+    t, q, sb, ob = b["t"], b["q"], b["sb"], b["ob"]
+    dev = torch.device("cuda", 0)
+    ids = b["ids"].copy()
+    d_ids = torch.from_numpy(ids.view(np.int64).copy()).to(dev)
+    d_s1 = torch.frombuffer(bytearray(b["s1"]), dtype=torch.uint8).to(dev)
+    d_s2 = torch.frombuffer(bytearray(b["s2"]), dtype=torch.uint8).to(dev)
+    o1, o2 = (torch.zeros(n * sb, dtype=torch.uint8, device=dev) for _ in range(2))
+    oX = torch.zeros(n * ob, dtype=torch.uint8, device=dev)
+    oY = torch.zeros(n * q * ob, dtype=torch.uint8, device=dev)
+    P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    torch.cuda.synchronize()
+    lib = _lib.lib
+    assert lib.cc_aggregate_credential_batch_device(ctx.h, n, t, t, P(d_ids), P(d_s1), P(d_s2), P(o1), P(o2),
+                                                    P(oX), P(oY), None) == 0
+    assert ctx.device_error() == 0
+    assert bytes(oX.cpu().numpy()) == b["want_X"] * n
+    assert bytes(oY.cpu().numpy()) == b["want_Y"] * n
+    assert bytes(o2.cpu().numpy()) == b["want_s2"][:n * sb]
+    assert bytes(o1.cpu().numpy()) == b["want_s1"][:n * sb]
+    bad = ids.copy().reshape(n, -1)
+    bad[7, 3] = 10 ** 9  # no issuer holds this id
+    d_bad = torch.from_numpy(bad.reshape(-1).view(np.int64).copy()).to(dev)
+    torch.cuda.synchronize()
+    assert lib.cc_aggregate_credential_batch_device(ctx.h, n, t, t, P(d_bad), P(d_s1), P(d_s2), P(o1), P(o2),
+                                                    P(oX), P(oY), None) == 0
+    assert ctx.device_error() == 1  # CC_DEVERR_UNKNOWN_ID
+
+
 def test_config5_full_size_pok_device(ctxs):
     """65,536 PoK proofs (q = 32, 8 revealed) through cc_pok_verify_batch_device: verdicts equal
     construction (1/16 corrupted responses); the host entry point agrees on a slice."""
