@@ -40,14 +40,18 @@ int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* 
 int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
              uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
-int cck_miller_lz_g2(int np, int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+int cck_miller_lz_g2(int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
-int cck_miller_lz_g1(int np, int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+int cck_miller_lz_g1(int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
 size_t cck_fold_words(int mode, size_t n);
 int cck_fold_pseudo();
+int cck_fold_window(int mode, size_t n, uint32_t* d_work, const uint8_t* d_finf, uint32_t* d_prep2,
+                    uint32_t* d_flags2, hipStream_t st);
+int cck_miller_wide(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f, size_t fstride,
+                    size_t foff, hipStream_t st);
 int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok,
              int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
              uint32_t* d_flags2, hipStream_t st);
@@ -167,13 +171,10 @@ struct cc_ctx {
     float last_ms[3] = {0, 0, 0};
     // orders a caller-supplied stream against the context stream (StreamOrder below)
     hipEvent_t ev_order = nullptr;
-    // side stream (high priority): Verkey::aggregate beside Signature::aggregate (ev_fork / ev_join)
+    // side stream (high priority; ev_fork / ev_join): Verkey::aggregate beside Signature::aggregate,
+    // the RLC fold's window pairs beside the delta MSM
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // RLC partial: the fold's window pairs' Miller launch (one wave, ~6 ms of latency) on one CU of
-    // its own (cu_one) while the delta MSM runs on the others (cu_rest); ev_msm after the MSM
-    hipStream_t cu_one = nullptr, cu_rest = nullptr;
-    hipEvent_t ev_msm = nullptr;
     // device set (cc_ctx_create_multi): one single-device context per GPU and one RCCL communicator
     // per GPU (ncclCommInitAll, this process drives every device); empty for a single-device context
     std::vector<cc_ctx*> peers;
@@ -208,22 +209,22 @@ struct StreamOrder {
 // [foff, foff + n) of stride fstride (default: n, 0).
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                       uint32_t* d_f, hipStream_t st) {
-    return mode == 0 ? cck_miller_lz_g2(2, 0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st)
-                     : cck_miller_lz_g1(2, 0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st);
+    return mode == 0 ? cck_miller_lz_g2(0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st)
+                     : cck_miller_lz_g1(0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st);
 }
 // the RLC credentials: pair 0 only (their second pairs are folded, fold.hip), two credentials per
 // lane pair through the shared-squaring loop: (n + 1) / 2 Miller values, each the product of two
 // credentials' (the RLC multiplies them all), to SoA elements [0, (n + 1) / 2) of stride fstride
 static int cck_miller_twin(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
                            size_t fstride, uint32_t* d_qcheck, hipStream_t st) {
-    return mode == 0 ? cck_miller_lz_g2(1, 1, n, d_prep, d_flags, nullptr, d_f, fstride, 0, d_qcheck, st)
-                     : cck_miller_lz_g1(1, 1, n, d_prep, d_flags, nullptr, d_f, fstride, 0, nullptr, st);
+    return mode == 0 ? cck_miller_lz_g2(1, n, d_prep, d_flags, nullptr, d_f, fstride, 0, d_qcheck, st)
+                     : cck_miller_lz_g1(1, n, d_prep, d_flags, nullptr, d_f, fstride, 0, nullptr, st);
 }
-// the RLC fold's pseudo-credentials: one (Q, P) pair per lane pair, Q affine G2 and P in evaluation
-// form, both per lane (either group mode: the SigG2 instantiation reads exactly that)
+// the RLC fold's pseudo-credentials: one (Q, P) pair each, Q affine G2 and P in evaluation form
+// (either group mode: the fold writes exactly that), one wave each in the wide form (fexp_pl.hip)
 static int cck_miller_pairs(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
                             size_t fstride, size_t foff, hipStream_t st) {
-    return cck_miller_lz_g2(1, 0, n, d_prep, d_flags, nullptr, d_f, fstride, foff, nullptr, st);
+    return cck_miller_wide(n, d_prep, d_flags, d_f, fstride, foff, st);
 }
 
 static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }
@@ -278,22 +279,12 @@ cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
     (void)hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&c->ev_msm, hipEventDisableTiming);
     {
         // high priority: a launch on the side stream gets its wave slots before a full launch on the
         // context stream fills the chip
         int lo = 0, hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
         if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess) c->side = nullptr;
-        // CU-masked pair for the RLC partial: CU 0 alone, and every other CU
-        int ncu = 0;
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 1) {
-            const uint32_t words = (uint32_t)((ncu + 31) / 32);
-            std::vector<uint32_t> one(words, 0u), rest(words, 0u);
-            for (int k = 0; k < ncu; k++) (k ? rest : one)[k / 32] |= 1u << (k % 32);
-            if (hipExtStreamCreateWithCUMask(&c->cu_one, words, one.data()) != hipSuccess) c->cu_one = nullptr;
-            if (hipExtStreamCreateWithCUMask(&c->cu_rest, words, rest.data()) != hipSuccess) c->cu_rest = nullptr;
-        }
     }
     *out = c;
     return CC_OK;
@@ -324,10 +315,7 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-    if (c->ev_msm) (void)hipEventDestroy(c->ev_msm);
     if (c->side) (void)hipStreamDestroy(c->side);
-    if (c->cu_one) (void)hipStreamDestroy(c->cu_one);
-    if (c->cu_rest) (void)hipStreamDestroy(c->cu_rest);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return CC_OK;
@@ -656,30 +644,28 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
         HIPCK(hipMemcpyAsync(c->rlc_any.p, &one, 4, hipMemcpyHostToDevice, st));
     }
     // The second pairs become 16 window pairs (fold.hip).  The fold's short kernels run alone
-    // (behind a full launch each would wait milliseconds for a free slot).  Then the windows' Miller
-    // launch (one wave: ~6 ms of latency, about the delta MSM's time) runs on CU 0 alone while the
-    // delta MSM runs on the other CUs, and pair 0 of every credential (two per lane pair: 2,048
-    // waves, exactly the chip's wave slots) starts once both are done — a wave still holding a slot
-    // would push one of its waves into a second round.  Both Miller launches write disjoint ranges
-    // of fbuf (stride N).
+    // (behind a full launch each would wait milliseconds for a free slot); its window sums (16 waves)
+    // and the window pairs' Miller launch (16 waves in the wide form) then run on the high-priority
+    // side stream beside the delta MSM (which fills half the wave slots), and pair 0 of every
+    // credential (two per lane pair: 2,048 waves, exactly the chip's wave slots) starts once both are
+    // done — a wave still holding a slot would push one of its waves into a second round.  Both
+    // Miller launches write disjoint ranges of fbuf (stride N).
     KCK(cck_fold(c->mode, n, c->rlc_dig.as<int8_t>(), c->rlc_pts.as<uint32_t>(), c->rlc_work.as<uint32_t>(),
                  c->rlc_fixed_ok ? 1 : 0, (int)q, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(),
                  c->rlc_prep2.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_flags2.as<uint32_t>(), st));
     c->rlc_fixed_ok = true;
-    const bool split = c->cu_one && c->cu_rest;
-    hipStream_t s_one = split ? c->cu_one : st, s_rest = split ? c->cu_rest : st;
-    if (split) {
+    hipStream_t side = c->side ? c->side : st;
+    if (side != st) {
         HIPCK(hipEventRecord(c->ev_fork, st));
-        HIPCK(hipStreamWaitEvent(s_one, c->ev_fork, 0));
-        HIPCK(hipStreamWaitEvent(s_rest, c->ev_fork, 0));
+        HIPCK(hipStreamWaitEvent(side, c->ev_fork, 0));
     }
+    KCK(cck_fold_window(c->mode, n, c->rlc_work.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_prep2.as<uint32_t>(),
+                        c->rlc_flags2.as<uint32_t>(), side));
     KCK(cck_miller_pairs(NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(), c->fbuf.as<uint32_t>(), N, M,
-                         s_one));
-    KCK(prep_part(1, s_rest));  // delta X~ + sum (delta m_j) Y~_j
-    if (split) {
-        HIPCK(hipEventRecord(c->ev_msm, s_rest));
-        HIPCK(hipEventRecord(c->ev_join, s_one));
-        HIPCK(hipStreamWaitEvent(st, c->ev_msm, 0));
+                         side));
+    KCK(prep_part(1, st));  // delta X~ + sum (delta m_j) Y~_j
+    if (side != st) {
+        HIPCK(hipEventRecord(c->ev_join, side));
         HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));
     }
     if (c->timing) (void)hipEventRecord(c->ev[1], st);

@@ -21,6 +21,10 @@ namespace pl {
 // (= 3*Phi_12(p)/r, AMCL's exponent).  Each step below is one out-of-line function reading its
 // Fp12 operands from, and writing its result to, a per-lane SoA slot (12 Fp slots each).
 enum FxOp { OP_ID = 0, OP_CONJ = 1, OP_FROB = 2, OP_FROB2 = 3 };
+template <bool W>
+DEV void m12(Fp12& r, const Fp12& x, const Fp12& y);  // f12_mul, wide when W (below)
+template <bool W>
+DEV void cs12(Fp12& r, const Fp12& x);  // f12_cyc_sqr, wide when W (below)
 
 DEV void fx_apply(Fp12& x, int op) {
     if (op == OP_CONJ) {
@@ -226,9 +230,10 @@ DEV void f4_from_products(Fp4& r, const Fp2& p0, const Fp2& p1, const Fp2& p2) {
 }
 
 // = f12_mul (tower.inc): the six f4 products (t0, t1, t2 and the three cross terms) as 18 Fp2
-// products on pairs 0..17
-DEV void f12_mul_wide(Fp12& r, const Fp12& x, const Fp12& y) {
-    const int j = pair_idx() % 18;
+// products on pairs 0..17 — f12w_operands picks pair j's two factors, f12w_assemble combines the
+// products (so a caller can run other independent products on pairs 18..31 in the same call)
+DEV void f12w_operands(Fp2& o1, Fp2& o2, int j, const Fp12& x, const Fp12& y) {
+    j %= 18;
     const int m = j / 3, p = j % 3;
     Fp4 U, V;
     {
@@ -250,35 +255,47 @@ DEV void f12_mul_wide(Fp12& r, const Fp12& x, const Fp12& y) {
         V.a = f2_pick(m, va, 6);
         V.b = f2_pick(m, vb, 6);
     }
-    Fp2 o1 = U.a, o2 = V.a, s1, s2, prod;
+    Fp2 s1, s2;
+    o1 = U.a;
+    o2 = V.a;
     f2_add_lz(s1, U.a, U.b);
     f2_add_lz(s2, V.a, V.b);
     o1.c = fp_sel(p == 1, U.b.c, o1.c);
     o2.c = fp_sel(p == 1, V.b.c, o2.c);
     o1.c = fp_sel(p == 2, s1.c, o1.c);
     o2.c = fp_sel(p == 2, s2.c, o2.c);
-    f2_mul(prod, o1, o2);
+}
+DEV void f12w_assemble(Fp12& r, const Fp2& prod, int base = 0) {
     Fp4 t0, t1, t2, s, w, ra, rb, rc;
-    f4_from_products(t0, bcast_f2(prod, 0), bcast_f2(prod, 1), bcast_f2(prod, 2));
-    f4_from_products(t1, bcast_f2(prod, 3), bcast_f2(prod, 4), bcast_f2(prod, 5));
-    f4_from_products(t2, bcast_f2(prod, 6), bcast_f2(prod, 7), bcast_f2(prod, 8));
-    f4_from_products(s, bcast_f2(prod, 9), bcast_f2(prod, 10), bcast_f2(prod, 11));  // (b + c)(b' + c')
+    f4_from_products(t0, bcast_f2(prod, base + 0), bcast_f2(prod, base + 1), bcast_f2(prod, base + 2));
+    f4_from_products(t1, bcast_f2(prod, base + 3), bcast_f2(prod, base + 4), bcast_f2(prod, base + 5));
+    f4_from_products(t2, bcast_f2(prod, base + 6), bcast_f2(prod, base + 7), bcast_f2(prod, base + 8));
+    // (b + c)(b' + c')
+    f4_from_products(s, bcast_f2(prod, base + 9), bcast_f2(prod, base + 10), bcast_f2(prod, base + 11));
     f4_sub(s, s, t1);
     f4_sub(s, s, t2);
     f4_mul_s(s, s);
     f4_add(ra, s, t0);
-    f4_from_products(s, bcast_f2(prod, 12), bcast_f2(prod, 13), bcast_f2(prod, 14));  // (a + b)(a' + b')
+    // (a + b)(a' + b')
+    f4_from_products(s, bcast_f2(prod, base + 12), bcast_f2(prod, base + 13), bcast_f2(prod, base + 14));
     f4_sub(s, s, t0);
     f4_sub(s, s, t1);
     f4_mul_s(w, t2);
     f4_add(rb, s, w);
-    f4_from_products(s, bcast_f2(prod, 15), bcast_f2(prod, 16), bcast_f2(prod, 17));  // (a + c)(a' + c')
+    // (a + c)(a' + c')
+    f4_from_products(s, bcast_f2(prod, base + 15), bcast_f2(prod, base + 16), bcast_f2(prod, base + 17));
     f4_sub(s, s, t0);
     f4_sub(s, s, t2);
     f4_add(rc, s, t1);
     r.a = ra;
     r.b = rb;
     r.c = rc;
+}
+DEV void f12_mul_wide(Fp12& r, const Fp12& x, const Fp12& y) {
+    Fp2 o1, o2, prod;
+    f12w_operands(o1, o2, pair_idx(), x, y);
+    f2_mul(prod, o1, o2);
+    f12w_assemble(r, prod);
 }
 
 // = f12_cyc_sqr (Granger-Scott): f4_sqr of a, b, c as 6 products on pairs 0..5 (pair 2m: ab,
@@ -488,6 +505,169 @@ __global__ __launch_bounds__(64, 1) void k_fexp1(uint32_t* __restrict__ fbuf, ui
     fexp_out(1, 0, scratch, flags, verdicts, gt_out, threadIdx.x < 2);
 }
 
+// ================================================================ wide Miller loop
+// The RLC fold's 16 window pairs (fold.hip): few, so each runs alone on a wave in the wide form of
+// k_fexp1 — the 32 lane pairs hold the same values and a step's independent Fp2 products (pairing.inc
+// line_dbl / line_add / eval_line / f12_mul_line, the same formulas) are spread over them, one
+// product a pair, results gathered with shuffles.  A doubling iteration is three product latencies:
+//   A: f^2 (pairs 0..17) with line_dbl's X Y, Y^2, Z^2, (Y + Z)^2, X^2 (pairs 18..22);
+//   B: T's a (b - 3e), e^2, g^2, b h (pairs 0..3) with the line's evaluation at P (pairs 4..6);
+//   C: f times the line as a full Fp12 (A + C w^2).
+// An addition step is four: Q_y Z, Q_x Z | theta^2, lambda^2, theta Q_x, lambda Q_y | lambda d, Z c,
+// X d and the evaluation | T's four products with f times the line (pairs 4..21).
+// P (slots S_P1..+2) is in evaluation form (X Z, Y, Z^3); an Fp factor multiplies as the Fp2 (k, 0).
+DEV Fp2 f2_of_fp(const Fp& k) {
+    Fp z;
+    fp_zero(z);
+    Fp2 r;
+    r.c = fp_sel(half_id() != 0, z, k);
+    return r;
+}
+// pair j's operands: opts1[j], opts2[j] for j < n (pair-uniform j)
+DEV void pick2(Fp2& o1, Fp2& o2, int j, const Fp2* a, const Fp2* b, int n) {
+    for (int k = 0; k < n; k++) {
+        o1.c = fp_sel(j == k, a[k].c, o1.c);
+        o2.c = fp_sel(j == k, b[k].c, o2.c);
+    }
+}
+DEV void line_fp12(Fp12& L, const Fp2& a0, const Fp2& a2, const Fp2& a3) {  // A + C w^2 (pairing.inc)
+    L.a.a = a0;
+    L.a.b = a3;
+    f2_zero(L.b.a);
+    f2_zero(L.b.b);
+    L.c.a = a2;
+    f2_zero(L.c.b);
+}
+
+__global__ __launch_bounds__(64, 1) void k_miller_wide(size_t n, const uint32_t* __restrict__ prep,
+                                                    const uint32_t* __restrict__ flags, uint32_t* __restrict__ fout,
+                                                    size_t fstride, size_t foff) {
+    const size_t i = blockIdx.x;  // the pair of this wave (wave-uniform)
+    if (i >= n) return;
+    const int j = pair_idx();
+    const Soa S{const_cast<uint32_t*>(prep), n};
+    Fp12 f;
+    f12_one(f);
+    if (!(flags[i] & 5u)) {
+        Aff<Fp2> Q;
+        ld_f2(Q.x, S, S_Q1, i);
+        ld_f2(Q.y, S, S_Q1 + 2, i);
+        Fp px, py, pz;
+        cc::ld_fp(px, S, S_P1, i);
+        cc::ld_fp(py, S, S_P1 + 1, i);
+        cc::ld_fp(pz, S, S_P1 + 2, i);
+        const Fp2 PX = f2_of_fp(px), PY = f2_of_fp(py), PZ = f2_of_fp(pz);
+        G2Proj T;
+        T.x = Q.x;
+        T.y = Q.y;
+        f2_one(T.z);
+#pragma unroll 1
+        for (int b = 62; b >= 0; b--) {
+            Fp2 o1, o2, pr, l0, l2c, l3c;
+            {  // A
+                f12w_operands(o1, o2, j, f, f);
+                Fp2 yz;
+                f2_add_lz(yz, T.y, T.z);
+                const Fp2 a1[5] = {T.x, T.y, T.z, yz, T.x}, a2[5] = {T.y, T.y, T.z, yz, T.x};
+                pick2(o1, o2, j - 18, a1, a2, 5);
+                f2_mul(pr, o1, o2);
+                f12w_assemble(f, pr);
+            }
+            Fp2 a = bcast_f2(pr, 18), bb = bcast_f2(pr, 19), c = bcast_f2(pr, 20), h = bcast_f2(pr, 21),
+                t = bcast_f2(pr, 22), e, ff, g;
+            f2_half(a, a);
+            f2_sub(h, h, bb);
+            f2_sub(h, h, c);
+            f2_mul_xi(e, c);
+            f2_mul12(e, e);  // e = 3 b' Z^2
+            f2_dbl(ff, e);
+            f2_add(ff, ff, e);
+            f2_add(g, bb, ff);
+            f2_half(g, g);
+            f2_sub(l0, e, bb);
+            f2_dbl(l2c, t);
+            f2_add(l2c, l2c, t);
+            f2_neg(l3c, h);
+            {  // B
+                Fp2 bmf;
+                f2_sub(bmf, bb, ff);
+                const Fp2 a1[7] = {a, e, g, bb, l0, l2c, l3c}, a2[7] = {bmf, e, g, h, PZ, PX, PY};
+                o1 = a1[0];
+                o2 = a2[0];
+                pick2(o1, o2, j, a1, a2, 7);
+                f2_mul(pr, o1, o2);
+            }
+            T.x = bcast_f2(pr, 0);
+            {
+                const Fp2 e2 = bcast_f2(pr, 1);
+                T.y = bcast_f2(pr, 2);
+                f2_sub(T.y, T.y, e2);
+                f2_sub(T.y, T.y, e2);
+                f2_sub(T.y, T.y, e2);
+            }
+            T.z = bcast_f2(pr, 3);
+            {  // C
+                Fp12 L;
+                line_fp12(L, bcast_f2(pr, 4), bcast_f2(pr, 5), bcast_f2(pr, 6));
+                f12_mul_wide(f, f, L);
+            }
+            if (!((X_ABS >> b) & 1ull)) continue;
+            // addition step (pairing.inc line_add)
+            Fp2 theta, lambda;
+            {  // D1
+                const Fp2 a1[2] = {Q.y, Q.x}, a2[2] = {T.z, T.z};
+                o1 = a1[0];
+                o2 = a2[0];
+                pick2(o1, o2, j, a1, a2, 2);
+                f2_mul(pr, o1, o2);
+                f2_sub(theta, T.y, bcast_f2(pr, 0));
+                f2_sub(lambda, T.x, bcast_f2(pr, 1));
+            }
+            {  // D2
+                const Fp2 a1[4] = {theta, lambda, theta, lambda}, a2[4] = {theta, lambda, Q.x, Q.y};
+                o1 = a1[0];
+                o2 = a2[0];
+                pick2(o1, o2, j, a1, a2, 4);
+                f2_mul(pr, o1, o2);
+            }
+            c = bcast_f2(pr, 0);
+            const Fp2 d = bcast_f2(pr, 1);
+            f2_sub(l0, bcast_f2(pr, 2), bcast_f2(pr, 3));
+            f2_neg(l2c, theta);
+            l3c = lambda;
+            {  // D3
+                const Fp2 a1[6] = {lambda, T.z, T.x, l0, l2c, l3c}, a2[6] = {d, c, d, PZ, PX, PY};
+                o1 = a1[0];
+                o2 = a2[0];
+                pick2(o1, o2, j, a1, a2, 6);
+                f2_mul(pr, o1, o2);
+            }
+            e = bcast_f2(pr, 0);
+            ff = bcast_f2(pr, 1);
+            g = bcast_f2(pr, 2);
+            f2_add(h, e, ff);
+            f2_sub(h, h, g);
+            f2_sub(h, h, g);
+            {  // D4: T's four products on pairs 0..3, f times the line on pairs 4..21
+                Fp12 L;
+                line_fp12(L, bcast_f2(pr, 3), bcast_f2(pr, 4), bcast_f2(pr, 5));
+                Fp2 gmh;
+                f2_sub(gmh, g, h);
+                f12w_operands(o1, o2, j - 4, f, L);
+                const Fp2 a1[4] = {lambda, theta, e, T.z}, a2[4] = {h, gmh, T.y, e};
+                pick2(o1, o2, j, a1, a2, 4);
+                f2_mul(pr, o1, o2);
+                T.x = bcast_f2(pr, 0);
+                f2_sub(T.y, bcast_f2(pr, 1), bcast_f2(pr, 2));
+                T.z = bcast_f2(pr, 3);
+                f12w_assemble(f, pr, 4);
+            }
+        }
+        f12_conj(f, f);
+    }
+    if (threadIdx.x < 2) st_f12(Soa{fout, fstride}, foff + i, f);
+}
+
 }  // namespace pl
 }  // namespace cc
 
@@ -503,5 +683,16 @@ extern "C" int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint
     if (n > 1) return cck_fexp_q(n, d_f, d_flags, d_verdicts, d_gt, st);
     // one element (the RLC batch's combined product): latency-bound, the wide one-wave form
     hipLaunchKernelGGL(cc::pl::k_fexp1, dim3(1), dim3(64), 0, st, d_f, d_scratch, d_flags, d_verdicts, d_gt);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the RLC fold's window pairs: pair i = SoA element i of n (Q: slots S_Q1.., P: S_P1.. in evaluation
+// form; flags bit 0 / 2: skip), one wave each; Miller value i to element foff + i of stride fstride
+extern "C" int cck_miller_wide(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
+                               size_t fstride, size_t foff, hipStream_t st) {
+    if (!n) return 0;
+    if (fstride < foff + n) return -1;
+    hipLaunchKernelGGL(cc::pl::k_miller_wide, dim3((unsigned)n), dim3(64), 0, st, n, d_prep, d_flags, d_f, fstride,
+                       foff);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -73,6 +73,18 @@ DEV void ft_add_lz(lz::JG& acc, const uint32_t k[8], const uint32_t* __restrict_
     }
 }
 
+// storage form (x R, R = 2^406, canonical) -> the lazy field's form as a canonical 12 x 32 value
+// (x R', R' = 2^392): fp_mul by 2^392 mod p.  Table entries and the RLC fold's points are stored so,
+// and the lazy sums read them with from_fp alone.
+DEV void fp_to_lazy_form(Fp& v) {
+    constexpr uint32_t C[NL] = {0x0347fcb8u, 0x19d80000u, 0x6d2002b1u, 0x12e00cdeu, 0xa2090c72u, 0x37669f83u,
+                                0xda0f73e0u, 0x09b09b42u, 0x8f1297bbu, 0xa7c515d9u, 0xfcfa012cu, 0x0577a659u};  // 2^392 mod p
+    Fp c;
+#pragma unroll
+    for (int j = 0; j < NL; j++) c.v[j] = C[j];
+    fp_mul(v, v, c);
+}
+
 // a G2 entry of a lazy-form table back to the storage form (one-lane consumers of the verkey tables:
 // the RLC fold's fixed points in SigG1 mode): x R' -> x R, times 2^14 = R^2 / R' (fp_mul by 2^420 mod p)
 DEV void g2_entry_from_lazy_form(Aff<Fp2>& e) {

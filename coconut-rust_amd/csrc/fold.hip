@@ -18,7 +18,8 @@
 //
 //   k_fold_count / k_fold_scan / k_fold_scatter : counting sort of the (w, i) digits into 2,048
 //                                                 bucket lists, each padded to FS-entry chunks
-//   k_fold_sum<F>                               : one lane per chunk: mixed additions of its points
+//   k_fold_sum_g1                               : one lane per chunk: mixed additions of its points
+//                                                 (lazy field: the fold points come in its form)
 //   k_fold_reduce<F>                            : one wave per bucket: chunk partials, butterfly
 //   k_fold_window<F>                            : one wave per window: S_w, affine
 //   k_fold_sum_g2pl / k_fold_reduce_g2pl /      : the same for G2 buckets (SigG2) on the pair-lane
@@ -26,7 +27,8 @@
 //                                                 per bucket or window, 2 waves/SIMD where the one-lane
 //                                                 G2 forms need 448-512 registers (1 wave/SIMD)
 //   k_fold_fixed<F>                             : the fixed points P_w (once per verkey)
-// X_i = -sigma_2,i (AoS affine, written by the RLC prep); S_w lands in the pseudo-credentials' prep
+// X_i = -sigma_2,i (AoS affine in the lazy field's form, fixed.h fp_to_lazy_form; written by the RLC
+// prep); S_w lands in the pseudo-credentials' prep
 // SoA (soa.h slots, stride FW; window w = pseudo-credential w, pair 0) as the Q side (SigG2: S in G2)
 // or the P side (SigG1: S in G1), P_w on the other side.
 #include "codec.h"
@@ -143,26 +145,26 @@ __global__ __launch_bounds__(256) void k_fold_scatter(size_t n, const int8_t* __
     }
 }
 
-// one lane per FS-entry chunk (all of one bucket): Jacobian partial sum of its signed points
-template <class F>
-__global__ __launch_bounds__(256) void k_fold_sum(size_t maxchunks, const uint32_t* __restrict__ off,
-                                                  const uint32_t* __restrict__ list, const uint32_t* __restrict__ pts,
-                                                  uint32_t* __restrict__ part) {
-    constexpr int AW = sizeof(Aff<F>) / 4, JW = sizeof(Jac<F>) / 4;
+// one lane per FS-entry chunk (all of one bucket): Jacobian partial sum of its signed G1 points (the
+// fold points are in the lazy field's form: mixed additions on the lazy field, curve_lz.h), written in
+// the storage form
+__global__ __launch_bounds__(256) void k_fold_sum_g1(size_t maxchunks, const uint32_t* __restrict__ off,
+                                                     const uint32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ pts, uint32_t* __restrict__ part) {
+    constexpr int AW = sizeof(Aff<Fp>) / 4, JW = sizeof(Jac<Fp>) / 4;
     const size_t c = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (c >= maxchunks || c * FS >= off[FB]) return;
-    Jac<F> acc;
-    jac_set_inf(acc);
+    lz::JG acc = lz::jg_inf();
 #pragma unroll 1
     for (int e = 0; e < FS; e++) {
         const uint32_t v = list[c * FS + e];
         if (v == PAD) continue;
-        Aff<F> a;
-        ld_aff_aos<F>(a, pts + (size_t)(v & 0x7fffffffu) * AW);
-        if (v >> 31) FT<F>::neg(a.y, a.y);
-        jac_add_aff(acc, acc, a);
+        Aff<Fp> a;
+        ld_aff_aos<Fp>(a, pts + (size_t)(v & 0x7fffffffu) * AW);
+        const auto y = lz::from_fp(a.y);
+        acc = lz::jg_add_aff(acc, lz::AG{lz::from_fp(a.x), lz::sel((v >> 31) != 0, lz::neg(y), y)});
     }
-    st_jac_aos<F>(part + c * JW, acc);
+    st_jac_aos<Fp>(part + c * JW, lz::jg_to(acc));
 }
 
 // one wave per bucket: lane-strided sum of the bucket's chunk partials, butterfly across the wave;
@@ -238,20 +240,23 @@ __global__ __launch_bounds__(256, 2) void k_fold_sum_g2pl(size_t maxchunks, cons
     const size_t c = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // pair-uniform
     const int h = (int)pl::half_id();
     if (c >= maxchunks || c * FS >= off[FB]) return;
-    Jac<pl::Fp2> acc;
-    jac_set_inf(acc);
+    lz::JL acc = lz::jl_inf();  // the lazy pair-lane field (curve_lz.h); the points are in its form
 #pragma unroll 1
     for (int e = 0; e < FS; e++) {
-        const uint32_t v = list[c * FS + e];
+        const uint32_t v = list[c * FS + e];  // pair-uniform
         if (v == PAD) continue;
         const uint32_t* p = pts + (size_t)(v & 0x7fffffffu) * AW;
-        Aff<pl::Fp2> a;
-        pl::ld_f2_aos(a.x, p);
-        pl::ld_f2_aos(a.y, p + 2 * NL);
-        if (v >> 31) pl::f2_neg(a.y, a.y);
-        jac_add_aff(acc, acc, a);
+        Fp x, y;
+#pragma unroll
+        for (int k = 0; k < NL; k++) {
+            x.v[k] = p[NL * h + k];
+            y.v[k] = p[2 * NL + NL * h + k];
+        }
+        const lz::F2<lz::AN, lz::BC> ly{lz::from_fp(y)};
+        const lz::F2<lz::AN, lz::BC> qy{lz::sel((v >> 31) != 0, lz::neg(ly).c, ly.c)};
+        acc = lz::jl_add_aff_c(acc, lz::F2<lz::AN, lz::BC>{lz::from_fp(x)}, qy);
     }
-    st_jac_aos<pl::Fp2>(part + c * JW + h * HW, acc);
+    st_jac_aos<pl::Fp2>(part + c * JW + h * HW, pl::jl_to_pl(acc));
 }
 
 // k_fold_reduce<Fp2> on the pair-lane Fp2: one wave (32 lane pairs) per bucket; bkt as part
@@ -320,6 +325,20 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 // work-buffer layout (32-bit words): cnt FB | off FB+1 | cur FB (+3) | list maxchunks*FS |
 // part maxchunks*JW (16-byte aligned) | bkt FB*JW
 static size_t fold_maxchunks(size_t n) { return (FW * n + (size_t)FB * (FS - 1)) / FS + 1; }
+struct FoldWork {
+    uint32_t *cnt, *off, *cur, *list, *part, *bkt;
+};
+static FoldWork fold_work(int mode, size_t n, uint32_t* d_work) {
+    const size_t mc = fold_maxchunks(n);
+    FoldWork w;
+    w.cnt = d_work;
+    w.off = w.cnt + FB;
+    w.cur = w.off + FB + 1;
+    w.list = w.cur + FB + 3;
+    w.part = reinterpret_cast<uint32_t*>(((uintptr_t)(w.list + mc * FS) + 15) & ~(uintptr_t)15);
+    w.bkt = w.part + mc * (mode == 0 ? sizeof(Jac<Fp2>) / 4 : sizeof(Jac<Fp>) / 4);
+    return w;
+}
 
 extern "C" {
 
@@ -334,19 +353,16 @@ int cck_fold_pseudo() { return FW; }
 // mode 0 (SigG2): X_i in G2 (AoS affine, 48 words), g~ in G1; mode 1: X_i in G1 (24 words), g~ in G2.
 // d_dig: [FW][n] int8 digits (0 for credentials to leave out).  fixed_ok = 0 recomputes P_w into
 // d_prep2 and their identity flags into d_finf (FW bytes); both persist between calls.
-// d_prep2: PREP_SLOTS x FW SoA; d_flags2: FW words (pair-0 skip flags of the pseudo-credentials).
+// d_prep2: PREP_SLOTS x FW SoA; d_flags2: FW words (pair-0 skip flags of the pseudo-credentials),
+// both written by cck_fold_window, which the host launches after this.
 int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok, int q,
              const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
              uint32_t* d_flags2, hipStream_t st) {
     if (!n) return -1;
     const size_t mc = fold_maxchunks(n);
-    uint32_t* cnt = d_work;
-    uint32_t* off = cnt + FB;
-    uint32_t* cur = off + FB + 1;
+    const FoldWork fw = fold_work(mode, n, d_work);
+    uint32_t *cnt = fw.cnt, *off = fw.off, *cur = fw.cur, *list = fw.list, *part = fw.part, *bkt = fw.bkt;
     uint8_t* finf = d_finf;
-    uint32_t* list = cur + FB + 3;
-    uint32_t* part = reinterpret_cast<uint32_t*>(((uintptr_t)(list + mc * FS) + 15) & ~(uintptr_t)15);
-    uint32_t* bkt = part + mc * (mode == 0 ? sizeof(Jac<Fp2>) / 4 : sizeof(Jac<Fp>) / 4);
     if (!fixed_ok) {
         if (mode == 0)
             hipLaunchKernelGGL(k_fold_fixed<Fp>, dim3(1), dim3(64), 0, st, q, d_table, wbits, d_binf, d_prep2, finf);
@@ -362,12 +378,23 @@ int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uin
     if (mode == 0) {
         hipLaunchKernelGGL(k_fold_sum_g2pl, dim3(nblocks(2 * mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
         hipLaunchKernelGGL(k_fold_reduce_g2pl, dim3(FB), dim3(64), 0, st, off, part, bkt);
-        hipLaunchKernelGGL(k_fold_window_g2pl, dim3(FW), dim3(64), 0, st, bkt, finf, d_prep2, d_flags2);
     } else {
-        hipLaunchKernelGGL(k_fold_sum<Fp>, dim3(nblocks(mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
+        hipLaunchKernelGGL(k_fold_sum_g1, dim3(nblocks(mc, 256)), dim3(256), 0, st, mc, off, list, d_pts, part);
         hipLaunchKernelGGL(k_fold_reduce<Fp>, dim3(FB), dim3(64), 0, st, off, part, bkt);
-        hipLaunchKernelGGL(k_fold_window, dim3(FW), dim3(64), 0, st, bkt, finf, d_prep2, d_flags2);
     }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the fold's last step, after cck_fold (16 waves, latency-bound: the host runs it beside other
+// work): the window sums S_w and the pseudo-credentials' prep SoA and flags
+int cck_fold_window(int mode, size_t n, uint32_t* d_work, const uint8_t* d_finf, uint32_t* d_prep2,
+                    uint32_t* d_flags2, hipStream_t st) {
+    if (!n) return -1;
+    uint32_t* bkt = fold_work(mode, n, d_work).bkt;
+    if (mode == 0)
+        hipLaunchKernelGGL(k_fold_window_g2pl, dim3(FW), dim3(64), 0, st, bkt, d_finf, d_prep2, d_flags2);
+    else
+        hipLaunchKernelGGL(k_fold_window, dim3(FW), dim3(64), 0, st, bkt, d_finf, d_prep2, d_flags2);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

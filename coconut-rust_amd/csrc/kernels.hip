@@ -133,14 +133,7 @@ __global__ __launch_bounds__(64) void k_table_pow2(int nbases, int wbits, const 
 }
 
 // x R (storage form) -> x R' (the lazy field's Montgomery form, fixed.h): times 2^392 / R = 2^-14
-DEV void g1_to_lazy_form(Fp& v) {
-    constexpr uint32_t C[NL] = {0x0347fcb8u, 0x19d80000u, 0x6d2002b1u, 0x12e00cdeu, 0xa2090c72u, 0x37669f83u,
-                                0xda0f73e0u, 0x09b09b42u, 0x8f1297bbu, 0xa7c515d9u, 0xfcfa012cu, 0x0577a659u};  // 2^392 mod p
-    Fp c;
-#pragma unroll
-    for (int j = 0; j < NL; j++) c.v[j] = C[j];
-    fp_mul(v, v, c);
-}
+DEV void g1_to_lazy_form(Fp& v) { fp_to_lazy_form(v); }
 // table entries: G1 always in the lazy form; G2 when the table's consumers are the pair-lane lazy sums
 // (verkey and issuer tables; cc_fixed_base_mul's one-lane tables stay in the storage form)
 DEV void to_lazy_form(Fp& v, int) { g1_to_lazy_form(v); }

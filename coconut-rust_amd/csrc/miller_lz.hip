@@ -9,8 +9,8 @@
 //   RLC mode keeps pair 0 of every credential (its second pairs are folded, fold.hip) and runs TWO
 //   credentials through the 2-pair loop (kTwin): the RLC only needs the product of the credentials'
 //   Miller values, and the shared squaring halves the Fp12 work per credential (5,696 Fp
-//   multiplications against 6,800 for a loop of its own).  The fold's 16 window pairs run one pair
-//   per loop (NP = 1).
+//   multiplications against 6,800 for a loop of its own).  The fold's 16 window pairs run in the
+//   wide one-wave form (fexp_pl.hip k_miller_wide).
 //
 // Representation boundary: the prep SoA holds canonical 12 x 32 values in R = 2^406 form.  The twist
 // points are moved to R' form once (in_r: T's start and the addition steps' Q).  The G1 evaluation
@@ -166,20 +166,19 @@ static __device__ __noinline__ void t_check(const Tw* T, const uint32_t* prep, s
 }  // namespace
 
 // prep: SoA slots of soa.h; flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 pr = O, bit4 pair-1 P = O
-// cst: SigG2 -> g~ affine (24 words); SigG1 -> g~ lines (68 x 72 words); unused by NP = 1 and kTwin
-// NP = 1: pair 0 only (the RLC fold's window pairs).  The Miller value of credential i goes to fout as
-// SoA element foff + i of stride fstride.  kTwin (NP = 2, RLC credentials): the one pair of credentials
-// 2j and 2j + 1, laid out as pairs 0 and 1 of element j (rlc.hip twin_slot; the second skipped when n
-// is odd); their product goes to element foff + j.  qcheck (one pair per credential, SigG2): each
-// credential's Q (sigma_1) gets the G2 subgroup test from the loop's own T (curve_pl.h
-// miller_t_in_subgroup); a failure sets *qcheck.
-template <int SIG, int NP, bool kTwin = false>
+// cst: SigG2 -> g~ affine (24 words); SigG1 -> g~ lines (68 x 72 words); unused by kTwin.
+// The Miller value of credential i goes to fout as SoA element foff + i of stride fstride.  kTwin (RLC
+// credentials): the one pair of credentials 2j and 2j + 1, laid out as pairs 0 and 1 of element j
+// (rlc.hip twin_slot; the second skipped when n is odd); their product goes to element foff + j.
+// qcheck (kTwin, SigG2): each credential's Q (sigma_1) gets the G2 subgroup test from the loop's own T
+// (curve_pl.h miller_t_in_subgroup); a failure sets *qcheck.
+template <int SIG, bool kTwin>
 __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __restrict__ prep,
                                                const uint32_t* __restrict__ flags, const uint32_t* __restrict__ cst,
                                                uint32_t* __restrict__ fout, size_t fstride, size_t foff,
                                                uint32_t* __restrict__ qcheck) {
-    static_assert(!kTwin || NP == 2, "twin: two credentials' pairs");
-    __shared__ int32_t lds[NP == 2 ? 2 * TP : 1][MB];
+    constexpr int NP = 2;  // pairs per loop
+    __shared__ int32_t lds[2 * TP][MB];
     const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // lane pair: credential (twin: pair)
     if (i >= (kTwin ? (n + 1) / 2 : n)) return;  // pair-uniform
     constexpr bool kSigG2 = SIG == 2;
@@ -200,17 +199,17 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
         ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, false};
     }
     const Soa S{const_cast<uint32_t*>(prep), n};
-    // NP = 1: T stays in registers; NP = 2: both T's parked in LDS between their uses
+    // both T's parked in LDS between their uses
     Tw T;
     {
         F2<AN, 17> qx, qy;
-        if ((kSigG2 || kTwin) && NP == 2) {  // pair 1's T: -sigma_2 (twin: the second credential's Q)
+        if (kSigG2 || kTwin) {  // pair 1's T: -sigma_2 (twin: the second credential's Q)
             ld_q(qx, qy, S, S_Q2, i);
             park(lds, 1, t_from(qx, qy));
         }
         ld_q(qx, qy, S, S_Q1, i);
         T = t_from(qx, qy);
-        if (NP == 2) park(lds, 0, T);
+        park(lds, 0, T);
     }
     F12S f = fit<AS, BF>(f12_one());
     const uint32_t* gl = cst;  // SigG1: next precomputed g~ line
@@ -225,13 +224,13 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
                 ln = ld_line(gl);
                 gl += 72;
             } else {
-                if (NP == 2) T = unpark(lds, k);
+                T = unpark(lds, k);
                 ln = fit_line(line_dbl(T));
-                if (NP == 2) park(lds, k, T);
+                park(lds, k, T);
             }
             g = fit<AS, BS>(eval_mul(g, ln, k ? ps1 : ps0, i, k ? skip1 : skip0));
         }
-        // NP >= 1 passes ran, so g holds an eval_mul result, whose type bound is BF
+        // both passes ran, so g holds an eval_mul result, whose type bound is BF
         f = narrow_to<BF>(g);
         if ((X_ABS >> b) & 1ull) {
 #pragma unroll 1
@@ -239,21 +238,20 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
                 const bool const_line = !kSigG2 && !kTwin && k == 1;
                 StepState st;
                 st.f = f;
-                if (!const_line) st.T = NP == 2 ? unpark(lds, k) : T;
+                if (!const_line) st.T = unpark(lds, k);
                 miller_add(&st, prep, n, k ? S_Q2 : S_Q1, i, const_line ? gl : nullptr, k ? ps1 : ps0,
                            k ? skip1 : skip0);
                 if (const_line) gl += 72;
-                else if (NP == 2) park(lds, k, st.T);
-                else T = st.T;
+                else park(lds, k, st.T);
                 f = st.f;
             }
         }
     }
-    if ((NP == 1 || kTwin) && kSigG2 && qcheck) {
+    if (kTwin && kSigG2 && qcheck) {
 #pragma unroll 1
         for (int k = 0; k < NP; k++) {
             if (k ? skip1 : skip0) continue;  // pair-uniform
-            const Tw Tk = NP == 2 ? unpark(lds, k) : T;
+            const Tw Tk = unpark(lds, k);
             t_check(&Tk, prep, n, k ? S_Q2 : S_Q1, i, qcheck);
         }
     }
@@ -273,26 +271,23 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
 #define CC_MILLER_LAUNCH cck_miller_lz_g1
 #endif
 
-// np: pairs per credential (1 or 2); twin (np = 1): two credentials per lane pair, one Miller value
-// (their product) per two credentials.  The m Miller values (m = n, twin: ceil(n / 2)) go to SoA
-// elements [foff, foff + m) of stride fstride (>= foff + m); d_qcheck (np = 1 or twin, SigG2, or
-// null): the sigma_1 subgroup test from the loop's T
-extern "C" int CC_MILLER_LAUNCH(int np, int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+// twin: two credentials per lane pair (their one pair each), one Miller value (their product) per
+// two credentials; otherwise two pairs per credential.  The m Miller values (m = n, twin:
+// ceil(n / 2)) go to SoA elements [foff, foff + m) of stride fstride (>= foff + m); d_qcheck (twin,
+// SigG2, or null): the sigma_1 subgroup tests from the loop's T
+extern "C" int CC_MILLER_LAUNCH(int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                                 const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff,
                                 uint32_t* d_qcheck, hipStream_t st) {
     if (!n) return 0;
     const size_t m = twin ? (n + 1) / 2 : n;
-    if (fstride < foff + m || (np != 1 && np != 2) || (twin && np != 1)) return -1;
+    if (fstride < foff + m) return -1;
     constexpr int MB = cc::lz::MB;
     dim3 g((unsigned)((2 * m + MB - 1) / MB)), b(MB);
     if (twin)
-        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, 2, true>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, true>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
                            fstride, foff, d_qcheck);
-    else if (np == 1)
-        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, 1>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f, fstride,
-                           foff, d_qcheck);
     else
-        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, 2>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f, fstride,
-                           foff, d_qcheck);
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, false>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+                           fstride, foff, d_qcheck);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

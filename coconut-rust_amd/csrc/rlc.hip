@@ -94,8 +94,12 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t b
         st_f2(S, twin_slot(S_Q1, S_Q2, i), i >> 1, a.x);
         st_f2(S, twin_slot(S_Q1, S_Q2, i) + 2, i >> 1, a.y);
     } else {
-        Aff<Fp2> m = a;
+        Aff<Fp2> m = a;  // the fold point, in the lazy field's form (fold.hip sums it there)
         f2_neg(m.y, m.y);
+        fp_to_lazy_form(m.x.a);
+        fp_to_lazy_form(m.x.b);
+        fp_to_lazy_form(m.y.a);
+        fp_to_lazy_form(m.y.b);
         st_aff_aos<Fp2>(pts + i * (sizeof(Aff<Fp2>) / 4), m);
     }
     fl |= pl::swp(fl);  // both decode flags on both lanes
@@ -167,6 +171,8 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, uint64_t b
         st_fp(S, twin_slot(S_P1, S_P2, i) + 1, i >> 1, a.y);
     } else {
         fp_neg(a.y, a.y);
+        fp_to_lazy_form(a.x);  // the fold point, in the lazy field's form (fold.hip sums it there)
+        fp_to_lazy_form(a.y);
         st_aff_aos<Fp>(pts + i * (sizeof(Aff<Fp>) / 4), a);
     }
     fl |= pl::swp(fl);

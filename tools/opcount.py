@@ -547,7 +547,7 @@ def mul_aff(g, base, k):
 
 # ---------------------------------------------------------------- verify (SigG2 shared verkey, pair prep)
 def verify_sigg2(cred, vk_aff, gtil_aff, q):
-    """k_prep_sigg2_pair -> k_miller<2,2> -> k_fexp.  Returns (verdict, gt, {kernel: M})."""
+    """k_prep_sigg2_pair -> k_miller<2,false> -> k_fexp.  Returns (verdict, gt, {kernel: M})."""
     counts = {}
     s1 = decode(G2, bytes.fromhex(cred["sigma1"]))
     s2 = decode(G2, bytes.fromhex(cred["sigma2"]))
@@ -581,7 +581,7 @@ def verify_sigg2(cred, vk_aff, gtil_aff, q):
 
 
 def verify_sigg1(cred, vk_aff, gtil_aff, q):
-    """k_prep_sigg1<true> -> k_miller<1,2> (g~ lines precomputed) -> k_fexp."""
+    """k_prep_sigg1<true> -> k_miller<1,false> (g~ lines precomputed) -> k_fexp."""
     counts = {}
     s1 = decode(G1, bytes.fromhex(cred["sigma1"]))
     s2 = decode(G1, bytes.fromhex(cred["sigma2"]))
@@ -753,7 +753,7 @@ def enc(g, a):
 
 # ---------------------------------------------------------------- PoK verify (k_prep_pok, SigG2)
 def pok_sigg2(d, p, vk_aff, gtil):
-    """k_prep_pok<Fp2, Fp> -> k_miller<2,2> -> k_fexp."""
+    """k_prep_pok<Fp2, Fp> -> k_miller<2,false> -> k_fexp."""
     counts = {}
     q, rev = d["q"], d["revealed"]
     X, Ys = vk_aff
@@ -827,10 +827,11 @@ RLC_N, RLC_PSEUDO = 131072, 16  # credentials per GPU (config 3), fold pseudo-cr
 
 
 def rlc_sigg2(cred, vk_aff, gtil_aff, q, rnd):
-    """k_rlc_check_sigg2 + k_rlc_msm_sigg2 -> fold (fold.hip) -> k_miller<2,2,true> (two
+    """k_rlc_check_sigg2 + k_rlc_msm_sigg2 -> fold (fold.hip) -> k_miller<2,true> (two
     credentials' first pairs per shared-squaring loop; + the 16 window pseudo-credentials' one-pair
-    k_miller<2,1>) -> k_f12_reduce over (RLC_N / 2 + RLC_PSEUDO) values; the batch's one final
-    exponentiation is amortised over RLC_N.  delta is a random 128-bit value here (the counts do not depend on the key stream)."""
+    loops, fexp_pl.hip k_miller_wide: the same products, spread over a wave) -> k_f12_reduce over
+    (RLC_N / 2 + RLC_PSEUDO) values; the batch's one final exponentiation is amortised over RLC_N.
+    delta is a random 128-bit value here (the counts do not depend on the key stream)."""
     counts = {}
     s1 = decode(G2, bytes.fromhex(cred["sigma1"]))
     s2 = decode(G2, bytes.fromhex(cred["sigma2"]))
