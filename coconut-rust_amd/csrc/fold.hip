@@ -21,7 +21,7 @@
 //   k_fold_sum_g1                               : one lane per chunk: mixed additions of its points
 //                                                 (lazy field: the fold points come in its form)
 //   k_fold_reduce<F>                            : one wave per bucket: chunk partials, butterfly
-//   k_fold_window<F>                            : one wave per window: S_w, affine
+//   k_fold_window                               : one wave per window: S_w (lazy field), affine
 //   k_fold_sum_g2pl / k_fold_reduce_g2pl /      : the same for G2 buckets (SigG2) on the pair-lane
 //   k_fold_window_g2pl                            Fp2 (curve_pl.h): one LANE PAIR per chunk / 32 pairs
 //                                                 per bucket or window, 2 waves/SIMD where the one-lane
@@ -187,41 +187,30 @@ __global__ __launch_bounds__(64) void k_fold_reduce(const uint32_t* __restrict__
     if (threadIdx.x == 0) st_jac_aos<F>(bkt + (size_t)b * JW, acc);
 }
 
-// lane t's share of S_w = sum_d d B_d over the digits d = CK t + k + 1 (k < CK): U + [CK t] T with
-// U = sum_k (k + 1) B, T = sum_k B (running sums from the top digit down); ld(k, B) loads B.  t < 64.
-template <class F, int CK, class Ld>
-DEV Jac<F> window_share(int t, Ld ld) {
-    Jac<F> run, u, v;
-    jac_set_inf(run);
-    jac_set_inf(u);
-#pragma unroll 1
-    for (int k = CK - 1; k >= 0; k--) {
-        Jac<F> b;
-        ld(k, b);
-        jac_add(run, run, b);
-        jac_add(u, u, run);
-    }
-    jac_set_inf(v);
-#pragma unroll 1
-    for (int s = 5; s >= 0; s--) {  // [t] T, then [CK] of it
-        jac_dbl(v, v);
-        if ((t >> s) & 1) jac_add(v, v, run);
-    }
-#pragma unroll 1
-    for (int c = 1; c < CK; c <<= 1) jac_dbl(v, v);
-    jac_add(u, u, v);
-    return u;
-}
-
-// one wave per window (one lane per CK = 2 digits): S_w, affine, as pseudo-credential w (P side:
-// SigG1, S in G1); flags2[w]: skip the pair (S_w = O or P_w = O)
+// one wave per window (one lane per CK = 2 digits): lane t's share of S_w = sum_d d B_d over the
+// digits d = CK t + k + 1 (k < CK) is U + [CK t] T with U = sum_k (k + 1) B and T = sum_k B (running
+// sums from the top digit down), on the lazy field; a butterfly adds the lanes.  S_w, affine, becomes
+// pseudo-credential w (P side: SigG1, S in G1); flags2[w]: skip the pair (S_w = O or P_w = O)
 __global__ __launch_bounds__(64) void k_fold_window(const uint32_t* __restrict__ bkt, const uint8_t* __restrict__ fixed_inf,
                                                     uint32_t* __restrict__ prep2, uint32_t* __restrict__ flags2) {
     constexpr int JW = sizeof(Jac<Fp>) / 4, CK = FD / 64;
     const int w = blockIdx.x, t = threadIdx.x;
-    Jac<Fp> acc = window_share<Fp, CK>(t, [&](int k, Jac<Fp>& b) {
+    lz::JG run = lz::jg_inf(), u = lz::jg_inf(), v = lz::jg_inf();
+#pragma unroll 1
+    for (int k = CK - 1; k >= 0; k--) {
+        Jac<Fp> b;
         ld_jac_aos<Fp>(b, bkt + (size_t)(w * FD + CK * t + k) * JW);
-    });
+        run = lz::jg_add(run, lz::jg_from(b));
+        u = lz::jg_add(u, run);
+    }
+#pragma unroll 1
+    for (int s = 5; s >= 0; s--) {  // [t] run (t < 64), then [CK] of it
+        v = lz::jg_dbl(v);
+        if ((t >> s) & 1) v = lz::jg_add(v, run);
+    }
+#pragma unroll 1
+    for (int c = 1; c < CK; c <<= 1) v = lz::jg_dbl(v);
+    Jac<Fp> acc = lz::jg_to(lz::jg_add(u, v));
     lane_group_sum<Fp, 64>(acc);
     if (threadIdx.x != 0) return;
     Aff<Fp> a;
@@ -280,16 +269,30 @@ __global__ __launch_bounds__(64, 2) void k_fold_reduce_g2pl(const uint32_t* __re
 }
 
 // k_fold_window for G2 buckets on the pair-lane Fp2 (one lane pair per CK = 4 digits), S_w as the
-// Q side (SigG2)
+// Q side (SigG2).  The lane pair's share runs on the lazy pair-lane field (curve_lz.h): latency-bound
+// (16 waves), and beside the delta MSM's waves every dependent step counts.
 __global__ __launch_bounds__(64, 2) void k_fold_window_g2pl(const uint32_t* __restrict__ bkt,
                                                            const uint8_t* __restrict__ fixed_inf,
                                                            uint32_t* __restrict__ prep2, uint32_t* __restrict__ flags2) {
     constexpr int JW = sizeof(Jac<Fp2>) / 4, HW = sizeof(Jac<pl::Fp2>) / 4, CK = FD / 32;
     const int w = blockIdx.x, t = threadIdx.x >> 1;  // pair-uniform
     const int h = (int)pl::half_id();
-    Jac<pl::Fp2> acc = window_share<pl::Fp2, CK>(t, [&](int k, Jac<pl::Fp2>& b) {
+    lz::JL run = lz::jl_inf(), u = lz::jl_inf(), v = lz::jl_inf();
+#pragma unroll 1
+    for (int k = CK - 1; k >= 0; k--) {  // running sums: run = sum B, u = sum (k + 1) B
+        Jac<pl::Fp2> b;
         ld_jac_aos<pl::Fp2>(b, bkt + (size_t)(w * FD + CK * t + k) * JW + h * HW);
-    });
+        run = lz::jl_add(run, pl::jl_from_pl(b));
+        u = lz::jl_add(u, run);
+    }
+#pragma unroll 1
+    for (int s = 4; s >= 0; s--) {  // [t] run (t < 32), then [CK] of it
+        v = lz::jl_dbl(v);
+        if ((t >> s) & 1) v = lz::jl_add(v, run);
+    }
+#pragma unroll 1
+    for (int c = 1; c < CK; c <<= 1) v = lz::jl_dbl(v);
+    Jac<pl::Fp2> acc = pl::jl_to_pl(lz::jl_add(u, v));
     pl::pair_group_sum<64>(acc);
     if (threadIdx.x >= 2) return;
     Aff<pl::Fp2> a;
