@@ -206,7 +206,7 @@ struct StreamOrder {
 
 // mode 0 (SigG2): d_const = g~ affine G1 (24 words); mode 1 (SigG1): g~ Miller lines (68 x 72 words).
 // Pairing kernels run one credential per lane pair (tower_pl.h).  Miller values go to SoA elements
-// [foff, foff + n) of stride fstride (default: n, 0).
+// [0, n) of stride n.
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                       uint32_t* d_f, hipStream_t st) {
     return mode == 0 ? cck_miller_lz_g2(0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st)
@@ -630,13 +630,13 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     HIPCK(hipMemcpyAsync(c->rlc_key.p, c->rlc_key_host, 32, hipMemcpyHostToDevice, st));
     HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
-    auto prep_part = [&](int part, hipStream_t s) {
+    auto prep_part = [&](int part) {
         return cck_prep_rlc(c->mode, part, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
                             c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
                             c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), c->rlc_pts.as<uint32_t>(),
-                            c->rlc_dig.as<int8_t>(), s);
+                            c->rlc_dig.as<int8_t>(), st);
     };
-    KCK(prep_part(0, st));  // decode, subgroup checks, the fold's inputs
+    KCK(prep_part(0));  // decode, subgroup checks, the fold's inputs
     if (!c->vk_subgroup) {
         // a verkey / g~ point outside the subgroup: the linear-combination argument does not hold,
         // so the batch is never accepted here and the caller verifies per credential (exact)
@@ -663,7 +663,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
                         c->rlc_flags2.as<uint32_t>(), side));
     KCK(cck_miller_pairs(NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(), c->fbuf.as<uint32_t>(), N, M,
                          side));
-    KCK(prep_part(1, st));  // delta X~ + sum (delta m_j) Y~_j
+    KCK(prep_part(1));  // delta X~ + sum (delta m_j) Y~_j
     if (side != st) {
         HIPCK(hipEventRecord(c->ev_join, side));
         HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));

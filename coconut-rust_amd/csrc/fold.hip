@@ -28,9 +28,9 @@
 //                                                 G2 forms need 448-512 registers (1 wave/SIMD)
 //   k_fold_fixed<F>                             : the fixed points P_w (once per verkey)
 // X_i = -sigma_2,i (AoS affine in the lazy field's form, fixed.h fp_to_lazy_form; written by the RLC
-// prep); S_w lands in the pseudo-credentials' prep
-// SoA (soa.h slots, stride FW; window w = pseudo-credential w, pair 0) as the Q side (SigG2: S in G2)
-// or the P side (SigG1: S in G1), P_w on the other side.
+// prep); S_w lands in the pseudo-credentials' prep SoA (soa.h slots, stride FW; window w =
+// pseudo-credential w, pair 0) as the Q side (SigG2: S in G2) or the P side (SigG1: S in G1), P_w on
+// the other side.
 #include "codec.h"
 #include "curve_pl.h"
 #include "fixed.h"
