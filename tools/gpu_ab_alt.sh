@@ -9,6 +9,7 @@ MODE=${MODE:-rlc}
 TESTS=${TESTS:-tests}
 REPS=${REPS:-2}
 mkdir -p "$OUT"
+[ -f coconut-rust_amd/libcoconut_hip_prev.so ] || { echo "[abalt] no coconut-rust_amd/libcoconut_hip_prev.so (build the previous version there first)"; exit 2; }
 echo "[abalt] tests $TESTS"
 timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
 tail -1 "$OUT/pytest_gpu.log"
