@@ -63,6 +63,30 @@ def peak_mad_per_s():
     return best
 
 
+# Verkey-table window width each bench mode opts into (cc_set_table_bits).  The library's own default
+# stays within 4 GiB of HBM a context (18 bits at q = 6, 16 at q = 16); the bench asks for the widths
+# the round-3 numbers were measured with, and names the width and the GiB in its config.
+BENCH_VK_BITS = {"verify": 22, "verify-g1": 22, "rlc": 22, "pok": 20, "pok-g1": 20}
+
+
+def vk_bits_for(args):
+    return args.vk_bits if args.vk_bits is not None else BENCH_VK_BITS.get(args.mode, 0)
+
+
+def table_config(ctx, q):
+    """The verkey tables a context holds: window bits, GiB of HBM (q + 2 bases, fixed.h layout) and
+    whether the width was the bench's explicit choice or the library default."""
+    bits = ctx.table_bits()[0]
+    entry = 96 if int(ctx.mode) == 0 else 192  # affine OtherGroup entry: G1 (SigG2) / G2 (SigG1)
+    gib = (q + 2) * ((256 + bits - 1) // bits) * ((1 << bits) - 1) * entry / 2**30 if bits else 0.0
+    return {"verkey_table_bits": bits, "verkey_table_GiB": round(gib, 2)}
+
+
+def lib_info():
+    import coconut
+    return {"library": coconut.version(), "src_hash": coconut.source_hash()}
+
+
 def opcounts(key):
     with open(OPCOUNT) as f:
         return json.load(f)["configs"][key]["M_per_credential"]
@@ -366,8 +390,7 @@ def bench_verify(args, mode):
     batch = make_verify_batch(ctx, mode, n, q, seed=1000 + rank + 100 * mode)
     ctx.set_params(batch["g_tilde"])
     t_vk = time.perf_counter()
-    if args.vk_bits:
-        ctx.set_table_bits(args.vk_bits, 0)
+    ctx.set_table_bits(vk_bits_for(args), 0)
     ctx.set_verkey(batch["X"], batch["Y"])
     vk_ms = (time.perf_counter() - t_vk) * 1e3
     setup_s = time.perf_counter() - t_setup
@@ -443,7 +466,9 @@ def bench_verify(args, mode):
                     "k*(x+sum y m)*G built on the GPU; 1/16 corrupted, split evenly over " + ", ".join(CORRUPT_KINDS) + ")",
             "config": {"workload": f"config2: batch of {n:,} Signature::verify per GPU, msg_count=6, shared "
                                    f"aggregated verkey, {layout}",
-                       "credentials_per_gpu": n, "msg_count": q, "parallelism": f"shard-by-credential x{world}"},
+                       "credentials_per_gpu": n, "msg_count": q, "parallelism": f"shard-by-credential x{world}",
+                       **table_config(ctx, q), "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
+            **lib_info(),
             "pairings_per_s": round(2 * value, 1),
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
@@ -486,8 +511,7 @@ def bench_rlc(args):
     ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
     batch = make_verify_batch(ctx, 0, n, q, seed=3000 + rank, bad_every=0)
     ctx.set_params(batch["g_tilde"])
-    if args.vk_bits:
-        ctx.set_table_bits(args.vk_bits, 0)
+    ctx.set_table_bits(vk_bits_for(args), 0)
     ctx.set_verkey(batch["X"], batch["Y"])
     d_s1, d_s2, d_m = to_dev(batch["s1"], dev), to_dev(batch["s2"], dev), to_dev(batch["msgs"], dev)
     eng = DeviceEngine(ctx, n, q, d_s1, d_s2, d_m, base_index=rank * n)
@@ -545,7 +569,9 @@ def bench_rlc(args):
             "data": "synthetic (seeded; all valid, reject path checked after timing)",
             "config": {"workload": "config3: RLC batch verify, msg_count=16, shared verkey, SigG2",
                        "credentials_per_gpu": n, "msg_count": q,
-                       "parallelism": f"shard-by-credential x{world} + RCCL all-gather of Fp12 partials"},
+                       "parallelism": f"shard-by-credential x{world} + RCCL all-gather of Fp12 partials",
+                       **table_config(ctx, q), "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
+            **lib_info(),
             "phase_ms": {"prep": round(phase_ms[0], 3), "miller": round(phase_ms[1], 3),
                          "reduce": round(phase_ms[2], 3)},
             "us_per_credential": round(elapsed / args.steps / n * 1e6, 4),
@@ -613,8 +639,9 @@ def main():
     ap.add_argument("--n", type=int, default=0, help="credentials per GPU per step (0 = the config's size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) rate")
-    ap.add_argument("--vk-bits", type=int, default=0,
-                    help="verkey table window width (cc_set_table_bits; 0 = the library's choice)")
+    ap.add_argument("--vk-bits", type=int, default=None,
+                    help="verkey table window width (cc_set_table_bits; 0 = the library's <= 4 GiB default; "
+                         "unset = the mode's opt-in width, BENCH_VK_BITS)")
     ap.add_argument("--mode", choices=["verify", "verify-g1", "rlc", "aggregate", "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
     args = ap.parse_args()
     if args.backend:

@@ -208,7 +208,8 @@ def bench_aggregate(args):
             "config": {"workload": f"config4: {n:,} credentials per GPU, t=67 of n=100 issuers, msg_count={q}, "
                                    + ("SigG1" if sigm else "SigG2"),
                        "credentials_per_gpu": n, "threshold": t, "issuers": 100,
-                       "parallelism": f"shard-by-credential x{world}"},
+                       "parallelism": f"shard-by-credential x{world}", "issuer_table_bits": ctx.table_bits()[1]},
+            **__import__("bench").lib_info(),
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 3),
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": round(ach / peak, 4),
@@ -272,8 +273,8 @@ def bench_pok(args):
     b = make_pok_batch(ctx, sigm, n, seed=5000 + rank)
     gen_s = time.perf_counter() - t0
     ctx.set_params(b["g_tilde"])
-    if args.vk_bits:
-        ctx.set_table_bits(args.vk_bits, 0)
+    from bench import vk_bits_for
+    ctx.set_table_bits(vk_bits_for(args), 0)
     ctx.set_verkey(b["X"], b["Y"])
     q, r, nresp = b["q"], len(b["revealed"]), b["nresp"]
     D = {k: to_dev(b[k], dev) for k in ("s1", "s2", "J", "T", "resp", "chal", "rev")}
@@ -309,7 +310,9 @@ def bench_pok(args):
             "data": "synthetic (seeded; proofs with known discrete logs built on the GPU; 1/16 bad response)",
             "config": {"workload": f"config5: {n:,} PoKOfSignatureProof::verify per GPU, q=32, revealed "
                                    f"{b['revealed']}, " + ("SigG1" if sigm else "SigG2"), "proofs_per_gpu": n,
-                       "parallelism": f"shard-by-proof x{world}"},
+                       "parallelism": f"shard-by-proof x{world}", **__import__("bench").table_config(ctx, q),
+                       "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
+            **__import__("bench").lib_info(),
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),

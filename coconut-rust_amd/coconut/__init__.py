@@ -6,6 +6,7 @@ Mirrors 3for/coconut-rust (`/root/reference/src/lib.rs:26-31` module list) for t
 importing this package on a machine without the built library raises immediately.
 """
 from .errors import CoconutError, CoconutErrorKind  # noqa: F401
+from ._lib import version, source_hash  # noqa: F401
 from .signature import (GroupMode, Params, Verkey, Signature, Context, verify_batch,  # noqa: F401
                         signature_aggregate_batch, verkey_aggregate_batch, verkey_aggregate_ids, fixed_base_mul, subgroup_check, hash_to_curve, hash_msg, params_new,
                         G1_GENERATOR, G2_GENERATOR)

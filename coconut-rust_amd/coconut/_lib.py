@@ -43,6 +43,7 @@ _SIGS = {
     "cc_device_error": (c_int, [c_p, c_p, ctypes.POINTER(ctypes.c_uint32)]),
     "cc_verify_batch": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int]),
     "cc_verify_batch_device": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p]),
+    "cc_verify_batch_pervk_device": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "cc_signature_aggregate_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p]),
     "cc_verkey_aggregate_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p]),
     "cc_pok_verify_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
@@ -74,6 +75,17 @@ for _name, (_res, _args) in _SIGS.items():
     _f = getattr(lib, _name)
     _f.restype = _res
     _f.argtypes = _args
+
+
+def version() -> str:
+    """cc_version(): library version and the source hash it was built from (tools/src_hash.py)."""
+    return lib.cc_version().decode()
+
+
+def source_hash() -> str:
+    """The 16-hex-digit source hash embedded at build time ("unknown" for a build outside the Makefile)."""
+    v = version()
+    return v.split(" src ", 1)[1].strip() if " src " in v else "unknown"
 
 
 def check(status: int, what: str = ""):

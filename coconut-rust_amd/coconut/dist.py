@@ -88,9 +88,12 @@ class DeviceEngine:
         self.stream = stream if stream is not None else torch.cuda.Stream(self.dev)
         self._sh = ctypes.c_void_p(self.stream.cuda_stream)
         # two partial / accept buffers: a pipelined caller's finish of batch i (finish_async, on its own
-        # stream) may still read one while the next partial writes the other
+        # stream) may still read one while the next partial writes the other.  A third partial issued
+        # before batch i's finish has run reuses batch i's slot: partial() then makes the engine's stream
+        # wait (on the device) for that finish's event, so the slot is never overwritten while read.
         self._parts = [torch.empty(PARTIAL_WORDS, dtype=torch.int32, device=self.dev) for _ in range(2)]
         self._accepts = [torch.zeros(1, dtype=torch.uint8, device=self.dev) for _ in range(2)]
+        self._slot_ev = [None, None]
         self._slot = 0
         self.part = self._parts[0]
         self.accept = self._accepts[0]
@@ -115,6 +118,9 @@ class DeviceEngine:
         self._slot ^= 1
         self.part = self._parts[self._slot]
         self._enter()
+        if self._slot_ev[self._slot] is not None:  # a finish_async still reading this slot
+            self.stream.wait_event(self._slot_ev[self._slot])
+            self._slot_ev[self._slot] = None
         self._check(self.lib.cc_rlc_partial_device(self.ctx.h, self.n, self.q, self.base_index, seed,
                                                    ctypes.c_void_p(self.d_s1.data_ptr()),
                                                    ctypes.c_void_p(self.d_s2.data_ptr()),
@@ -138,7 +144,9 @@ class DeviceEngine:
     def finish_async(self, allp, k: int):
         """cc_rlc_finish_device on the engine's second stream, NOT ordered before later work on the
         engine's main stream: the next batch's partial() can overlap this batch's final exponentiation.
-        Returns a callable that waits for the decision and returns it."""
+        Returns a callable that waits for the decision and returns it.  Any number of finishes may be
+        outstanding: the library runs the finishes of one context in call order, and a partial() that
+        reuses the slot of an unfinished batch waits for that batch's finish on the device."""
         import torch
         if self._fin_stream is None:
             self._fin_stream = torch.cuda.Stream(self.dev)
@@ -151,12 +159,18 @@ class DeviceEngine:
         self._check(self.lib.cc_rlc_finish_device(self.ctx.h, k, ctypes.c_void_p(allp.data_ptr()),
                                                   ctypes.c_void_p(acc.data_ptr()), None,
                                                   ctypes.c_void_p(fs.cuda_stream)), "cc_rlc_finish_device")
+        # the decision is copied out on the finish stream, so a later batch reusing this slot cannot
+        # change what result() returns
+        host = torch.empty(1, dtype=torch.uint8, pin_memory=True)
+        with torch.cuda.stream(fs):
+            host.copy_(acc, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(fs)
+        self._slot_ev[self._slot] = ev
 
         def result() -> bool:
             ev.synchronize()
-            return bool(acc.item())
+            return bool(host[0].item())
         return result
 
     def per_credential(self) -> np.ndarray:

@@ -165,7 +165,12 @@ class Context:
         if self._gtilde == g_tilde:
             return
         p, keep = buf(g_tilde)
-        check(lib.cc_set_params(self.h, p), "cc_set_params")
+        self._gtilde = None
+        try:
+            check(lib.cc_set_params(self.h, p), "cc_set_params")
+        except Exception:
+            self._vk = None  # a failed table rebuild leaves the C context without a verkey
+            raise
         self._gtilde = g_tilde
 
     def set_verkey(self, X: bytes, Y: Sequence[bytes]):

@@ -21,6 +21,7 @@
 #include "fr.h"
 #include "pairing.h"
 #include "soa.h"
+#include "straus.h"
 
 using namespace cc;
 
@@ -172,17 +173,6 @@ __host__ __device__ inline size_t straus_words(size_t t) {
     return t * 8 * (3 * FS * NL) + t * 8 * (FS * NL) + (t * 65 + 3) / 4;
 }
 
-// signed radix-16 digits of a canonical 255-bit scalar: 65 digits in [-8, 8], least significant first
-DEV void recode_w4(int8_t* d, const uint32_t k[8]) {
-    int carry = 0;
-#pragma unroll 1
-    for (int w = 0; w < 64; w++) {
-        int v = (int)((k[w >> 3] >> (4 * (w & 7))) & 0xfu) + carry;
-        carry = v > 8;
-        d[w] = (int8_t)(v - 16 * carry);
-    }
-    d[64] = (int8_t)carry;
-}
 
 
 // L lanes per task: lane l takes the bases k = l, l + L, ... (t = 67, L = 16: 4-5 bases per lane),
@@ -295,103 +285,7 @@ __global__ __launch_bounds__(256, 2) void k_msm_straus(size_t ntask, size_t t, c
     }
 }
 
-// G2 bases on the lazy pair-lane field (curve_lz.h): the same algorithm with ONE task lane per lane
-// PAIR (lane 2i + h holds half h of every Fp2 coordinate) and lazy radix-2^28 arithmetic (no conversion
-// per multiplication, carry-free additions, identity and exceptional cases tested on reduced values).
-// The pair form keeps a Jacobian G2 point in 3 Fp a lane (2 waves/SIMD) and halves each lane's share of
-// every Fp2 product; the one-lane G2 form needed 512 VGPRs.  NG pairs per task take the bases
-// k = pair, pair + NG, ...  Scratch per task (lazy words, each entry's two halves side by side):
-// 8t Jacobian entries [entry][half][3 LN + 1] (x, y, z, infinity flag; affine x, y written back in
-// place), 8t prefix products [entry][half][LN], 65t digit bytes.
-__host__ __device__ inline size_t straus_lz_words(size_t t) {
-    return t * 8 * 2 * (3 * lz::LN + 1) + t * 8 * 2 * lz::LN + (t * 65 + 3) / 4;
-}
-DEV void st_w(uint32_t* w, const lz::F2R& x) {
-#pragma unroll
-    for (int c = 0; c < lz::LN; c++) w[c] = (uint32_t)x.c.v[c];
-}
-DEV lz::F2R ld_w(const uint32_t* w) {
-    lz::F2R x;
-#pragma unroll
-    for (int c = 0; c < lz::LN; c++) x.c.v[c] = (int32_t)w[c];
-    return x;
-}
-// One task's share on one lane pair: multiples of its bases built and batch-normalised, then the 65
-// windows over them into acc
-DEV void straus_g2lz_pair(lz::JL& acc, int NG, int pair, int h, size_t task, size_t t,
-                          const uint8_t* __restrict__ pts, size_t pt_stride, size_t pt_jstride, size_t pt_step,
-                          const uint32_t* __restrict__ l, size_t l_div, uint32_t* __restrict__ scratch) {
-    using namespace lz;
-    constexpr int JW = 3 * LN + 1;
-    const size_t cred = task / l_div;
-    const uint8_t* base = pts + cred * pt_stride + (task % l_div) * pt_jstride;
-    const uint32_t* lk = l + cred * t * 8;
-    uint32_t* ent = scratch + task * straus_lz_words(t);
-    uint32_t* pre = ent + t * 8 * 2 * JW;
-    int8_t* dig = reinterpret_cast<int8_t*>(pre + t * 8 * 2 * LN);
-    acc = jl_inf();
-    F2R acc_z = r_one();
-#pragma unroll 1
-    for (size_t k = pair; k < t; k += NG) {
-        cc::Aff<cc::Fp2> P1;
-        const bool ok = pl::pair_all(g2_decode(P1, base + k * pt_step));  // both lanes decode the point
-        recode_w4(dig + k * 65, lk + k * 8);                            // both write the same digits
-        pl::Fp2 hx, hy;
-        hx.c = h ? P1.x.b : P1.x.a;
-        hy.c = h ? P1.y.b : P1.y.a;
-        const AL P{reduce(in_r2(hx)), reduce(in_r2(hy))};
-        JL J = ok ? jl_from_aff(P) : jl_inf();
-#pragma unroll 1
-        for (int d = 0; d < 8; d++) {
-            if (d == 1) J = jl_dbl(J);
-            else if (d > 1 && ok) J = jl_add_aff(J, P);
-            const size_t e = k * 8 + d;
-            uint32_t* w = ent + (e * 2 + h) * JW;
-            const bool inf = jl_is_inf(J);
-            st_w(w, J.x);
-            st_w(w + LN, J.y);
-            st_w(w + 2 * LN, J.z);
-            w[3 * LN] = inf ? 1u : 0u;
-            st_w(pre + (e * 2 + h) * LN, acc_z);
-            if (!inf) acc_z = reduce(mulr(acc_z, J.z));
-        }
-    }
-    F2R zinv = reduce(inv(acc_z));
-    if (t > (size_t)pair) {
-        const long long kmax = (long long)(((t - 1 - pair) / NG) * NG + pair);
-#pragma unroll 1
-        for (long long kk = kmax; kk >= pair; kk -= NG) {
-#pragma unroll 1
-            for (int d = 7; d >= 0; d--) {
-                const size_t e = (size_t)kk * 8 + d;
-                uint32_t* w = ent + (e * 2 + h) * JW;
-                if (w[3 * LN]) continue;  // identity multiple (pair-uniform: both halves carry the flag)
-                const F2R z = ld_w(w + 2 * LN);
-                const auto zi = mulr(zinv, ld_w(pre + (e * 2 + h) * LN));
-                zinv = reduce(mulr(zinv, z));
-                const auto zi2 = sqrr(zi);
-                st_w(w, reduce(mulr(ld_w(w), zi2)));
-                st_w(w + LN, reduce(mulr(ld_w(w + LN), mulr(zi2, zi))));
-            }
-        }
-    }
-#pragma unroll 1
-    for (int win = 64; win >= 0; win--) {
-        if (win != 64 && !jl_is_inf(acc))
-#pragma unroll 1
-            for (int z = 0; z < 4; z++) acc = jl_dbl(acc);
-#pragma unroll 1
-        for (size_t k = pair; k < t; k += NG) {
-            const int d = dig[k * 65 + win];
-            if (!d) continue;
-            const uint32_t* w = ent + ((k * 8 + (d < 0 ? -d : d) - 1) * 2 + h) * JW;
-            if (w[3 * LN]) continue;  // identity multiple
-            AL e{ld_w(w), ld_w(w + LN)};
-            if (d < 0) e = jl_neg_aff(e);
-            acc = jl_add_aff(acc, e);
-        }
-    }
-}
+// straus_lz_words, straus_g2lz_pair: straus.h
 
 // affine encoding (amcl_wrapper to_bytes) of a lane-pair point; lane h = 0 writes
 DEV void straus_g2lz_out(const lz::JL& acc, int h, uint8_t* out) {

@@ -35,11 +35,13 @@ size_t cck_sigreq_scratch_words(int group, size_t n, int k);
 int cck_sigreq_verify(int group, size_t n, int k, const uint8_t* d_g, const uint8_t* d_hvec, const uint8_t* d_comm,
                       const uint8_t* d_cts, const uint8_t* d_pk, const uint8_t* d_proof, const uint8_t* d_chal,
                       const uint8_t* d_hpts, uint32_t* d_scratch, uint8_t* d_ok, uint8_t* d_verdicts, hipStream_t st);
-int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* d_Y, uint32_t* d_bases,
-                  uint32_t* d_binf, const uint8_t* d_msgs, uint8_t* d_msgs_canon, hipStream_t st);
-int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
+int cck_prep(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
-             uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
+             uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
+size_t cck_prep_var_words(int mode, size_t n, size_t q);
+int cck_prep_var(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_vkX,
+                 const uint8_t* d_vkY, const uint8_t* d_msgs, uint32_t* d_scratch, uint32_t* d_prep,
+                 uint32_t* d_flags, hipStream_t st);
 int cck_miller_lz_g2(int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
@@ -99,6 +101,8 @@ static size_t free_hbm() {
     return fr;
 }
 constexpr int PREP_SLOTS = 14;  // soa.h
+// default HBM budget of a context's shared-verkey tables (wider: cc_set_table_bits)
+constexpr double kVkTableBudget = 4.0 * (double)(1ull << 30);
 
 struct DevBuf {
     void* p = nullptr;
@@ -131,7 +135,7 @@ struct cc_ctx {
     hipStream_t stream = nullptr;
     // params
     bool have_params = false;
-    std::vector<uint8_t> gtilde_bytes;  // encoding as given (subgroup status at cc_set_verkey)
+    std::vector<uint8_t> gtilde_bytes;  // encoding as given (subgroup status at cc_set_verkey; idempotence)
     DevBuf gtilde_aff;   // OtherGroup affine (Montgomery, AoS)
     uint32_t gtilde_inf = 0;
     DevBuf gtilde_lines; // SigG1: Miller lines of g~
@@ -145,13 +149,17 @@ struct cc_ctx {
     int wbits = 16;      // window width of `table`
     int force_vk_bits = 0, force_iss_bits = 0;  // cc_set_table_bits (0: chosen by memory)
     bool vk_subgroup = false;  // X~, Y~ and g~ all in the order-r subgroup (RLC soundness needs it)
+    std::vector<uint8_t> vk_bytes;  // X~ || Y~ encodings of the current verkey (cc_set_verkey idempotence)
+    int vk_built_force = 0;         // force_vk_bits when the current tables were built
     uint32_t X_inf = 0;
     // workspaces
     DevBuf in_s1, in_s2, in_msgs, in_vkX, in_vkY, in_aux[6];
-    DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, vkbinf, msgs_canon, lag;
+    DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, lag;  // vkb: per-credential-verkey MSM scratch
     // RLC batch mode: ChaCha20 key, identity flag word, partial / gathered partials, verdict
     DevBuf rlc_key, rlc_any, rlc_part, rlc_flag, rlc_accept;
     DevBuf fin_f, fin_scratch;  // cc_rlc_finish_device's own buffers
+    hipEvent_t ev_fin = nullptr;  // end of the last finish: finishes of one context run in call order
+    bool fin_recorded = false;
     // RLC g~-side fold (fold.hip): fold points, delta digits, sort/partials/bucket workspace, the 16
     // pseudo-credentials' prep SoA (window sums + the fixed points P_w = (256^w) g~) and flags
     DevBuf rlc_pts, rlc_dig, rlc_work, rlc_prep2, rlc_finf, rlc_flags2;
@@ -261,7 +269,11 @@ const char* cc_status_str(int s) {
     }
 }
 
-const char* cc_version(void) { return "coconut-mi355x 0.1.0 (gfx950)"; }
+// CC_SRC_HASH: tools/src_hash.py over csrc/, the header, the Makefile and the flags (Makefile)
+#ifndef CC_SRC_HASH
+#define CC_SRC_HASH "unknown"
+#endif
+const char* cc_version(void) { return "coconut-mi355x 0.2.0 (gfx950) src " CC_SRC_HASH; }
 
 cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
     if (!out || (mode != CC_SIG_G2 && mode != CC_SIG_G1)) return CC_ERR_DECODE;
@@ -279,6 +291,7 @@ cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
     (void)hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming);
     {
         // high priority: a launch on the side stream gets its wave slots before a full launch on the
         // context stream fills the chip
@@ -305,7 +318,7 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
-                      &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->vkbinf, &c->msgs_canon, &c->lag,
+                      &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->lag,
                       &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->fin_f, &c->fin_scratch, &c->pok_idx, &c->rlc_gath,
                       &c->rlc_pts, &c->rlc_dig, &c->rlc_work, &c->rlc_prep2, &c->rlc_finf, &c->rlc_flags2,
                       &c->iss_ids, &c->iss_aff, &c->iss_inf, &c->iss_table, &c->agg_scratch, &c->dev_err};
@@ -315,6 +328,7 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     if (c->ev_order) (void)hipEventDestroy(c->ev_order);
     if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
     if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+    if (c->ev_fin) (void)hipEventDestroy(c->ev_fin);
     if (c->side) (void)hipStreamDestroy(c->side);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -366,11 +380,14 @@ static cc_status subgroup_host(cc_ctx* c, int group, size_t n, const uint8_t* by
     return CC_OK;
 }
 
-// Shared-verkey tables: the widest of 22 / 20 / 16-bit windows whose q + 2 bases' tables fit 40 % of the
-// free HBM (at most 96 GiB of the 288): 22 bits = 12 windows of 4,194,303 entries, 4.8 / 9.7 GB a G1 / G2
-// base, 12 mixed additions per scalar against 16 at 16 bits (100 / 200 MB a base); else 8-bit windows
-// (32 x 255 entries, 0.8 / 1.6 MB a base); a failed wide allocation falls back to 8 bits.
-// cc_set_table_bits forces a width in [8, 22].  On failure the caller leaves the context without a verkey.
+// Shared-verkey tables: by default the widest of 22 / 20 / 18 / 16 / 14 / 12 / 10-bit windows whose q + 2
+// bases' tables fit kVkTableBudget (4 GiB) and 40 % of the free HBM — a drop-in verifier must not claim a
+// shared GPU's memory: config 2 (q = 6, 8 G1 bases) gets 18 bits (15 windows of 262,143 entries, 3.0 GB),
+// config 3 (q = 16) 16 bits (1.8 GB); 16 / 15 / 12 mixed additions per scalar at 16 / 18 / 22 bits.  Wider
+// tables (22 bits: 4.8 / 9.7 GB a G1 / G2 base, +1.2 % on config 2, profiles/r03/vkbits) are opt-in through
+// cc_set_table_bits, which forces a width in [8, 22]; else 8-bit windows (32 x 255 entries, 0.8 / 1.6 MB a
+// base); a failed wide allocation falls back to 8 bits.  On failure the caller leaves the context without
+// a verkey.
 static cc_status rebuild_tables(cc_ctx* c) {
     // bases for the fixed-base tables: Y~[0..q), g~ (PoK Schnorr base), X~ (RLC) -> q + 2 bases
     int og = oth_group(c->mode);
@@ -382,10 +399,9 @@ static cc_status rebuild_tables(cc_ctx* c) {
     c->table.release();
     const double fr = (double)free_hbm();
     if (!wb) {
-        // the widest of 22 / 20 / 16 bits whose tables fit 40 % of the free HBM, at most 96 GiB
-        const double cap = std::min(0.4 * fr, 96.0 * (double)(1ull << 30));
+        const double cap = std::min(0.4 * fr, kVkTableBudget);
         wb = 8;
-        for (int w : {22, 20, 16})
+        for (int w : {22, 20, 18, 16, 14, 12, 10})
             if ((double)nb * (double)tab_words(og, w) * 4.0 <= cap) {
                 wb = w;
                 break;
@@ -405,6 +421,7 @@ static cc_status rebuild_tables(cc_ctx* c) {
         if (c->table.ensure((size_t)nb * tab_words(og, wb) * 4)) return CC_ERR_HIP;
     }
     c->wbits = wb;
+    c->vk_built_force = c->force_vk_bits;
     if (c->table_inf.ensure((size_t)nb * 4)) return CC_ERR_HIP;
     // [Y~..., g~, X~] are contiguous in vk_aff (X~ at 0, Y~ at 1..q, g~ at q+1, X~ again at q+2)
     HIPCK(hipMemcpyAsync(c->table_inf.p, c->vk_inf.as<uint32_t>() + 1, (size_t)nb * 4, hipMemcpyDeviceToDevice,
@@ -428,7 +445,13 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
         c->have_params = true;
         return CC_OK;
     }
+    // the same g~ again (a caller re-binding its Params every batch): nothing to do
+    if (c->have_params && c->gtilde_bytes.size() == (size_t)oth_bytes(c->mode) &&
+        !memcmp(c->gtilde_bytes.data(), g_tilde, c->gtilde_bytes.size()))
+        return CC_OK;
     HIPCK(hipSetDevice(c->device));
+    c->have_params = false;  // until the decode below has succeeded
+    c->gtilde_bytes.clear();
     int og = oth_group(c->mode);
     size_t aw = aff_words(og);
     if (c->gtilde_aff.ensure(aw * 4)) return CC_ERR_HIP;
@@ -453,6 +476,7 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
         if (st) {
             c->have_vk = false;
             c->q = 0;
+            c->vk_bytes.clear();
         }
         return st;
     }
@@ -462,11 +486,9 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
 cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q) {
     if (!c || !X || (q && !Y) || q > 4096) return CC_ERR_DECODE;
     if (!c->have_params) return CC_ERR_STATE;
-    // no verkey until every step below has succeeded: a failed call leaves the context refusing
-    // verify / RLC / PoK calls with CC_ERR_STATE instead of running on a half-built table
-    c->have_vk = false;
-    c->q = 0;
     if (!c->peers.empty()) {
+        c->have_vk = false;
+        c->q = 0;
         for (cc_ctx* p : c->peers) {
             cc_status s = cc_set_verkey(p, X, Y, q);
             if (s) return s;
@@ -475,12 +497,20 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
         c->have_vk = true;
         return CC_OK;
     }
-    HIPCK(hipSetDevice(c->device));
     int og = oth_group(c->mode);
     size_t eb = (size_t)oth_bytes(c->mode), aw = aff_words(og);
     std::vector<uint8_t> all((q + 1) * eb);
     memcpy(all.data(), X, eb);
     if (q) memcpy(all.data() + eb, Y, q * eb);
+    // the same verkey again, tables built at the width now asked for: nothing to rebuild (a caller
+    // binding its verkey every batch, INTEGRATION.md §3, pays a byte compare, not a table build)
+    if (c->have_vk && c->q == q && c->vk_built_force == c->force_vk_bits && c->vk_bytes == all) return CC_OK;
+    // no verkey until every step below has succeeded: a failed call leaves the context refusing
+    // verify / RLC / PoK calls with CC_ERR_STATE instead of running on a half-built table
+    c->have_vk = false;
+    c->q = 0;
+    c->vk_bytes.clear();
+    HIPCK(hipSetDevice(c->device));
     if (c->vk_aff.ensure((q + 3) * aw * 4) || c->vk_inf.ensure((q + 3) * 4)) return CC_ERR_HIP;
     cc_status s = decode_points_host(c, og, q + 1, all.data(), c->vk_aff.as<uint32_t>(), c->vk_inf.as<uint32_t>());
     if (s) return s;
@@ -507,6 +537,7 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
         c->q = 0;
         return st;
     }
+    c->vk_bytes.swap(all);
     c->have_vk = true;
     return CC_OK;
 }
@@ -543,13 +574,20 @@ static cc_status ensure_work(cc_ctx* c, size_t n) {
     return CC_OK;
 }
 
-// the three verify launches on device buffers; timing per phase when enabled
-static cc_status launch_verify(cc_ctx* c, size_t n, size_t q, int fixed, const uint8_t* d_s1, const uint8_t* d_s2,
-                               const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
+// the three verify launches on device buffers; timing per phase when enabled.  d_vkX == NULL: the
+// shared verkey's tables; else one verkey per credential (d_vkX n x OtherGroup, d_vkY n x q x
+// OtherGroup; the Straus MSM of pervk.hip, its scratch in c->vkb, sized by the caller)
+static cc_status launch_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s1, const uint8_t* d_s2,
+                               const uint8_t* d_msgs, const uint8_t* d_vkX, const uint8_t* d_vkY, uint8_t* d_verdicts,
+                               uint8_t* d_gt, hipStream_t st) {
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
-    KCK(cck_prep(c->mode, fixed, n, (int)q, d_s1, d_s2, d_msgs, c->vk_aff.as<uint32_t>(), c->X_inf,
-                 c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->vkb.as<uint32_t>(),
-                 c->vkbinf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
+    if (d_vkX)
+        KCK(cck_prep_var(c->mode, n, (int)q, d_s1, d_s2, d_vkX, d_vkY, d_msgs, c->vkb.as<uint32_t>(),
+                         c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
+    else
+        KCK(cck_prep(c->mode, n, (int)q, d_s1, d_s2, d_msgs, c->vk_aff.as<uint32_t>(), c->X_inf,
+                     c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
+                     c->flags.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
@@ -578,7 +616,29 @@ cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     {
         StreamOrder order(c, st);
-        s = launch_verify(c, n, q, 1, d_s1, d_s2, d_msgs, d_verdicts, d_gt, st);
+        s = launch_verify(c, n, q, d_s1, d_s2, d_msgs, nullptr, nullptr, d_verdicts, d_gt, st);
+    }
+    if (s) return s;
+    if (c->timing) collect_timing(c);
+    return CC_OK;
+}
+
+cc_status cc_verify_batch_pervk_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s1, const uint8_t* d_s2,
+                                       const uint8_t* d_msgs, const uint8_t* d_vkX, const uint8_t* d_vkY,
+                                       uint8_t* d_verdicts, uint8_t* d_gt, void* stream) {
+    c = primary(c);  // a device set forwards to its first device
+    if (!c || q > 4096 || (n && (!d_s1 || !d_s2 || !d_vkX || !d_verdicts || (q && (!d_msgs || !d_vkY)))))
+        return CC_ERR_DECODE;
+    if (!c->have_params) return CC_ERR_STATE;
+    if (!n) return CC_OK;
+    HIPCK(hipSetDevice(c->device));
+    cc_status s = ensure_work(c, n);
+    if (s) return s;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    {
+        StreamOrder order(c, st);
+        if (c->vkb.ensure(cck_prep_var_words(c->mode, n, q) * 4)) return CC_ERR_HIP;
+        s = launch_verify(c, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
     }
     if (s) return s;
     if (c->timing) collect_timing(c);
@@ -689,14 +749,19 @@ cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_parti
     HIPCK(hipSetDevice(c->device));
     // the finish owns its buffers (combined product, the one-element fexp's scratch, flag) and touches no
     // other context state, so it is NOT ordered against the context's stream: on a caller stream it may
-    // overlap the next batch's cc_rlc_partial_device (the caller orders d_partials itself)
+    // overlap the next batch's cc_rlc_partial_device (the caller orders d_partials itself).  Finishes of
+    // one context are ordered among themselves (ev_fin): two finishes on different streams never share
+    // the buffers at the same time, whichever engines or streams issue them.
     if (c->rlc_flag.ensure(4) || c->fin_f.ensure(12 * 12 * 4) || c->fin_scratch.ensure(2 * 72 * 12 * 4))
         return CC_ERR_HIP;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (c->fin_recorded) HIPCK(hipStreamWaitEvent(st, c->ev_fin, 0));
     KCK(cck_rlc_combine(nparts, d_partials, c->fin_f.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), st));
     // one final exponentiation; flags[0] bit0 (a sigma was the identity somewhere) forces a reject
     KCK(cck_fexp(1, c->fin_f.as<uint32_t>(), c->fin_scratch.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), d_accept,
                  d_gt, st));
+    HIPCK(hipEventRecord(c->ev_fin, st));
+    c->fin_recorded = true;
     return CC_OK;
 }
 
@@ -724,7 +789,7 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
     if (!c || (n && (!s1 || !s2 || !verdicts || (q && !msgs)))) return CC_ERR_DECODE;
     if (!c->have_params) return CC_ERR_STATE;
     const bool per_vk = vkX != nullptr;
-    if (per_vk && q && !vkY) return CC_ERR_DECODE;
+    if (per_vk && ((q && !vkY) || q > 4096)) return CC_ERR_DECODE;
     if (!per_vk) {
         if (!c->have_vk) return CC_ERR_STATE;
         if (q != c->q) return CC_ERR_LEN;
@@ -755,19 +820,14 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
         }
     }
     if (per_vk) {
-        int og = oth_group(c->mode);
-        size_t fs = og == 1 ? 1 : 2;  // Fp slots per coordinate
         if (c->in_vkX.ensure(n * ob) || c->in_vkY.ensure(n * q * ob + 16) ||
-            c->vkb.ensure(n * 12 * 4 * 2 * fs * (q + 1)) || c->vkbinf.ensure(n * 4 * (q + 1)) ||
-            c->msgs_canon.ensure(n * q * 48 + 16))
+            c->vkb.ensure(cck_prep_var_words(c->mode, n, q) * 4))
             return CC_ERR_HIP;
         HIPCK(hipMemcpyAsync(c->in_vkX.p, vkX, n * ob, hipMemcpyHostToDevice, st));
         if (q) HIPCK(hipMemcpyAsync(c->in_vkY.p, vkY, n * q * ob, hipMemcpyHostToDevice, st));
-        KCK(cck_decode_vk(c->mode, n, (int)q, c->in_vkX.as<uint8_t>(), c->in_vkY.as<uint8_t>(), c->vkb.as<uint32_t>(),
-                          c->vkbinf.as<uint32_t>(), d_msgs, c->msgs_canon.as<uint8_t>(), st));
-        d_msgs = c->msgs_canon.as<uint8_t>();
     }
-    s = launch_verify(c, n, q, per_vk ? 0 : 1, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), d_msgs,
+    s = launch_verify(c, n, q, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), d_msgs,
+                      per_vk ? c->in_vkX.as<uint8_t>() : nullptr, per_vk ? c->in_vkY.as<uint8_t>() : nullptr,
                       c->verdicts.as<uint8_t>(), gt ? c->gt.as<uint8_t>() : nullptr, st);
     if (s) return s;
     HIPCK(hipMemcpyAsync(verdicts, c->verdicts.p, n, hipMemcpyDeviceToHost, st));
@@ -1140,7 +1200,9 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
         for (size_t j = 0; j < q; j++) memcpy(&enc[(r * (q + 1) + 1 + j) * ob], Y + (k * q + j) * ob, ob);
     }
     // the widest window whose tables fit the budget (16 GiB of the 288 GB HBM, at most half of what is
-    // free; cc_set_table_bits forces a width): t x nwin additions per aggregated key, nwin = ceil(256 / w)
+    // free; cc_set_table_bits forces a width): t x nwin additions per aggregated key, nwin = ceil(256 / w).
+    // The old table is released first so its memory counts as free (identical calls pick the same width).
+    c->iss_table.release();
     const double budget = std::min(16.0 * (double)(1ull << 30), 0.5 * (double)free_hbm());
     int wb = 8;
     if (c->force_iss_bits >= 8 && c->force_iss_bits <= 16) {
@@ -1154,7 +1216,6 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
     }
     if (c->iss_ids.ensure(n_iss * 8) || c->iss_aff.ensure(nb * aw * 4) || c->iss_inf.ensure(nb * 4))
         return CC_ERR_HIP;
-    c->iss_table.release();
     const double fr = (double)free_hbm();
     if (fr > 0 && (double)(nb * tab_words(og, wb) * 4) > 0.9 * fr) {  // see rebuild_tables
         if (c->force_iss_bits) return CC_ERR_HIP;

@@ -6,8 +6,8 @@
 //
 // One credential per lane; three launches per batch so each kernel's live state fits the
 // 512-entry register file of one wave per SIMD:
-//   k_prep_*   : decode sigma/messages, fixed-base (shared vk) or variable-base (per-credential
-//                vk) MSM, write the Miller-loop operands (SoA, limb-major: coalesced per limb)
+//   k_prep_*   : decode sigma/messages, fixed-base (shared vk) MSM, write the Miller-loop operands
+//                (SoA, limb-major: coalesced per limb); per-credential verkeys: pervk.hip
 //   k_miller_* : shared-squaring 2-pair Miller loop -> f (Fp12, SoA)
 //   k_fexp     : final exponentiation, is_one, identity check -> verdict (+ optional GT bytes)
 // Group assignment is a template parameter: kSigG2 (reference default, sigma in G2, vk in G1)
@@ -271,113 +271,9 @@ DEV void msm_fixed_part(Jac<F>& acc, const uint8_t* msgs, int q, const uint32_t*
     msm_fixed_terms<F>(acc, msgs, q, table, wbits, binf, w0, w1);
 }
 
-// variable-base (per-credential verkey): interleaved double-and-add over the q+1 bases.
-// bases: SoA scratch of decoded affine points, slots [j][coord] ; binf per (j, i)
-template <class F>
-DEV void msm_var(Jac<F>& acc, const uint8_t* msgs, int q, const Soa& bases, const uint32_t* binf, size_t i,
-                 size_t n) {
-    constexpr int FS = sizeof(F) / sizeof(Fp);  // Fp slots per coordinate
-    // X~ (scalar 1)
-    if (binf[i]) {
-        jac_set_inf(acc);
-    } else {
-        Aff<F> x;
-        Fp* px = reinterpret_cast<Fp*>(&x);
-#pragma unroll
-        for (int k = 0; k < 2 * FS; k++) ld_fp(px[k], bases, k, i);
-        jac_from_aff(acc, x);
-    }
-    Jac<F> s;
-    jac_set_inf(s);
-    for (int b = 254; b >= 0; b--) {
-        jac_dbl(s, s);
-        for (int j = 0; j < q; j++) {
-            const uint8_t* mp = msgs + (size_t)j * 48;
-            // bit b of the BE scalar (assumed canonical here; reduced copies are made by the caller)
-            uint32_t byte = mp[47 - (b >> 3)];
-            if (((byte >> (b & 7)) & 1u) && !binf[(size_t)(j + 1) * n + i]) {
-                Aff<F> y;
-                Fp* py = reinterpret_cast<Fp*>(&y);
-#pragma unroll
-                for (int k = 0; k < 2 * FS; k++) ld_fp(py[k], bases, (j + 1) * 2 * FS + k, i);
-                jac_add_aff(s, s, y);
-            }
-        }
-    }
-    jac_add(acc, acc, s);
-}
-
-// per-credential verkey decode into SoA scratch (+ canonicalised message copy)
-template <class F>
-__global__ __launch_bounds__(64) void k_decode_vk(size_t n, int q, const uint8_t* __restrict__ X, const uint8_t* __restrict__ Y,
-                            uint32_t* __restrict__ bases, size_t stride, uint32_t* __restrict__ binf,
-                            const uint8_t* __restrict__ msgs, uint8_t* __restrict__ msgs_canon) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    constexpr int FS = sizeof(F) / sizeof(Fp);
-    constexpr int EB = enc_bytes<F>();
-    Soa s{bases, stride};
-    for (int j = 0; j <= q; j++) {
-        Aff<F> a;
-        const uint8_t* src = j == 0 ? X + i * EB : Y + (i * q + (j - 1)) * EB;
-        bool ok = decode_point<F>(a, src);
-        const Fp* pa = reinterpret_cast<const Fp*>(&a);
-        for (int k = 0; k < 2 * FS; k++) st_fp(s, j * 2 * FS + k, i, pa[k]);
-        binf[(size_t)j * n + i] = ok ? 0u : 1u;
-    }
-    for (int j = 0; j < q; j++) {
-        Fr m;
-        fr_from_be48(m, msgs + (i * q + j) * 48);
-        uint32_t* dst = reinterpret_cast<uint32_t*>(msgs_canon + (i * q + j) * 48);
-        for (int k = 0; k < 4; k++) dst[k] = 0;
-        for (int k = 0; k < 8; k++) dst[11 - k] = __builtin_bswap32(m.v[k]);
-    }
-}
 
 // ================================================================ prep kernels
 
-// SigG2: sigma in G2 (192 B), verkey in G1
-template <bool kFixed>
-__global__ __launch_bounds__(256) void k_prep_sigg2(size_t n, int q, const uint8_t* __restrict__ s1b,
-                                                    const uint8_t* __restrict__ s2b,
-                                                    const uint8_t* __restrict__ msgs,
-                                                    const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                                                    const uint32_t* __restrict__ table, int wbits,
-                                                    const uint32_t* __restrict__ binf_fixed,
-                                                    uint32_t* __restrict__ vkb, size_t vk_stride,
-                                                    const uint32_t* __restrict__ binf_var,
-                                                    uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Soa S{prep, n};
-    uint32_t fl = 0;
-    {
-        Aff<Fp2> a;
-        if (!g2_decode(a, s1b + i * 192)) fl |= 1u;
-        st_f2(S, S_Q1, i, a.x);
-        st_f2(S, S_Q1 + 2, i, a.y);
-        if (!g2_decode(a, s2b + i * 192)) fl |= 2u;
-        f2_neg(a.y, a.y);  // -sigma_2
-        st_f2(S, S_Q2, i, a.x);
-        st_f2(S, S_Q2 + 2, i, a.y);
-    }
-    Jac<Fp> pr;
-    if (kFixed) {
-        msm_fixed<Fp>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, table, wbits, binf_fixed);
-    } else {
-        msm_var<Fp>(pr, msgs + i * (size_t)q * 48, q, Soa{vkb, vk_stride}, binf_var, i, vk_stride);
-    }
-    if (jac_is_inf(pr)) fl |= 4u;
-    // line evaluation form (X Z, Y, Z^3)
-    Fp t;
-    fp_mul(t, pr.x, pr.z);
-    st_fp(S, S_P1, i, t);
-    st_fp(S, S_P1 + 1, i, pr.y);
-    fp_sqr(t, pr.z);
-    fp_mul(t, t, pr.z);
-    st_fp(S, S_P1 + 2, i, t);
-    flags[i] = fl;
-}
 
 // SigG2 + shared verkey, one credential per lane PAIR (the layout of the pairing kernels): the even
 // lane decodes sigma_1, the odd lane sigma_2; each lane sums half of the fixed-base windows, the two
@@ -432,43 +328,6 @@ __global__ __launch_bounds__(256) void k_prep_sigg2_pair(size_t n, int q, const 
     }
 }
 
-// SigG1: sigma in G1 (97 B), verkey in G2; pr converted to affine (it is the Miller-loop T)
-template <bool kFixed>
-__global__ __launch_bounds__(256) void k_prep_sigg1(size_t n, int q, const uint8_t* __restrict__ s1b,
-                                                    const uint8_t* __restrict__ s2b,
-                                                    const uint8_t* __restrict__ msgs,
-                                                    const uint32_t* __restrict__ Xaff, uint32_t Xinf,
-                                                    const uint32_t* __restrict__ table, int wbits,
-                                                    const uint32_t* __restrict__ binf_fixed,
-                                                    uint32_t* __restrict__ vkb, size_t vk_stride,
-                                                    const uint32_t* __restrict__ binf_var,
-                                                    uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
-    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    Soa S{prep, n};
-    uint32_t fl = 0;
-    {
-        Aff<Fp> a;
-        if (!g1_decode(a, s1b + i * 97)) fl |= 1u;
-        st_fp(S, S_P1, i, a.x);
-        st_fp(S, S_P1 + 1, i, a.y);
-        if (!g1_decode(a, s2b + i * 97)) fl |= 2u;
-        fp_neg(a.y, a.y);
-        st_fp(S, S_P2, i, a.x);
-        st_fp(S, S_P2 + 1, i, a.y);
-    }
-    Jac<Fp2> pr;
-    if (kFixed) {
-        msm_fixed<Fp2>(pr, msgs + i * (size_t)q * 48, q, Xaff, Xinf, table, wbits, binf_fixed);
-    } else {
-        msm_var<Fp2>(pr, msgs + i * (size_t)q * 48, q, Soa{vkb, vk_stride}, binf_var, i, vk_stride);
-    }
-    Aff<Fp2> a;
-    if (!jac_to_aff(a, pr)) fl |= 4u;
-    st_f2(S, S_Q1, i, a.x);
-    st_f2(S, S_Q1 + 2, i, a.y);
-    flags[i] = fl;
-}
 
 // SigG1, shared verkey, one credential per lane PAIR: lane h decodes sigma_{h+1} (one-lane G1) and
 // the G2 verkey MSM X~ + sum m_j Y~_j runs on the pair-lane Fp2 (curve_pl.h): both lanes hold halves
@@ -613,40 +472,18 @@ int cck_gtilde_lines(const uint32_t* d_gtilde_aff, uint32_t* d_lines, hipStream_
     return 0;
 }
 
-int cck_decode_vk(int mode, size_t n, int q, const uint8_t* d_X, const uint8_t* d_Y, uint32_t* d_bases,
-                  uint32_t* d_binf, const uint8_t* d_msgs, uint8_t* d_msgs_canon, hipStream_t st) {
+
+// shared-verkey prep (the fixed-base tables); per-credential verkeys: pervk.hip cck_prep_var
+int cck_prep(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
+             const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
+             uint32_t* d_prep, uint32_t* d_flags, hipStream_t st) {
     if (!n) return 0;
     if (mode == 0)
-        hipLaunchKernelGGL(k_decode_vk<Fp>, dim3(nblocks(n, 64)), dim3(64), 0, st, n, q, d_X, d_Y, d_bases, n, d_binf,
-                           d_msgs, d_msgs_canon);
+        hipLaunchKernelGGL(k_prep_sigg2_pair, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_msgs,
+                           d_Xaff, Xinf, d_table, wbits, d_binf_fixed, d_prep, d_flags);
     else
-        hipLaunchKernelGGL(k_decode_vk<Fp2>, dim3(nblocks(n, 64)), dim3(64), 0, st, n, q, d_X, d_Y, d_bases, n,
-                           d_binf, d_msgs, d_msgs_canon);
-    CC_CHECK(hipGetLastError());
-    return 0;
-}
-
-// fixed != 0: shared verkey tables; else per-credential bases decoded by cck_decode_vk
-int cck_prep(int mode, int fixed, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
-             const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
-             uint32_t* d_vkb, const uint32_t* d_binf_var, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st) {
-    if (!n) return 0;
-    dim3 g(nblocks(n, 256)), b(256);
-    if (mode == 0) {
-        if (fixed)
-            hipLaunchKernelGGL(k_prep_sigg2_pair, dim3(nblocks(2 * n, 256)), b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff,
-                               Xinf, d_table, wbits, d_binf_fixed, d_prep, d_flags);
-        else
-            hipLaunchKernelGGL(k_prep_sigg2<false>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
-                               wbits, d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
-    } else {
-        if (fixed)
-            hipLaunchKernelGGL(k_prep_sigg1_pair, dim3(nblocks(2 * n, 256)), b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff,
-                               Xinf, d_table, wbits, d_binf_fixed, d_prep, d_flags);
-        else
-            hipLaunchKernelGGL(k_prep_sigg1<false>, g, b, 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf, d_table,
-                               wbits, d_binf_fixed, d_vkb, n, d_binf_var, d_prep, d_flags);
-    }
+        hipLaunchKernelGGL(k_prep_sigg1_pair, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_msgs,
+                           d_Xaff, Xinf, d_table, wbits, d_binf_fixed, d_prep, d_flags);
     CC_CHECK(hipGetLastError());
     return 0;
 }

@@ -1,0 +1,166 @@
+// Signature::verify with the CALLER's verkey per credential (the product path).
+//
+// Reference: src/signature.rs:473-478 -> ps_sig Signature::verify [EXT]: per call,
+// pr = multi_scalar_mul_var_time([X~, Y~_1..Y~_q], [1, m_1..m_q]), then the
+// 2-pairing check e(sigma_1, pr) e(-sigma_2, g~) == 1 that the shared-verkey path also ends in.
+// With a verkey per credential the bases are not fixed, so no window tables exist: the MSM is a
+// windowed Straus (straus.h) — signed radix-16 digits, per base the multiples 1..8 batch-normalised
+// with one inversion per lane, 65 windows of 4 doublings + one mixed addition per base.  No per-lane
+// branch on scalar bits (the round-1 bitwise double-and-add paid a mixed addition at nearly every bit
+// in SIMT, some lane of the wave always having the bit set).
+//
+// Both group modes run one credential per lane PAIR, the layout the Miller loop and the shared-verkey
+// preps use:
+//   SigG2 (verkey in G1): lane h decodes sigma_{h+1} and runs the lazy one-lane G1 Straus over the
+//     bases Y~_j with j = h mod 2 (lane 0 also adds X~); the two partial sums meet by DPP.
+//   SigG1 (verkey in G2): lane h decodes sigma_{h+1}; the pair runs the G2 Straus on the lazy pair-lane
+//     field over every Y~_j (straus_g2lz_pair) and adds X~.
+// The prep writes the SoA operands of kernels.hip's k_prep_*_pair, so k_miller / k_fexp finish.
+#include "codec.h"
+#include "curve_lz.h"
+#include "curve_pl.h"
+#include "fr.h"
+#include "pairing.h"
+#include "soa.h"
+#include "straus.h"
+
+using namespace cc;
+
+// messages (48-byte big-endian, any value) -> canonical 8-word little-endian scalars (mod r), the
+// Straus digits' input
+__global__ __launch_bounds__(256) void k_scalars_w8(size_t nm, const uint8_t* __restrict__ msgs,
+                                                    uint32_t* __restrict__ out) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= nm) return;
+    Fr m;
+    fr_from_be48(m, msgs + i * 48);
+    uint4* o = reinterpret_cast<uint4*>(out + i * 8);
+    o[0] = make_uint4(m.v[0], m.v[1], m.v[2], m.v[3]);
+    o[1] = make_uint4(m.v[4], m.v[5], m.v[6], m.v[7]);
+}
+
+// SigG2, per-credential verkey (G1 bases), one credential per lane pair
+__global__ __launch_bounds__(256, 2) void k_prep_sigg2_var(size_t n, int q, const uint8_t* __restrict__ s1b,
+                                                           const uint8_t* __restrict__ s2b,
+                                                           const uint8_t* __restrict__ vkX,
+                                                           const uint8_t* __restrict__ vkY,
+                                                           const uint32_t* __restrict__ scal,
+                                                           uint32_t* __restrict__ scratch,
+                                                           uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t i = g >> 1;
+    const int h = (int)(g & 1);
+    if (i >= n) return;  // pair-uniform
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp2> a;
+        if (!g2_decode(a, (h ? s2b : s1b) + i * 192)) fl |= h ? 2u : 1u;
+        if (h) f2_neg(a.y, a.y);  // -sigma_2
+        const int slot = h ? S_Q2 : S_Q1;
+        st_f2(S, slot, i, a.x);
+        st_f2(S, slot + 2, i, a.y);
+    }
+    lz::JG a;
+    straus_g1lz_lane(a, 2, h, (size_t)q, vkY + i * (size_t)q * 97, scal + i * (size_t)q * 8,
+                     scratch + i * straus_g1lz_words((size_t)q));
+    if (!h) {  // X~ with scalar 1
+        Aff<Fp> X;
+        if (g1_decode(X, vkX + i * 97)) a = lz::jg_add_aff(a, ag_of(lz::reduce(lz::in_r(X.x)), lz::reduce(lz::in_r(X.y))));
+    }
+    Jac<Fp> pr = lz::jg_to(a), o;
+    o.x = pl::swp(pr.x);
+    o.y = pl::swp(pr.y);
+    o.z = pl::swp(pr.z);
+    fl |= pl::swp(fl);
+    if (h) {
+        Jac<Fp> t = pr;
+        pr = o;
+        o = t;
+    }
+    jac_add(pr, pr, o);  // (even lane's sum) + (odd lane's sum), the same operand order on both lanes
+    if (jac_is_inf(pr)) fl |= 4u;
+    Fp t;
+    if (!h) {
+        fp_mul(t, pr.x, pr.z);
+        st_fp(S, S_P1, i, t);
+        st_fp(S, S_P1 + 1, i, pr.y);
+        flags[i] = fl;
+    } else {
+        fp_sqr(t, pr.z);
+        fp_mul(t, t, pr.z);
+        st_fp(S, S_P1 + 2, i, t);
+    }
+}
+
+// SigG1, per-credential verkey (G2 bases on the lazy pair-lane field), one credential per lane pair
+__global__ __launch_bounds__(256, 2) void k_prep_sigg1_var(size_t n, int q, const uint8_t* __restrict__ s1b,
+                                                           const uint8_t* __restrict__ s2b,
+                                                           const uint8_t* __restrict__ vkX,
+                                                           const uint8_t* __restrict__ vkY,
+                                                           const uint32_t* __restrict__ scal,
+                                                           uint32_t* __restrict__ scratch,
+                                                           uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
+    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    const size_t i = g >> 1;
+    const int h = (int)(g & 1);
+    if (i >= n) return;  // pair-uniform
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp> a;
+        if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
+        if (h) fp_neg(a.y, a.y);  // -sigma_2
+        const int slot = h ? S_P2 : S_P1;
+        st_fp(S, slot, i, a.x);
+        st_fp(S, slot + 1, i, a.y);
+    }
+    fl |= pl::swp(fl);
+    lz::JL la;
+    straus_g2lz_pair(la, 1, 0, h, i, (size_t)q, vkY, (size_t)q * 192, 0, 192, scal, 1, scratch);
+    {  // X~ with scalar 1 (both lanes decode it)
+        Aff<Fp2> X;
+        if (pl::pair_all(g2_decode(X, vkX + i * 192))) {
+            pl::Fp2 hx, hy;
+            hx.c = h ? X.x.b : X.x.a;
+            hy.c = h ? X.y.b : X.y.a;
+            la = lz::jl_add_aff(la, lz::AL{lz::reduce(lz::in_r2(hx)), lz::reduce(lz::in_r2(hy))});
+        }
+    }
+    Jac<pl::Fp2> acc = pl::jl_to_pl(la);
+    Aff<pl::Fp2> a;
+    if (!jac_to_aff(a, acc)) fl |= 4u;
+    pl::st_f2(S, S_Q1, i, a.x);
+    pl::st_f2(S, S_Q1 + 2, i, a.y);
+    if (!h) flags[i] = fl;
+}
+
+static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+extern "C" {
+
+// scratch words of cck_prep_var for n credentials of q messages
+size_t cck_prep_var_words(int mode, size_t n, size_t q) {
+    return n * q * 8 + n * (mode == 0 ? straus_g1lz_words(q) : straus_lz_words(q)) + 64;
+}
+
+// Per-credential-verkey prep: vkX n x OtherGroup, vkY n x q x OtherGroup, msgs n x q x 48 B;
+// scratch: cck_prep_var_words words.  Writes the Miller-loop operands and flags like cck_prep.
+int cck_prep_var(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_vkX,
+                 const uint8_t* d_vkY, const uint8_t* d_msgs, uint32_t* d_scratch, uint32_t* d_prep,
+                 uint32_t* d_flags, hipStream_t st) {
+    if (!n) return 0;
+    uint32_t* scal = d_scratch;
+    uint32_t* straus = d_scratch + n * (size_t)q * 8;
+    if (q) hipLaunchKernelGGL(k_scalars_w8, dim3(nblocks(n * (size_t)q, 256)), dim3(256), 0, st, n * (size_t)q, d_msgs, scal);
+    if (mode == 0)
+        hipLaunchKernelGGL(k_prep_sigg2_var, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_vkX,
+                           d_vkY, scal, straus, d_prep, d_flags);
+    else
+        hipLaunchKernelGGL(k_prep_sigg1_var, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_vkX,
+                           d_vkY, scal, straus, d_prep, d_flags);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // extern "C"

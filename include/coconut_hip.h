@@ -4,7 +4,7 @@
  * /root/reference).  The reference has no FFI of its own; these entry points are what its Rust
  * API would bind through `extern "C"` (binding shown in INTEGRATION.md):
  *
- *   cc_verify_batch / cc_verify_batch_device
+ *   cc_verify_batch / cc_verify_batch_device / cc_verify_batch_pervk_device
  *        replaces  Signature::verify              src/signature.rs:473-478
  *                  (-> ps_sig Signature::verify [EXT], via transforms signature.rs:83-104)
  *   cc_signature_aggregate_batch
@@ -106,6 +106,16 @@ cc_status cc_verify_batch(cc_ctx* ctx, size_t n, size_t q, const uint8_t* sigma1
  * asynchronous with respect to the host; synchronise the stream before reading verdicts. */
 cc_status cc_verify_batch_device(cc_ctx* ctx, size_t n, size_t q, const uint8_t* d_sigma1, const uint8_t* d_sigma2,
                                  const uint8_t* d_msgs, uint8_t* d_verdicts, uint8_t* d_gt_or_null, void* stream);
+
+/* Per-credential verkeys with every buffer in device memory: Signature::verify(msgs, vk_i, params) for
+ * each credential i with ITS OWN verkey (src/signature.rs:473-478 takes the verkey per call;
+ * ps_sig's var-time MSM over [X~, Y~_1..q]): d_vk_X n x OtherGroup, d_vk_Y n x q x OtherGroup, the
+ * rest as cc_verify_batch_device.  Needs only cc_set_params (g~); q <= 4096.  Asynchronous on
+ * `stream` (NULL: the context stream). */
+cc_status cc_verify_batch_pervk_device(cc_ctx* ctx, size_t n, size_t q, const uint8_t* d_sigma1,
+                                       const uint8_t* d_sigma2, const uint8_t* d_msgs, const uint8_t* d_vk_X,
+                                       const uint8_t* d_vk_Y, uint8_t* d_verdicts, uint8_t* d_gt_or_null,
+                                       void* stream);
 
 /* RLC batch mode, multi-GPU form.  Each GPU reduces its shard to one 145-word
  * partial (Fp12 Miller product in the library's Montgomery words + an identity flag); the caller

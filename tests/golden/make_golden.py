@@ -113,6 +113,62 @@ def make_verify(mode, q, ncred, seed, per_cred_vk=False):
     return out
 
 
+PERVK_EDGES = ["vk_x_identity", "vk_y_identity", "vk_dup_bases", "vk_y_offcurve", "msg_zero", "msg_r_minus_1",
+               "msg_nibbles_8", "msg_noncanonical", "msg_top_nibble"]
+
+
+def make_verify_pervk_edges(mode, q, seed):
+    """Per-credential verkeys (Signature::verify takes the verkey per call, signature.rs:473-478) at
+    msg_count q: the corruption kinds of make_verify, each under its own key, then the edge cases of
+    a variable-base MSM over [X~, Y~_1..q]: identity X~ or Y~_j (x = 0 / y_j = 0), repeated bases, an
+    off-curve Y~_j (AMCL decodes it to the identity, so the credential fails), scalars 0, r - 1, all
+    radix-16 digits 8 (the signed recoding's carry chain), a message given as m + r (48 bytes: decoded
+    mod r) and one whose top nibble is set."""
+    grp, rng, params, sx, sy, signers, vk = setup(mode, q, 3, 5, seed)
+    base = make_verify(mode, q, 28, seed, per_cred_vk=True)
+    creds = base["creds"]
+    for kind in PERVK_EDGES:
+        sk = (rng.fr(), [rng.fr() for _ in range(q)])
+        msgs = [rng.fr() for _ in range(q)]
+        enc_msgs = None
+        if kind == "vk_x_identity":
+            sk = (0, sk[1])
+        elif kind == "vk_y_identity":
+            sk = (sk[0], [0 if j % 2 == 1 else y for j, y in enumerate(sk[1])])
+        elif kind == "vk_dup_bases":
+            sk = (sk[0], [sk[1][0]] * q)
+        elif kind == "msg_zero":
+            msgs = [0] + msgs[1:]
+        elif kind == "msg_r_minus_1":
+            msgs = [B.R - 1] * q
+        elif kind == "msg_nibbles_8":
+            msgs = [int("8" * 63, 16) % B.R] + [int("8" * 62, 16)] * (q - 1)
+        elif kind == "msg_noncanonical":
+            enc_msgs = [(m + B.R).to_bytes(48, "big").hex() for m in msgs]
+        elif kind == "msg_top_nibble":
+            msgs = [B.R - (1 << 200) - j for j in range(q)]
+        cvk = (grp.other.mul(params["g_tilde"], sk[0]) if sk[0] else None,
+               [grp.other.mul(params["g_tilde"], y) if y else None for y in sk[1]])
+        h = grp.sig.mul(grp.sig.gen, rng.fr())
+        sig = C.sign(grp, sk, msgs, h)
+        vkj = vk_json(grp, cvk)
+        vk_used = cvk
+        if kind == "vk_y_offcurve":
+            bb = bytearray.fromhex(vkj["Y"][1])
+            bb[-1] ^= 1  # y flipped: off the curve -> decoded as the identity
+            vkj["Y"][1] = bb.hex()
+            vk_used = (cvk[0], [None if j == 1 else y for j, y in enumerate(cvk[1])])
+        s1b, s2b = grp.sig_to_bytes(sig[0]), grp.sig_to_bytes(sig[1])
+        verdict, gt = C.verify_gt(grp, (grp.sig_from_bytes(s1b), grp.sig_from_bytes(s2b)), msgs, vk_used,
+                                  params["g_tilde"])
+        assert verdict == (kind != "vk_y_offcurve"), kind
+        creds.append({"kind": kind, "sigma1": hx(s1b), "sigma2": hx(s2b),
+                      "msgs": enc_msgs or [fr_hex(m) for m in msgs], "verdict": int(verdict),
+                      "gt": hx(B.gt_to_bytes(gt)), "vk": vkj})
+        print(f"  verify-pervk {mode} q={q} {kind} -> {int(verdict)}", flush=True)
+    return base
+
+
 def make_aggregate(mode, seed, q=6, t=3, n=6, big=False):
     """Config 1-style keygen + the reference's aggregation test shapes
     (signature.rs:537-580 ids 1..t and gaps {1,3,5}; 761-822 sig set {1,3,5} vs vk set {2,4,6};
@@ -431,6 +487,8 @@ def main():
         if want("verify"):
             write(f"verify_{mode.lower()}_q6.json", make_verify(mode, 6, 30, 2))
             write(f"verify_{mode.lower()}_q16_pervk.json", make_verify(mode, 16, 6, 3, per_cred_vk=True))
+        if want("pervk6"):
+            write(f"verify_{mode.lower()}_q6_pervk.json", make_verify_pervk_edges(mode, 6, 12))
         if want("aggregate"):
             write(f"aggregate_{mode.lower()}.json", make_aggregate(mode, 4))
         if want("pok"):

@@ -63,3 +63,42 @@ def test_package_import_requires_built_library(tmp_path):
     r = subprocess.run([sys.executable, "-c", "import coconut"], cwd=os.path.join(ROOT, "coconut-rust_amd"),
                        env=env, capture_output=True, text=True)
     assert r.returncode != 0 and "no CPU fallback" in r.stderr
+
+
+def _makefile_flags():
+    mk = open(os.path.join(ROOT, "coconut-rust_amd", "Makefile")).read()
+    flags = re.search(r"^FLAGS \?= (.*)$", mk, flags=re.M).group(1)
+    arch = re.search(r"^ARCH \?= (.*)$", mk, flags=re.M).group(1).strip()
+    return flags.replace("$(ARCH)", arch)
+
+
+def test_version_carries_the_source_hash_of_this_tree():
+    """cc_version() embeds tools/src_hash.py's hash of csrc/, the header, the Makefile and the flags: the
+    loaded library was built from exactly these sources (the default build)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from src_hash import src_hash
+    import coconut
+    h = src_hash(_makefile_flags())
+    assert len(h) == 16
+    assert coconut.source_hash() == h, (coconut.version(), h)
+
+
+def test_source_hash_changes_with_the_sources(tmp_path):
+    import shutil
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from src_hash import src_hash
+    root = tmp_path / "tree"
+    shutil.copytree(os.path.join(ROOT, "coconut-rust_amd", "csrc"), root / "coconut-rust_amd" / "csrc")
+    shutil.copy(os.path.join(ROOT, "coconut-rust_amd", "Makefile"), root / "coconut-rust_amd" / "Makefile")
+    (root / "include").mkdir()
+    shutil.copy(HDR, root / "include" / "coconut_hip.h")
+    flags = _makefile_flags()
+    h0 = src_hash(flags, str(root))
+    assert h0 == src_hash(flags, ROOT)
+    f = root / "coconut-rust_amd" / "csrc" / "fexp_q.hip"
+    f.write_bytes(f.read_bytes() + b"\n")
+    h1 = src_hash(flags, str(root))
+    assert h1 != h0
+    assert src_hash(flags + " -DX", ROOT) != h0

@@ -43,7 +43,8 @@ def test_verify_shared_vk_golden(ctxs, name):
         assert gts[576 * i:576 * (i + 1)].hex() == c["gt"], (i, c["kind"])
 
 
-@pytest.mark.parametrize("name", ["verify_g2_q16_pervk.json", "verify_g1_q16_pervk.json"])
+@pytest.mark.parametrize("name", ["verify_g2_q16_pervk.json", "verify_g1_q16_pervk.json", "verify_g2_q6_pervk.json",
+                                  "verify_g1_q6_pervk.json"])
 def test_verify_per_credential_vk_golden(ctxs, name):
     from coconut import verify_batch
     d = golden(name)
@@ -57,6 +58,120 @@ def test_verify_per_credential_vk_golden(ctxs, name):
     for i, c in enumerate(cr):
         assert v[i] == c["verdict"], (i, c["kind"])
         assert gts[576 * i:576 * (i + 1)].hex() == c["gt"], (i, c["kind"])
+
+
+@pytest.mark.parametrize("name", ["verify_g2_q6_pervk.json", "verify_g1_q6_pervk.json"])
+def test_verify_pervk_device_entry_golden(ctxs, name):
+    """cc_verify_batch_pervk_device (HBM-resident batch, one verkey per credential): the q = 6 per-verkey
+    fixture — every corruption kind plus the variable-base MSM's edge cases (identity / repeated /
+    off-curve bases, scalars 0, r - 1, all digits 8, m + r, a high top nibble) — gives the oracle's
+    verdicts and GT bytes; ragged batch sizes 1 and 3 reuse the same scratch."""
+    import torch
+    from coconut import _lib
+    d = golden(name)
+    ctx = ctxs[d["mode"]]
+    ctx.set_params(bytes.fromhex(d["g_tilde"]))
+    dev = torch.device("cuda", 0)
+    to = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)  # noqa: E731
+    P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    for sel in (slice(None), slice(0, 1), slice(5, 8)):
+        cr = d["creds"][sel]
+        n = len(cr)
+        D = [to(_cat(c[k] for c in cr)) for k in ("sigma1", "sigma2")]
+        D.append(to(_cat(m for c in cr for m in c["msgs"])))
+        D.append(to(_cat(c["vk"]["X"] for c in cr)))
+        D.append(to(_cat(y for c in cr for y in c["vk"]["Y"])))
+        v = torch.zeros(n, dtype=torch.uint8, device=dev)
+        gt = torch.zeros(n * 576, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        assert _lib.lib.cc_verify_batch_pervk_device(ctx.h, n, d["q"], *[P(x) for x in D], P(v), P(gt), None) == 0
+        torch.cuda.synchronize()
+        v, gt = v.cpu().numpy(), bytes(gt.cpu().numpy())
+        for i, c in enumerate(cr):
+            assert v[i] == c["verdict"], (i, c["kind"])
+            assert gt[576 * i:576 * (i + 1)].hex() == c["gt"], (i, c["kind"])
+
+
+def _be48(v):
+    return int(v).to_bytes(48, "big")
+
+
+def make_pervk_batch(ctx, mode, n, q, seed, bad_every=16):
+    """n credentials, each under ITS OWN verkey (x_i, y_ij random; X~_i = x_i g~, Y~_ij = y_ij g~ built by
+    the product's cc_fixed_base_mul), sigma_1 = k G, sigma_2 = k (x_i + sum y_ij m_ij) G; every
+    bad_every-th corrupted, cycling sigma_2 + G / m_0 + 1 / sigma_2 under another credential's key."""
+    import coconut
+    R = coconut.signature.R_ORDER
+    rng = np.random.default_rng(seed)
+    og, sg = (1, 2) if mode == 0 else (2, 1)
+    gen = {1: coconut.G1_GENERATOR, 2: coconut.G2_GENERATOR}
+    gk = int(rng.integers(1, 2**62))
+    g_tilde = coconut.fixed_base_mul(ctx, og, gen[og], _be48(gk))
+    sk = rng.integers(1, 2**62, size=(n, q + 1), dtype=np.int64)
+    msgs = rng.integers(0, 2**62, size=(n, q), dtype=np.int64)
+    ks = rng.integers(1, 2**62, size=n, dtype=np.int64)
+    vk_sc, e1, e2 = [], [], []
+    expect = np.ones(n, np.uint8)
+    for i in range(n):
+        row = [int(v) for v in sk[i]]
+        m = [int(v) for v in msgs[i]]
+        vk_sc.extend(v * gk % R for v in row)
+        x = row[0]
+        if bad_every and i % bad_every == bad_every - 1:
+            expect[i] = 0
+            kind = (i // bad_every) % 3
+            if kind == 1:
+                m = [m[0] + 1] + m[1:]
+            elif kind == 2:
+                x = int(sk[(i + 1) % n][0])
+        e = int(ks[i]) * (x + sum(y * mm for y, mm in zip(row[1:], m))) % R
+        if bad_every and i % bad_every == bad_every - 1 and (i // bad_every) % 3 == 0:
+            e = (e + 1) % R
+        e1.append(_be48(int(ks[i])))
+        e2.append(_be48(e))
+    ob = 97 if og == 1 else 192
+    vk = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(_be48(v) for v in vk_sc))
+    X = b"".join(vk[(i * (q + 1)) * ob:(i * (q + 1) + 1) * ob] for i in range(n))
+    Y = b"".join(vk[(i * (q + 1) + 1) * ob:(i + 1) * (q + 1) * ob] for i in range(n))
+    s1 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e1))
+    s2 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e2))
+    mb = b"".join(_be48(int(v)) for v in msgs.reshape(-1))
+    return dict(X=X, Y=Y, g_tilde=g_tilde, s1=s1, s2=s2, msgs=mb, expect=expect)
+
+
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_pervk_full_size_65536_distinct_verkeys(ctxs, mode):
+    """Config 2's size with a DISTINCT verkey per credential (65,536 credentials, q = 6): verdicts equal
+    construction through cc_verify_batch_pervk_device; a 128-credential sample's GT bytes equal the C
+    oracle's (per-credential verkeys)."""
+    import torch
+    from coconut import _lib
+    m = MODES[mode]
+    n, q = 65536, 6
+    ctx = ctxs[mode]
+    b = make_pervk_batch(ctx, m, n, q, seed=777 + m)
+    ctx.set_params(b["g_tilde"])
+    dev = torch.device("cuda", 0)
+    to = lambda x: torch.frombuffer(bytearray(x), dtype=torch.uint8).to(dev)  # noqa: E731
+    P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    D = [to(b[k]) for k in ("s1", "s2", "msgs", "X", "Y")]
+    v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    k0, k = 40000, 128
+    gt = torch.zeros(n * 576, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    assert _lib.lib.cc_verify_batch_pervk_device(ctx.h, n, q, *[P(x) for x in D], P(v), P(gt), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(v.cpu().numpy(), b["expect"])
+    sb, ob = (192, 97) if m == 0 else (97, 192)
+    oc = oracle_lib()
+    ver = ctypes.create_string_buffer(k)
+    gts = ctypes.create_string_buffer(576 * k)
+    oc.oc_verify_batch(m, ctypes.c_size_t(k), ctypes.c_size_t(q), b["s1"][k0 * sb:(k0 + k) * sb],
+                       b["s2"][k0 * sb:(k0 + k) * sb], b["msgs"][k0 * q * 48:(k0 + k) * q * 48],
+                       b["X"][k0 * ob:(k0 + k) * ob], b["Y"][k0 * q * ob:(k0 + k) * q * ob], 1, b["g_tilde"], ver, gts,
+                       host_threads())
+    assert np.array_equal(np.frombuffer(ver.raw, np.uint8), b["expect"][k0:k0 + k])
+    assert bytes(gt[k0 * 576:(k0 + k) * 576].cpu().numpy()) == gts.raw
 
 
 def test_single_signature_verify_api(ctxs):

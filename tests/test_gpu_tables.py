@@ -2,8 +2,11 @@
 context state after a failed table build (C ABI cc_set_table_bits / cc_table_bits /
 cc_device_error):
 
-* shared-verkey tables at 8 and 16 bits: the golden verify and PoK fixtures (both group modes) give
-  the oracle's verdicts and GT bytes with either width;
+* shared-verkey tables at 8 to 22 bits: the golden verify and PoK fixtures (both group modes) give
+  the oracle's verdicts and GT bytes with every width;
+* the default table budget (4 GiB: config 2's q = 6 gets 18 bits) and the boundary's idempotence: a
+  repeated identical cc_set_params / cc_set_verkey returns without rebuilding (< 1 ms), a changed
+  width or key rebuilds;
 * issuer tables at every width the budget can pick (8, 10, 12, 13, 16): the golden Verkey::aggregate
   cases;
 * a verkey too large for wide tables (q = 2,048 in SigG1: 410 GB at 16 bits) falls back to 8 bits and verifies;
@@ -32,7 +35,7 @@ def _ctx(mode):
     return coconut.Context(0, coconut.GroupMode(0 if mode == "G2" else 1))
 
 
-@pytest.mark.parametrize("bits", [8, 16])
+@pytest.mark.parametrize("bits", [8, 12, 16, 18, 20, 22])
 @pytest.mark.parametrize("name", ["verify_g2_q6.json", "verify_g1_q6.json"])
 def test_verkey_table_widths_verify_golden(name, bits):
     from coconut import verify_batch
@@ -110,6 +113,60 @@ def test_issuer_table_widths_golden(name, bits):
 
 def _be(v):
     return int(v % R).to_bytes(48, "big")
+
+
+def _table_gib(mode_other_group, q, bits):
+    nwin = (256 + bits - 1) // bits
+    entry = 96 if mode_other_group == 1 else 192
+    return (q + 2) * nwin * ((1 << bits) - 1) * entry / 2**30
+
+
+def test_default_table_budget_and_idempotent_boundary():
+    """Library default: the widest window whose q + 2 bases fit 4 GiB (q = 6 SigG2: 18 bits, 3.0 GB);
+    a repeated identical cc_set_params / cc_set_verkey through the C ABI (no Python cache in the way)
+    returns in < 1 ms without rebuilding; a new key or a new forced width rebuilds; verdicts stay the
+    oracle's throughout."""
+    import time
+    from coconut import _lib, verify_batch
+    d = golden("verify_g2_q6.json")
+    ctx = _ctx("G2")
+    try:
+        g = bytes.fromhex(d["g_tilde"])
+        X = bytes.fromhex(d["vk"]["X"])
+        Y = b"".join(bytes.fromhex(y) for y in d["vk"]["Y"])
+        q = d["q"]
+        L = _lib.lib
+        assert L.cc_set_params(ctx.h, g) == 0
+        t0 = time.perf_counter()
+        assert L.cc_set_verkey(ctx.h, X, Y, q) == 0
+        build_ms = (time.perf_counter() - t0) * 1e3
+        bits = ctx.table_bits()[0]
+        assert bits == 18, bits
+        assert _table_gib(1, q, bits) <= 4.0
+        times = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            assert L.cc_set_params(ctx.h, g) == 0
+            assert L.cc_set_verkey(ctx.h, X, Y, q) == 0
+            times.append((time.perf_counter() - t0) * 1e3)
+        assert min(times) < 1.0, (times, build_ms)
+        ctx._gtilde, ctx._vk = g, (X, Y)
+        cr = d["creds"]
+        args = (ctx, len(cr), q, _cat(c["sigma1"] for c in cr), _cat(c["sigma2"] for c in cr),
+                _cat(m for c in cr for m in c["msgs"]))
+        assert [int(v) for v in verify_batch(*args)] == [c["verdict"] for c in cr]
+        # another key (X~ and Y~_0 swapped) rebuilds: the honest credentials now fail
+        Ysw = X + Y[97:]
+        assert L.cc_set_verkey(ctx.h, Y[:97], Ysw, q) == 0
+        assert not any(int(v) for v in verify_batch(*args))
+        assert L.cc_set_verkey(ctx.h, X, Y, q) == 0
+        # a new forced width rebuilds the same key at that width
+        assert L.cc_set_table_bits(ctx.h, 12, 0) == 0
+        assert L.cc_set_verkey(ctx.h, X, Y, q) == 0
+        assert ctx.table_bits()[0] == 12
+        assert [int(v) for v in verify_batch(*args)] == [c["verdict"] for c in cr]
+    finally:
+        ctx.close()
 
 
 def test_large_verkey_falls_back_to_8_bits_and_failed_build_leaves_no_verkey():

@@ -119,6 +119,7 @@ def _verify_fixture_c(oc, name):
 
 
 @pytest.mark.parametrize("name", ["verify_g2_q6.json", "verify_g1_q6.json", "verify_g2_q16_pervk.json",
+                                  "verify_g2_q6_pervk.json", "verify_g1_q6_pervk.json",
                                   "verify_g1_q16_pervk.json", "verify_g2_q16.json", "verify_g1_q16.json"])
 def test_c_oracle_matches_golden_verify(oc, name):
     d, ver, gts = _verify_fixture_c(oc, name)

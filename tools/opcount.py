@@ -561,6 +561,11 @@ def verify_sigg2(cred, vk_aff, gtil_aff, q):
         lo = fixed_table_mul_add(G1, lo, msgs[j], Ys[j], 0, nw // 2, VK_WBITS)
         hi = fixed_table_mul_add(G1, hi, msgs[j], Ys[j], nw // 2, nw, VK_WBITS)
     pr = G1.add_j(lo, hi)
+    return _pair_sigg2(s1, s2, pr, gtil_aff, counts)
+
+
+def _pair_sigg2(s1, s2, pr, gtil_aff, counts):
+    """The Miller loop and final exponentiation of a SigG2 verify after its prep (pr Jacobian G1)."""
     pr_inf = G1.is_inf(pr)
     pe = None
     if not pr_inf:
@@ -591,6 +596,11 @@ def verify_sigg1(cred, vk_aff, gtil_aff, q):
     for j in range(q):
         acc = fixed_table_mul_add(G2, acc, msgs[j], Ys[j], 0, -(-256 // VK_WBITS), VK_WBITS)
     pr = G2.to_aff(acc)
+    return _pair_sigg1(s1, s2, pr, gtil_aff, counts)
+
+
+def _pair_sigg1(s1, s2, pr, gtil_aff, counts):
+    """The Miller loop (g~ lines precomputed) and final exponentiation of a SigG1 verify after its prep."""
     counts["prep"] = C.take()
     # pair 0: (pr, sigma_1); pair 1: (g~ [precomputed lines: no line cost], -sigma_2)
     skip0 = s1 is None or pr is None
@@ -647,8 +657,9 @@ def recode_w4(k):
     return d
 
 
-def straus(g, pts, scalars):
-    """k_msm_straus: signed 4-bit windows, multiples 1P..8P batch-normalised with one inversion."""
+def straus(g, pts, scalars, to_affine=True):
+    """k_msm_straus / straus.h: signed 4-bit windows, multiples 1P..8P batch-normalised with one inversion
+    (to_affine=False: the Jacobian sum, as the per-credential-verkey preps use it)."""
     ent = []
     acc_z = g.one
     for P in pts:
@@ -691,7 +702,26 @@ def straus(g, pts, scalars):
             if d < 0:
                 e = (e[0], g.neg(e[1]))
             acc = g.add_aff(acc, e)
-    return g.to_aff(acc)
+    return g.to_aff(acc) if to_affine else acc
+
+
+def verify_pervk(cred, gtil_aff, mode):
+    """pervk.hip k_prep_sig*_var (Straus over [Y~_1..q] with the messages, + X~) -> k_miller -> k_fexp.
+    Counted as ONE Straus over all q bases: the SigG2 kernel splits the bases over a lane pair and
+    repeats the doubling chain on both lanes, which is not counted (the conservative figure)."""
+    counts = {}
+    gs, go = (G2, G1) if mode == "G2" else (G1, G2)
+    s1 = decode(gs, bytes.fromhex(cred["sigma1"]))
+    s2 = decode(gs, bytes.fromhex(cred["sigma2"]))
+    X = decode(go, bytes.fromhex(cred["vk"]["X"]))
+    Ys = [decode(go, bytes.fromhex(y)) for y in cred["vk"]["Y"]]
+    msgs = [int.from_bytes(bytes.fromhex(m), "big") % R for m in cred["msgs"]]
+    acc = straus(go, Ys, msgs, to_affine=False)
+    if X:
+        acc = go.add_aff(acc, X)
+    if mode == "G2":
+        return _pair_sigg2(s1, s2, acc, gtil_aff, counts)
+    return _pair_sigg1(s1, s2, go.to_aff(acc), gtil_aff, counts)
 
 
 def _raw_mul(g, a, b):
@@ -799,6 +829,50 @@ def pok_sigg2(d, p, vk_aff, gtil):
     counts["fexp"] = C.take()
     ok = f12_is_one(r) and s1 is not None and s2 is not None and schnorr_ok
     return int(ok), counts
+
+
+def pok_sigg1(d, p, vk_aff, gtil):
+    """k_prep_pok_g1pl (SigG1: the Schnorr MSM and J' in G2 on lane pairs) -> k_miller<1,false> -> k_fexp."""
+    counts = {}
+    q, rev = d["q"], d["revealed"]
+    X, Ys = vk_aff
+    s1 = decode(G1, bytes.fromhex(p["sigma1"]))
+    s2 = decode(G1, bytes.fromhex(p["sigma2"]))
+    Ja = decode(G2, bytes.fromhex(p["J"]))
+    resp = [int(h, 16) % R for h in p["responses"]]
+    chal = int(p["chal"], 16) % R
+    nw = -(-256 // VK_WBITS)
+    acc = fixed_table_mul_add(G2, G2.inf(), resp[0], gtil, 0, nw, VK_WBITS)
+    slot = 1
+    for h in range(q):
+        if h in rev:
+            continue
+        acc = fixed_table_mul_add(G2, acc, resp[slot], Ys[h], 0, nw, VK_WBITS)
+        slot += 1
+    if Ja:  # chal J in fixed 4-bit windows from a per-lane table of d J, d = 1..15
+        tab = [(Ja[0], Ja[1], F2_ONE)]
+        for _ in range(14):
+            tab.append(G2.add_aff(tab[-1], Ja))
+        sacc = G2.inf()
+        for win in range(63, -1, -1):
+            for _ in range(4):
+                sacc = G2.dbl_j(sacc)
+            dd = (chal >> (4 * win)) & 15
+            if dd:
+                sacc = G2.add_j(sacc, tab[dd - 1])
+        acc = G2.add_j(acc, sacc)
+    Ta = decode(G2, bytes.fromhex(p["T"]))
+    if Ta:
+        acc = G2.add_aff(acc, (Ta[0], G2.neg(Ta[1])))
+    schnorr_ok = G2.is_inf(acc)
+    jp = (X[0], X[1], F2_ONE)
+    if Ja:
+        jp = G2.add_aff(jp, Ja)
+    for z, h in enumerate(rev):
+        jp = fixed_table_mul_add(G2, jp, int(p["revealed_msgs"][z], 16) % R, Ys[h], 0, nw, VK_WBITS)
+    pr = G2.to_aff(jp)
+    v, _, cnt = _pair_sigg1(s1, s2, pr, gtil, counts)
+    return int(v and schnorr_ok), cnt
 
 
 # ---------------------------------------------------------------- RLC batch mode (rlc.hip + fold.hip, SigG2)
@@ -952,6 +1026,55 @@ def main():
                 "credentials (the fold's per-window bucket combination, ~30 G2 operations a lane on 16 "
                 "waves, is not counted: < 0.01 M a credential); reduce = the tree's Fp12 products over "
                 "65,536 + 16 values, per credential"}
+    # per-credential verkeys (Signature::verify with the caller's verkey; pervk.hip), q = 6
+    VK_WBITS = 22
+    for name, key, mode in (("verify_g2_q6_pervk.json", "verify_sigg2_q6_pervk", "G2"),
+                            ("verify_g1_q6_pervk.json", "verify_sigg1_q6_pervk", "G1")):
+        with open(os.path.join(root, "tests", "golden", name)) as f:
+            d = json.load(f)
+        gt = decode(G1 if mode == "G2" else G2, bytes.fromhex(d["g_tilde"]))
+        C.take()
+        rows = []
+        for c in d["creds"]:
+            v, gtb, cnt = verify_pervk(c, gt, mode)
+            assert v == c["verdict"] and gtb.hex() == c["gt"], c["kind"]
+            if c["kind"] == "valid":
+                rows.append(cnt)
+        res["configs"][key] = {
+            "credentials_averaged": len(rows),
+            "M_per_credential": {k: round(sum(r[k] for r in rows) / len(rows), 1) for k in rows[0]},
+            "mads_per_credential": {k: round(sum(r[k] for r in rows) / len(rows) * 288) for k in rows[0]},
+            "note": f"valid credentials of tests/golden/{name} (verdicts and GT bytes of every kind checked); prep = "
+                    "one signed-4-bit Straus over the q bases + X~ (the kernel's repeated doubling chain on the "
+                    "second lane of a SigG2 pair is not counted)"}
+    # SigG1 forms of configs 4 and 5
+    with open(os.path.join(root, "tests", "golden", "aggregate_g1_t67_subsets.json")) as f:
+        d = json.load(f)
+    sig, vkX, vkY, cnt = aggregate_case(d, d["cases"][0])
+    assert enc(G1, sig).hex() == d["cases"][0]["out_sigma2"] and enc(G2, vkX).hex() == d["cases"][0]["out_X"]
+    res["configs"]["aggregate_sigg1_t67"] = {
+        "credentials_averaged": 1, "M_per_credential": cnt,
+        "mads_per_credential": {k: v * 288 for k, v in cnt.items()},
+        "note": "SigG1: straus_sigma2 = Signature::aggregate (67-point G1 Straus MSM); fixed_verkey = Verkey::aggregate "
+                "(q+1 = 7 67-point G2 fixed-base MSMs from the issuer tables at the width cc_set_issuers picks for "
+                "100 issuers x 7 G2 keys); case 0 of tests/golden/aggregate_g1_t67_subsets.json, outputs checked"}
+    with open(os.path.join(root, "tests", "golden", "pok_g1_q32.json")) as f:
+        d = json.load(f)
+    VK_WBITS = 20
+    g2 = lambda h: decode(G2, bytes.fromhex(h))  # noqa: E731
+    vk, gt = (g2(d["vk"]["X"]), [g2(y) for y in d["vk"]["Y"]]), g2(d["g_tilde"])
+    C.take()
+    rows = []
+    for p in d["proofs"]:
+        v, cnt = pok_sigg1(d, p, vk, gt)
+        assert v == p["verdict"], p["kind"]
+        if p["kind"] == "valid":
+            rows.append(cnt)
+    res["configs"]["pok_sigg1_q32_r8"] = {
+        "credentials_averaged": len(rows),
+        "M_per_credential": {k: round(sum(r[k] for r in rows) / len(rows), 1) for k in rows[0]},
+        "mads_per_credential": {k: round(sum(r[k] for r in rows) / len(rows) * 288) for k in rows[0]},
+        "note": "SigG1, valid proofs of tests/golden/pok_g1_q32.json (verdicts of every kind checked), 20-bit tables"}
     out = os.path.join(root, "tests", "fixtures", "opcount.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:
