@@ -10,6 +10,7 @@ the serialized inputs already resident in HBM (cc_verify_batch_device).
 
 Other modes (one JSON line each; the headline is the default):
   --mode verify-g1   config 2 in the literal "G2 MSM" layout (SigG1: sigma in G1, verkey in G2)
+  --mode verify-pervk  config 2's size with a distinct verkey per credential (per-call Signature::verify)
   --mode rlc         config 3: q = 16, 131,072 credentials per GPU, RLC batch mode, RCCL all-gather
   --mode aggregate   config 4: Signature::aggregate + Verkey::aggregate, t = 67 of n = 100, 10k creds
   --mode pok         config 5: PoKOfSignatureProof::verify, q = 32, revealed {3,5,7,11,13,17,19,23}
@@ -311,18 +312,21 @@ def cpu_verify_rate(batch, threads, target_s):
     oc = _oracle()
     mode, q = batch["mode"], batch["q"]
     sb = 192 if mode == 0 else 97
+    ob = 97 if mode == 0 else 192
+    per = 1 if batch.get("per_vk") else 0  # one verkey per credential (X: n x ob, Y: n x q x ob)
+    vk = lambda k: (batch["X"][:k * ob], batch["Y"][:k * q * ob]) if per else (batch["X"], batch["Y"])  # noqa: E731
     k0 = max(2, threads * 2)
     ver = ctypes.create_string_buffer(k0)
     t = time.perf_counter()
     oc.oc_verify_batch(mode, ctypes.c_size_t(k0), ctypes.c_size_t(q), batch["s1"][:k0 * sb], batch["s2"][:k0 * sb],
-                       batch["msgs"][:k0 * q * 48], batch["X"], batch["Y"], 0, batch["g_tilde"], ver, None, threads)
+                       batch["msgs"][:k0 * q * 48], *vk(k0), per, batch["g_tilde"], ver, None, threads)
     per = (time.perf_counter() - t) / k0
     k = int(min(batch["n"], max(threads * 4, target_s / max(per, 1e-6))))
     k = max(threads, (k // threads) * threads)
     ver = ctypes.create_string_buffer(k)
     t = time.perf_counter()
     oc.oc_verify_batch(mode, ctypes.c_size_t(k), ctypes.c_size_t(q), batch["s1"][:k * sb], batch["s2"][:k * sb],
-                       batch["msgs"][:k * q * 48], batch["X"], batch["Y"], 0, batch["g_tilde"], ver, None, threads)
+                       batch["msgs"][:k * q * 48], *vk(k), per, batch["g_tilde"], ver, None, threads)
     dt = time.perf_counter() - t
     agree = bool(np.array_equal(np.frombuffer(ver.raw, np.uint8), batch["expect"][:k]))
     return k / dt, k, dt, agree
@@ -642,7 +646,8 @@ def main():
     ap.add_argument("--vk-bits", type=int, default=None,
                     help="verkey table window width (cc_set_table_bits; 0 = the library's <= 4 GiB default; "
                          "unset = the mode's opt-in width, BENCH_VK_BITS)")
-    ap.add_argument("--mode", choices=["verify", "verify-g1", "rlc", "aggregate", "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
+    ap.add_argument("--mode", choices=["verify", "verify-g1", "verify-pervk", "verify-pervk-g1", "rlc", "aggregate",
+                                       "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
     args = ap.parse_args()
     if args.backend:
         BACKEND = args.backend
@@ -661,6 +666,9 @@ def main():
         return bench_verify(args, 1)
     if args.mode == "rlc":
         return bench_rlc(args)
+    if args.mode in ("verify-pervk", "verify-pervk-g1"):
+        from bench_modes import bench_pervk
+        return bench_pervk(args)
     if args.mode in ("aggregate", "aggregate-g1"):
         from bench_modes import bench_aggregate
         return bench_aggregate(args)

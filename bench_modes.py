@@ -5,6 +5,9 @@ config 4 (--mode aggregate): Threshold aggregation at scale — per credential o
   Signature::aggregate (signature.rs:448-470) over the partial signatures of a seeded random
   67-subset of n = 100 issuers, and one Verkey::aggregate (signature.rs:483-526) of the same
   subset's verkeys from the resident issuer table (cc_set_issuers).  10,000 credentials per GPU.
+verify with per-credential verkeys (--mode verify-pervk / verify-pervk-g1): config 2's size (65,536
+  credentials, q = 6) where every credential carries ITS OWN verkey, the reference's per-call
+  Signature::verify(msgs, vk, params) (signature.rs:473-478): a variable-base Straus MSM per credential.
 config 5 (--mode pok): PoKOfSignatureProof::verify (ps_sig [EXT], reference pok_sig.rs:103-105),
   q = 32, revealed {3,5,7,11,13,17,19,23}, 65,536 proofs per GPU; 1/16 with a corrupted response.
 
@@ -116,6 +119,48 @@ def make_pok_batch(ctx, mode, n, q=32, revealed=REVEALED, seed=5, bad_every=16):
     T = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(ts))
     return dict(mode=mode, n=n, q=q, revealed=list(revealed), X=X, Y=Y, g_tilde=g_tilde, s1=S1, s2=S2, J=J, T=T,
                 resp=b"".join(resp), chal=b"".join(chal), rev=b"".join(rev), nresp=len(hidden) + 1, expect=expect)
+
+
+def make_pervk_batch(ctx, mode, n, q, seed, bad_every=16):
+    """n credentials, each under ITS OWN verkey (x_i, y_ij random; X~_i = x_i g~, Y~_ij = y_ij g~ built by
+    the product's cc_fixed_base_mul), sigma_1 = k G, sigma_2 = k (x_i + sum y_ij m_ij) G; every
+    bad_every-th corrupted, cycling sigma_2 + G / m_0 + 1 / sigma_2 under another credential's key."""
+    import coconut
+    rng = np.random.default_rng(seed)
+    og, sg = (1, 2) if mode == 0 else (2, 1)
+    gen = {1: coconut.G1_GENERATOR, 2: coconut.G2_GENERATOR}
+    gk = int(rng.integers(1, 2**62))
+    g_tilde = coconut.fixed_base_mul(ctx, og, gen[og], _be(gk))
+    sk = rng.integers(1, 2**62, size=(n, q + 1), dtype=np.int64)
+    msgs = rng.integers(0, 2**62, size=(n, q), dtype=np.int64)
+    ks = rng.integers(1, 2**62, size=n, dtype=np.int64)
+    vk_sc, e1, e2 = [], [], []
+    expect = np.ones(n, np.uint8)
+    for i in range(n):
+        row = [int(v) for v in sk[i]]
+        m = [int(v) for v in msgs[i]]
+        vk_sc.extend(v * gk % R for v in row)
+        x = row[0]
+        if bad_every and i % bad_every == bad_every - 1:
+            expect[i] = 0
+            kind = (i // bad_every) % 3
+            if kind == 1:
+                m = [m[0] + 1] + m[1:]
+            elif kind == 2:
+                x = int(sk[(i + 1) % n][0])
+        e = int(ks[i]) * (x + sum(y * mm for y, mm in zip(row[1:], m))) % R
+        if bad_every and i % bad_every == bad_every - 1 and (i // bad_every) % 3 == 0:
+            e = (e + 1) % R
+        e1.append(_be(int(ks[i])))
+        e2.append(_be(e))
+    ob = 97 if og == 1 else 192
+    vk = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(_be(v) for v in vk_sc))
+    X = b"".join(vk[(i * (q + 1)) * ob:(i * (q + 1) + 1) * ob] for i in range(n))
+    Y = b"".join(vk[(i * (q + 1) + 1) * ob:(i + 1) * (q + 1) * ob] for i in range(n))
+    s1 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e1))
+    s2 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e2))
+    mb = b"".join(_be(int(v)) for v in msgs.reshape(-1))
+    return dict(X=X, Y=Y, g_tilde=g_tilde, s1=s1, s2=s2, msgs=mb, expect=expect)
 
 
 def _timed(args, step, dev, dist, ctx):
@@ -344,6 +389,80 @@ def bench_pok(args):
                                              f"oc_pok_verify); verdicts agree with construction: "
                                              f"{list(ver) == list(b['expect'][:k])}",
                                    "nproc": nproc, "cpu_model": model}
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+    ctx.close()
+
+
+def bench_pervk(args):
+    """Signature::verify with a distinct verkey per credential (cc_verify_batch_pervk_device): 65,536
+    credentials, q = 6, inputs resident in HBM; verdicts checked against construction after timing."""
+    import torch
+    import coconut
+    from bench import (_dist_setup, to_dev, MADS_PER_M, peak_mad_per_s, opcounts, kernel_table, lib_info,
+                       cpu_baseline_verify)
+    world, rank, local, dist = _dist_setup()
+    dev = torch.device("cuda", local)
+    n, q = args.n or 65536, 6
+    mode = 1 if args.mode.endswith("-g1") else 0
+    ctx = coconut.Context(local, coconut.GroupMode(mode))
+    t0 = time.perf_counter()
+    b = make_pervk_batch(ctx, mode, n, q, seed=6000 + rank + 100 * mode)
+    gen_s = time.perf_counter() - t0
+    ctx.set_params(b["g_tilde"])
+    D = [to_dev(b[k], dev) for k in ("s1", "s2", "msgs", "X", "Y")]
+    d_v = torch.zeros(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.Stream(dev)
+    stream.wait_stream(torch.cuda.current_stream(dev))
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    lib = coconut._lib.lib
+    P = [ctypes.c_void_p(x.data_ptr()) for x in D]
+
+    def step():
+        st = lib.cc_verify_batch_pervk_device(ctx.h, n, q, *P, ctypes.c_void_p(d_v.data_ptr()), None, sh)
+        if st:
+            raise RuntimeError(f"cc_verify_batch_pervk_device: {lib.cc_status_str(st).decode()}")
+
+    el, phase_ms = _timed(args, step, dev, dist, ctx)
+    if not np.array_equal(d_v.cpu().numpy(), b["expect"]):
+        raise SystemExit("per-verkey verdicts disagree with construction — refusing to report a number")
+    value = n * world * args.steps / el
+    if rank == 0:
+        key = "verify_sigg2_q6_pervk" if mode == 0 else "verify_sigg1_q6_pervk"
+        counts = opcounts(key)
+        peak = peak_mad_per_s()
+        sb, ob = (192, 97) if mode == 0 else (97, 192)
+        kt = kernel_table(phase_ms, n, counts, 2 * sb + q * 48 + (q + 1) * ob, peak,
+                          "k_prep_sigg2_var" if mode == 0 else "k_prep_sigg1_var", None)
+        dom = max(kt, key=lambda k: kt[k]["ms"])
+        total = sum(counts.values()) * MADS_PER_M * n
+        out = {
+            "metric": "verified credentials/sec (msg_count=6), one verkey per credential" + ("" if mode == 0 else " [SigG1]"),
+            "value": round(value, 1), "unit": "credentials/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "int32/u32 (lazy 14 x 28-bit signed limbs in the MSM and pairing; integer-only)",
+            "data": "synthetic (seeded; 65,536 distinct verkeys x_i g~, y_ij g~ and signatures built on the GPU by "
+                    "cc_fixed_base_mul; 1/16 corrupted: sigma_2 + G, m_0 + 1, signed under another key)",
+            "config": {"workload": f"Signature::verify with per-credential verkeys: {n:,} per GPU, msg_count=6, "
+                                   + ("SigG2" if mode == 0 else "SigG1"),
+                       "credentials_per_gpu": n, "msg_count": q, "parallelism": f"shard-by-credential x{world}"},
+            **lib_info(),
+            "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
+                         "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
+                         "frac": kt[dom]["frac"], "traffic": None,
+                         "algorithmic_mads_per_credential": round(counts[dom] * MADS_PER_M),
+                         "opcount_fixture": f"tests/fixtures/opcount.json {key}",
+                         "whole_step_frac": round(total / (el / args.steps) / peak, 4)},
+            "kernels": kt,
+            "prep_over_miller": round(kt["prep"]["ms"] / kt["miller"]["ms"], 3) if kt["miller"]["ms"] else None,
+            "setup": {"synthetic_data_s": round(gen_s, 2)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            cb = dict(mode=mode, q=q, n=n, s1=b["s1"], s2=b["s2"], msgs=b["msgs"], X=b["X"], Y=b["Y"],
+                      g_tilde=b["g_tilde"], expect=b["expect"], per_vk=True)
+            out["cpu_baseline"] = cpu_baseline_verify(cb, value, "per-credential verkeys")
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -92,53 +92,6 @@ def test_verify_pervk_device_entry_golden(ctxs, name):
             assert gt[576 * i:576 * (i + 1)].hex() == c["gt"], (i, c["kind"])
 
 
-def _be48(v):
-    return int(v).to_bytes(48, "big")
-
-
-def make_pervk_batch(ctx, mode, n, q, seed, bad_every=16):
-    """n credentials, each under ITS OWN verkey (x_i, y_ij random; X~_i = x_i g~, Y~_ij = y_ij g~ built by
-    the product's cc_fixed_base_mul), sigma_1 = k G, sigma_2 = k (x_i + sum y_ij m_ij) G; every
-    bad_every-th corrupted, cycling sigma_2 + G / m_0 + 1 / sigma_2 under another credential's key."""
-    import coconut
-    R = coconut.signature.R_ORDER
-    rng = np.random.default_rng(seed)
-    og, sg = (1, 2) if mode == 0 else (2, 1)
-    gen = {1: coconut.G1_GENERATOR, 2: coconut.G2_GENERATOR}
-    gk = int(rng.integers(1, 2**62))
-    g_tilde = coconut.fixed_base_mul(ctx, og, gen[og], _be48(gk))
-    sk = rng.integers(1, 2**62, size=(n, q + 1), dtype=np.int64)
-    msgs = rng.integers(0, 2**62, size=(n, q), dtype=np.int64)
-    ks = rng.integers(1, 2**62, size=n, dtype=np.int64)
-    vk_sc, e1, e2 = [], [], []
-    expect = np.ones(n, np.uint8)
-    for i in range(n):
-        row = [int(v) for v in sk[i]]
-        m = [int(v) for v in msgs[i]]
-        vk_sc.extend(v * gk % R for v in row)
-        x = row[0]
-        if bad_every and i % bad_every == bad_every - 1:
-            expect[i] = 0
-            kind = (i // bad_every) % 3
-            if kind == 1:
-                m = [m[0] + 1] + m[1:]
-            elif kind == 2:
-                x = int(sk[(i + 1) % n][0])
-        e = int(ks[i]) * (x + sum(y * mm for y, mm in zip(row[1:], m))) % R
-        if bad_every and i % bad_every == bad_every - 1 and (i // bad_every) % 3 == 0:
-            e = (e + 1) % R
-        e1.append(_be48(int(ks[i])))
-        e2.append(_be48(e))
-    ob = 97 if og == 1 else 192
-    vk = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(_be48(v) for v in vk_sc))
-    X = b"".join(vk[(i * (q + 1)) * ob:(i * (q + 1) + 1) * ob] for i in range(n))
-    Y = b"".join(vk[(i * (q + 1) + 1) * ob:(i + 1) * (q + 1) * ob] for i in range(n))
-    s1 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e1))
-    s2 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e2))
-    mb = b"".join(_be48(int(v)) for v in msgs.reshape(-1))
-    return dict(X=X, Y=Y, g_tilde=g_tilde, s1=s1, s2=s2, msgs=mb, expect=expect)
-
-
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_pervk_full_size_65536_distinct_verkeys(ctxs, mode):
     """Config 2's size with a DISTINCT verkey per credential (65,536 credentials, q = 6): verdicts equal
@@ -149,6 +102,7 @@ def test_pervk_full_size_65536_distinct_verkeys(ctxs, mode):
     m = MODES[mode]
     n, q = 65536, 6
     ctx = ctxs[mode]
+    from bench_modes import make_pervk_batch
     b = make_pervk_batch(ctx, m, n, q, seed=777 + m)
     ctx.set_params(b["g_tilde"])
     dev = torch.device("cuda", 0)

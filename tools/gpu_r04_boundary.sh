@@ -9,3 +9,5 @@ tail -3 "$OUT/pytest_gpu.log"
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 1; }
 cat "$OUT/smoke.log"
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/verify.json" 2> "$OUT/verify.err" || { tail "$OUT/verify.err"; exit 1; }
+timeout -k 10 300 python -u bench.py --mode verify-pervk --steps 5 --warmup 1 > "$OUT/pervk.json" 2> "$OUT/pervk.err" || { tail "$OUT/pervk.err"; exit 1; }
+timeout -k 10 300 python -u bench.py --mode verify-pervk-g1 --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pervk_g1.json" 2> "$OUT/pervk_g1.err" || { tail "$OUT/pervk_g1.err"; exit 1; }
