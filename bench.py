@@ -364,6 +364,43 @@ def cpu_baseline_verify(batch, value, what="shared vk"):
     }
 
 
+def cpu_pool_rate(fn, n_avail, threads, target_s):
+    """Rate of fn(i) (one oracle call on item i; ctypes releases the GIL, so the calls run in parallel)
+    over a sample of the first items sized to ~target_s of wall time on `threads` threads.  Returns
+    (items/s, items, seconds, results)."""
+    from concurrent.futures import ThreadPoolExecutor
+    t = time.perf_counter()
+    fn(0)
+    per = max(time.perf_counter() - t, 1e-6)
+    k = int(min(n_avail, max(threads * 2, target_s * threads / per)))
+    k = max(min(threads, n_avail), (k // threads) * threads) if k >= threads else k
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        t = time.perf_counter()
+        res = list(ex.map(fn, range(k)))
+        dt = time.perf_counter() - t
+    return k / dt, k, dt, res
+
+
+def cpu_report(value, unit, what, mt, one, thr, agree):
+    """cpu_baseline object from a `thr`-thread sample and a one-thread sample (cpu_pool_rate results):
+    the whole host is extrapolated as single thread x nproc x the share's per-thread efficiency, as in
+    cpu_baseline_verify."""
+    model, nproc, aff = cpu_info()
+    v_mt, k_mt, dt_mt = mt[:3]
+    v_1, k_1, dt_1 = one[:3]
+    eff = min(1.0, v_mt / (thr * v_1)) if thr > 1 else 1.0
+    host = v_1 * nproc * eff
+    return {
+        "value": round(v_mt, 2), "unit": unit, "cores": thr, "kind": "port",
+        "sample": f"{k_mt} items of the timed batch on {thr} threads in {dt_mt:.2f} s, plus {k_1} on 1 thread in "
+                  f"{dt_1:.2f} s; {what} (oracle/c, test infrastructure); outputs agree with construction: {agree}",
+        "single_thread": round(v_1, 2), "per_thread_efficiency": round(eff, 3),
+        "nproc": nproc, "affinity_cpus": aff, "cpu_model": model,
+        "all_cores_extrapolated": round(host, 1),
+        "gpu_over_cpu": round(value / host, 2), "gpu_over_cpu_share": round(value / v_mt, 1),
+    }
+
+
 # ---------------------------------------------------------------- modes
 def kernel_table(phase_ms, n, counts, in_bytes_per_cred, peak, prep_kernel="k_prep_sigg2_pair", mode=None):
     """Per-kernel roofline: algorithmic M (tests/fixtures/opcount.json) x 288 mads x n / kernel time.

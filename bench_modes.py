@@ -238,11 +238,11 @@ def bench_aggregate(args):
         sig_ms, vk_ms = phase[1], phase[2]
         msm_ms = sig_ms + vk_ms
         # the op-count fixture covers SigG2; SigG1 lines report times only
-        counts = opcounts("aggregate_sigg2_t67") if not sigm else {"straus_sigma2": 0, "fixed_verkey": 0}
+        counts = opcounts("aggregate_sigg1_t67" if sigm else "aggregate_sigg2_t67")
         ach = (counts["straus_sigma2"] + counts["fixed_verkey"]) * MADS_PER_M * n / (msm_ms * 1e-3)
         dom = "signature_msm+verkey_msm (concurrent)"
         from bench import kernel_pmc_report
-        rk = kernel_pmc_report("aggregate")
+        rk = kernel_pmc_report("aggregate-g1" if sigm else "aggregate")
         out = {
             "metric": "aggregated credentials/sec (Signature::aggregate + Verkey::aggregate, t=67 of n=100)",
             "value": round(value, 1), "unit": "credentials/s", "n_gpus": world, "steps": args.steps,
@@ -267,27 +267,26 @@ def bench_aggregate(args):
             "rocprof_kernels": rk,
             "setup": {"issuer_tables_ms": round(iss_ms, 1), "synthetic_data_s": round(gen_s, 2)},
         }
-        if sigm:
-            out["roofline"] = None  # no SigG1 op-count fixture (tests/fixtures/opcount.json)
-        if not args.no_cpu_baseline and world == 1 and not sigm:
-            out["cpu_baseline"] = cpu_aggregate(b)
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_aggregate(b, value)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
     ctx.close()
 
 
-def cpu_aggregate(b, k=6):
-    """oracle/c oc_signature_aggregate + oc_verkey_aggregate on one thread over k credentials."""
-    from bench import _oracle, cpu_info
+def cpu_aggregate(b, value):
+    """oracle/c oc_signature_aggregate + oc_verkey_aggregate per credential, on the box's CPU share and on
+    one thread, each sample >= 2 s (cpu_pool_rate)."""
+    from bench import _oracle, cpu_pool_rate, cpu_report, host_threads
     oc = _oracle()
     t, q, sb, ob = b["t"], b["q"], b["sb"], b["ob"]
-    o1 = ctypes.create_string_buffer(sb)
-    o2 = ctypes.create_string_buffer(sb)
-    oX = ctypes.create_string_buffer(ob)
-    oY = ctypes.create_string_buffer(ob * q)
-    t0 = time.perf_counter()
-    for i in range(k):
+
+    def one(i):
+        o1 = ctypes.create_string_buffer(sb)
+        o2 = ctypes.create_string_buffer(sb)
+        oX = ctypes.create_string_buffer(ob)
+        oY = ctypes.create_string_buffer(ob * q)
         ids = np.ascontiguousarray(b["ids"][i])
         oc.oc_signature_aggregate(b["mode"], ctypes.c_size_t(t), ctypes.c_size_t(t), ids.ctypes.data_as(ctypes.c_void_p),
                                   b["s1"][i * t * sb:(i + 1) * t * sb], b["s2"][i * t * sb:(i + 1) * t * sb], o1, o2)
@@ -296,13 +295,13 @@ def cpu_aggregate(b, k=6):
         Ys = b"".join(b["Y"][r * q * ob:(r + 1) * q * ob] for r in rows)
         oc.oc_verkey_aggregate(b["mode"], ctypes.c_size_t(t), ctypes.c_size_t(t), ctypes.c_size_t(q),
                                ids.ctypes.data_as(ctypes.c_void_p), Xs, Ys, oX, oY)
-    dt = time.perf_counter() - t0
-    model, nproc, _ = cpu_info()
-    return {"value": round(k / dt, 2), "unit": "credentials/s", "cores": 1, "kind": "port",
-            "sample": f"{k} credentials of the timed batch on 1 thread in {dt:.2f} s (oracle/c "
-                      f"oc_signature_aggregate + oc_verkey_aggregate, test infrastructure); last outputs equal the "
-                      f"construction: {o2.raw == b['want_s2'][(k - 1) * sb:k * sb] and oX.raw == b['want_X']}",
-            "nproc": nproc, "cpu_model": model}
+        return o2.raw == b["want_s2"][i * sb:(i + 1) * sb] and oX.raw == b["want_X"]
+
+    thr = host_threads()
+    mt = cpu_pool_rate(one, b["n"], thr, 2.5)
+    st = cpu_pool_rate(one, b["n"], 1, 2.5)
+    return cpu_report(value, "credentials/s", "oc_signature_aggregate + oc_verkey_aggregate per credential", mt, st,
+                      thr, all(mt[3]) and all(st[3]))
 
 
 def bench_pok(args):
@@ -344,8 +343,9 @@ def bench_pok(args):
     if rank == 0:
         from bench import kernel_table, cpu_info, kernel_pmc_report
         peak = peak_mad_per_s()
-        counts = opcounts("pok_sigg2_q32_r8")  # SigG2 op counts; a SigG1 line's fractions are not meaningful
-        kt = kernel_table(phase_ms, n, counts, 2 * 192 + 2 * 97 + (nresp + 1 + r) * 48, peak, "k_prep_pok", "pok")
+        counts = opcounts("pok_sigg1_q32_r8" if sigm else "pok_sigg2_q32_r8")
+        kt = kernel_table(phase_ms, n, counts, 2 * 192 + 2 * 97 + (nresp + 1 + r) * 48, peak,
+                          "k_prep_pok_g1pl" if sigm else "k_prep_pok_split", "pok-g1" if sigm else "pok")
         dom = max(kt, key=lambda k: kt[k]["ms"])
         out = {
             "metric": "verified PoK-of-signature proofs/sec (msg_count=32, 8 revealed)",
@@ -363,32 +363,29 @@ def bench_pok(args):
                          "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),
                          "traffic_unit": "HBM-side bytes per launch (PMC, 2 x FETCH_SIZE + WRITE_SIZE)"},
             "kernels": kt,
-            "rocprof_kernels": kernel_pmc_report("pok"),
+            "rocprof_kernels": kernel_pmc_report("pok-g1" if sigm else "pok"),
             "setup": {"synthetic_data_s": round(gen_s, 2), "verkey_table_bits": ctx.table_bits()[0]},
         }
-        if sigm:
-            out["roofline"] = None  # no SigG1 op-count fixture
-        if not args.no_cpu_baseline and world == 1 and not sigm:
-            oc = __import__("bench")._oracle()
-            k = 24
-            ver = []
-            tt = time.perf_counter()
-            gtb = ctypes.create_string_buffer(576)
-            for p in range(k):
-                v = oc.oc_pok_verify(0, ctypes.c_size_t(q), ctypes.c_size_t(r), b["s1"][p * 192:(p + 1) * 192],
-                                     b["s2"][p * 192:(p + 1) * 192], b["J"][p * 97:(p + 1) * 97],
-                                     b["T"][p * 97:(p + 1) * 97], b["resp"][p * nresp * 48:(p + 1) * nresp * 48],
-                                     ctypes.c_size_t(nresp), b["chal"][p * 48:(p + 1) * 48],
-                                     (ctypes.c_uint64 * r)(*b["revealed"]), b["rev"][p * r * 48:(p + 1) * r * 48],
-                                     b["X"], b["Y"], b["g_tilde"], gtb)
-                ver.append(v)
-            dt = time.perf_counter() - tt
-            model, nproc, _ = cpu_info()
-            out["cpu_baseline"] = {"value": round(k / dt, 2), "unit": "proofs/s", "cores": 1, "kind": "port",
-                                   "sample": f"{k} proofs of the timed batch on 1 thread in {dt:.2f} s (oracle/c "
-                                             f"oc_pok_verify); verdicts agree with construction: "
-                                             f"{list(ver) == list(b['expect'][:k])}",
-                                   "nproc": nproc, "cpu_model": model}
+        if not args.no_cpu_baseline and world == 1:
+            from bench import _oracle, cpu_pool_rate, cpu_report, host_threads
+            oc = _oracle()
+            ridx_c = (ctypes.c_uint64 * r)(*b["revealed"])
+            sb, ob = (97, 192) if sigm else (192, 97)
+
+            def one(p):
+                gtb = ctypes.create_string_buffer(576)
+                v = oc.oc_pok_verify(sigm, ctypes.c_size_t(q), ctypes.c_size_t(r), b["s1"][p * sb:(p + 1) * sb],
+                                     b["s2"][p * sb:(p + 1) * sb], b["J"][p * ob:(p + 1) * ob],
+                                     b["T"][p * ob:(p + 1) * ob], b["resp"][p * nresp * 48:(p + 1) * nresp * 48],
+                                     ctypes.c_size_t(nresp), b["chal"][p * 48:(p + 1) * 48], ridx_c,
+                                     b["rev"][p * r * 48:(p + 1) * r * 48], b["X"], b["Y"], b["g_tilde"], gtb)
+                return int(v) == int(b["expect"][p])
+
+            thr = host_threads()
+            mt = cpu_pool_rate(one, n, thr, 2.5)
+            st = cpu_pool_rate(one, n, 1, 2.5)
+            out["cpu_baseline"] = cpu_report(value, "proofs/s", "oc_pok_verify per proof", mt, st, thr,
+                                             all(mt[3]) and all(st[3]))
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
