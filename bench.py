@@ -313,20 +313,20 @@ def cpu_verify_rate(batch, threads, target_s):
     mode, q = batch["mode"], batch["q"]
     sb = 192 if mode == 0 else 97
     ob = 97 if mode == 0 else 192
-    per = 1 if batch.get("per_vk") else 0  # one verkey per credential (X: n x ob, Y: n x q x ob)
-    vk = lambda k: (batch["X"][:k * ob], batch["Y"][:k * q * ob]) if per else (batch["X"], batch["Y"])  # noqa: E731
+    pervk = 1 if batch.get("per_vk") else 0  # one verkey per credential (X: n x ob, Y: n x q x ob)
+    vk = lambda k: (batch["X"][:k * ob], batch["Y"][:k * q * ob]) if pervk else (batch["X"], batch["Y"])  # noqa: E731
     k0 = max(2, threads * 2)
     ver = ctypes.create_string_buffer(k0)
     t = time.perf_counter()
     oc.oc_verify_batch(mode, ctypes.c_size_t(k0), ctypes.c_size_t(q), batch["s1"][:k0 * sb], batch["s2"][:k0 * sb],
-                       batch["msgs"][:k0 * q * 48], *vk(k0), per, batch["g_tilde"], ver, None, threads)
+                       batch["msgs"][:k0 * q * 48], *vk(k0), pervk, batch["g_tilde"], ver, None, threads)
     per = (time.perf_counter() - t) / k0
     k = int(min(batch["n"], max(threads * 4, target_s / max(per, 1e-6))))
     k = max(threads, (k // threads) * threads)
     ver = ctypes.create_string_buffer(k)
     t = time.perf_counter()
     oc.oc_verify_batch(mode, ctypes.c_size_t(k), ctypes.c_size_t(q), batch["s1"][:k * sb], batch["s2"][:k * sb],
-                       batch["msgs"][:k * q * 48], *vk(k), per, batch["g_tilde"], ver, None, threads)
+                       batch["msgs"][:k * q * 48], *vk(k), pervk, batch["g_tilde"], ver, None, threads)
     dt = time.perf_counter() - t
     agree = bool(np.array_equal(np.frombuffer(ver.raw, np.uint8), batch["expect"][:k]))
     return k / dt, k, dt, agree

@@ -662,6 +662,8 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_g1pl(size_t n, int q, int r
         if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
         if (h) fp_neg(a.y, a.y);
         const int slot = h ? S_P2 : S_P1;
+        fp_to_lazy_form(a.x);  // the Miller loop's affine P in the lazy R' form (miller_lz.hip kAffRp)
+        fp_to_lazy_form(a.y);
         st_fp(S, slot, i, a.x);
         st_fp(S, slot + 1, i, a.y);
     }

@@ -20,6 +20,7 @@ int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_o
 int cck_build_table(int group, int nbases, int wbits, const uint32_t* d_bases, const uint32_t* d_inf, uint32_t* d_pw,
                     uint32_t* d_table, int lazy_g2, hipStream_t st);
 int cck_gtilde_lines(const uint32_t* d_gtilde_aff, uint32_t* d_lines, hipStream_t st);
+int cck_lazy_form(size_t n, const uint32_t* d_in, uint32_t* d_out, hipStream_t st);
 int cck_subgroup(int group, size_t n, const uint8_t* d_bytes, uint8_t* d_status, hipStream_t st);
 int cck_hash_to_curve(int group, size_t n, const uint8_t* d_data, const uint64_t* d_offsets, uint8_t* d_out,
                       uint32_t* d_fail, hipStream_t st);
@@ -139,6 +140,7 @@ struct cc_ctx {
     DevBuf gtilde_aff;   // OtherGroup affine (Montgomery, AoS)
     uint32_t gtilde_inf = 0;
     DevBuf gtilde_lines; // SigG1: Miller lines of g~
+    DevBuf gtilde_lz;    // SigG2: g~ affine in the lazy field's R' form (the Miller loop's constant P)
     // verkey
     bool have_vk = false;
     size_t q = 0;
@@ -212,7 +214,8 @@ struct StreamOrder {
     }
 };
 
-// mode 0 (SigG2): d_const = g~ affine G1 (24 words); mode 1 (SigG1): g~ Miller lines (68 x 72 words).
+// mode 0 (SigG2): d_const = g~ affine G1 in the lazy R' form (24 words); mode 1 (SigG1): g~ Miller lines
+// (68 x 72 words).
 // Pairing kernels run one credential per lane pair (tower_pl.h).  Miller values go to SoA elements
 // [0, n) of stride n.
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
@@ -316,7 +319,7 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     }
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
+    DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->gtilde_lz, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->lag,
                       &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->fin_f, &c->fin_scratch, &c->pok_idx, &c->rlc_gath,
@@ -466,6 +469,10 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
         if (c->gtilde_lines.ensure(68 * 72 * 4)) return CC_ERR_HIP;
         KCK(cck_gtilde_lines(c->gtilde_aff.as<uint32_t>(), c->gtilde_lines.as<uint32_t>(), c->stream));
         HIPCK(hipStreamSynchronize(c->stream));
+    } else {
+        if (c->gtilde_lz.ensure(aw * 4)) return CC_ERR_HIP;
+        KCK(cck_lazy_form(2, c->gtilde_aff.as<uint32_t>(), c->gtilde_lz.as<uint32_t>(), c->stream));
+        HIPCK(hipStreamSynchronize(c->stream));
     }
     c->have_params = true;
     if (c->have_vk) {
@@ -589,7 +596,7 @@ static cc_status launch_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s
                      c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
                      c->flags.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
-    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
+    const uint32_t* cst = c->mode == 0 ? c->gtilde_lz.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(), d_verdicts, d_gt, st));
@@ -1395,7 +1402,7 @@ static cc_status launch_pok(cc_ctx* c, size_t n, size_t q, size_t r, const uint8
                      c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(),
                      c->scratch.as<uint32_t>(), st));  // J*chal window table: the fexp scratch, free until fexp
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
-    const uint32_t* cst = c->mode == 0 ? c->gtilde_aff.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
+    const uint32_t* cst = c->mode == 0 ? c->gtilde_lz.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(), d_verdicts, d_gt, st));

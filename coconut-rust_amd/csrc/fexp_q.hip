@@ -38,11 +38,13 @@ namespace {
 // fexp_pl.hip cyc4_sqr (Karabina's compression restated for this tower) on b = b0 + b1 s, c = c0 + c1 s:
 //     b0' = 3 (2 xi c0 c1) + 2 b0    b1' = 3 (c0^2 + xi c1^2) - 2 b1
 //     c0' = 3 (b0^2 + xi b1^2) - 2 c0    c1' = 3 (2 b0 b1) + 2 c1
-// Pair 0 holds V = c0, W = b0; pair 1 V = b1, W = c1.  Each lane squares V, W and W + V' (V' the
-// other pair's V: b0 + b1 on pair 0, c0 + c1 on pair 1) and then both pairs run the same formulas:
-//     X = M' - V^2 - W'^2  (2 c0 c1 | 2 b0 b1, times xi on pair 0),  T = b0^2 + xi b1^2 | c0^2 + xi c1^2,
+// Pair 0 holds V = c0, W = b0; pair 1 V = b1, W = c1.  Each lane squares S1 = V, S2 = W and S3 = W + V'
+// (V' the other pair's V: b0 + b1 on pair 0, c1 + c0 on pair 1); with primes for the other pair's values
+//     X = S3' - S2' - S1 = (S3 - S2)' - S1   (2 c0 c1 | 2 b0 b1; times xi on pair 0)
+//     T = S1' + S2 + i B,  B = S1' (pair 0) | S2 (pair 1)   (b0^2 + xi b1^2 | c0^2 + xi c1^2)
 //     V <- 3 T - 2 V,  W <- 3 X + 2 W
-// (primes: the other pair's values) — 3 Fp2 squarings a lane and three selects.
+// — 3 Fp2 squarings a lane, three exchanges between the pairs, one select; the pair-0-only xi and the
+// i B term run on their lanes under exec masks.
 using F2R = F2<AN, 9>;
 struct QZ {
     F2R V, W;
@@ -55,13 +57,13 @@ DEV F2R qz_b(const QZ& x) { return qsel(qhi(), x.V, x.W); }
 DEV F2R qz_c(const QZ& x) { return qsel(qhi(), x.W, x.V); }
 DEV void qz_sqr(QZ& x) {
     const bool j = qhi();
-    const auto sV = sqrr_in(x.V);
-    const auto sW = sqrr_in(x.W);
-    const auto M = sqrr_in(add(x.W, qx(x.V)));  // (b0 + b1)^2 | (c0 + c1)^2
-    const auto psV = qx(sV), psW = qx(sW), pM = qx(M);
-    const auto X = norm(sub(sub(pM, sV), psW));  // 2 c0 c1 | 2 b0 b1
-    const auto Xs = norm(qsel(j, X, xi(X)));
-    const auto T = norm(add(qsel(j, psV, sW), xi(qsel(j, sW, psV))));
+    const auto S1 = sqrr_in(x.V);
+    const auto S2 = sqrr_in(x.W);
+    const auto S3 = sqrr_in(add(x.W, qx(x.V)));  // (b0 + b1)^2 | (c1 + c0)^2
+    const auto pE = qx(sub(S3, S2));
+    const auto pS1 = qx(S1);
+    const auto Xs = norm(xi_pair0(sub(pE, S1)));          // xi 2 c0 c1 | 2 b0 b1
+    const auto T = norm(add_i(add(pS1, S2), qsel(j, S2, pS1)));
     // 3T - 2V = T + 2 (T - V), 3X + 2W = X + 2 (X + W)
     x.V = reduce(add(T, dbl(sub(T, x.V))));
     x.W = reduce(add(Xs, dbl(add(Xs, x.W))));

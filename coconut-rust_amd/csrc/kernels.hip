@@ -352,6 +352,8 @@ __global__ __launch_bounds__(256, 2) void k_prep_sigg1_pair(size_t n, int q, con
         if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
         if (h) fp_neg(a.y, a.y);  // -sigma_2
         const int slot = h ? S_P2 : S_P1;
+        fp_to_lazy_form(a.x);  // the Miller loop's affine P in the lazy R' form (miller_lz.hip kAffRp)
+        fp_to_lazy_form(a.y);
         st_fp(S, slot, i, a.x);
         st_fp(S, slot + 1, i, a.y);
     }
@@ -462,6 +464,23 @@ int cck_subgroup(int group, size_t n, const uint8_t* d_bytes, uint8_t* d_status,
         hipLaunchKernelGGL(k_subgroup<Fp>, dim3(nblocks(n, 64)), dim3(64), 0, st, n, d_bytes, d_status);
     else
         hipLaunchKernelGGL(k_subgroup<Fp2>, dim3(nblocks(n, 64)), dim3(64), 0, st, n, d_bytes, d_status);
+    CC_CHECK(hipGetLastError());
+    return 0;
+}
+
+// n values of the storage form (x R, canonical 12 x 32) -> the lazy field's R' form (x R' mod p, canonical)
+__global__ __launch_bounds__(64) void k_lazy_form(size_t n, const uint32_t* __restrict__ in, uint32_t* __restrict__ out) {
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Fp v;
+    for (int k = 0; k < NL; k++) v.v[k] = in[i * NL + k];
+    fp_to_lazy_form(v);
+    for (int k = 0; k < NL; k++) out[i * NL + k] = v.v[k];
+}
+
+int cck_lazy_form(size_t n, const uint32_t* d_in, uint32_t* d_out, hipStream_t st) {
+    if (!n) return 0;
+    hipLaunchKernelGGL(k_lazy_form, dim3(nblocks(n, 64)), dim3(64), 0, st, n, d_in, d_out);
     CC_CHECK(hipGetLastError());
     return 0;
 }

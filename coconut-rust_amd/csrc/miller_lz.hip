@@ -5,7 +5,8 @@
 //
 //   SigG2: pair 0 = (sigma_1, pr) with pr in Jacobian-evaluation form (XZ, Y, Z^3);
 //          pair 1 = (-sigma_2, g~): g~ affine constant.
-//   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2).
+//   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2); sigma_1,
+//          -sigma_2 arrive in the lazy R' form (kAffRp: no product for l0).
 //   RLC mode keeps pair 0 of every credential (its second pairs are folded, fold.hip) and runs TWO
 //   credentials through the 2-pair loop (kTwin): the RLC only needs the product of the credentials'
 //   Miller values, and the shared squaring halves the Fp12 work per credential (5,696 Fp
@@ -46,11 +47,16 @@ using LineS = Line<F2L, F2L, F2L>;
 template <class L>
 DEV LineS fit_line(const L& l) { return {fit<AS, BL>(l.l0), fit<AS, BL>(l.l2), fit<AS, BL>(l.l3)}; }
 
-// where a pair's G1 evaluation point lives: word (slot * NL + limb) * n + i * is
+// where a pair's G1 evaluation point lives: word (slot * NL + limb) * n + i * is.  form:
+//   kJac    (XZ, Y, Z^3), R form: every line coefficient scaled by 2^14 (header)
+//   kAffR   affine (x, y), R form: l0 times R mod p (the affine Z), scale 2^14
+//   kAffRp  affine (x, y) in the lazy field's R' form (x R' mod p, canonical): l2 x, l3 y come out
+//           unscaled and l0 needs no product (SigG2's constant g~: one Fp product less per step)
+enum { kJac = 0, kAffR = 1, kAffRp = 2 };
 struct PSrc {
     const uint32_t* p;
     size_t n, is;
-    bool jac;  // (XZ, Y, Z^3) form; affine (x, y) [z = 1] otherwise
+    int form;
 };
 
 DEV Fq<AN, BC> ld_Pc(const PSrc& s, int slot, size_t i) {
@@ -67,7 +73,10 @@ DEV Fq<AN, BC> ld_Pc(const PSrc& s, int slot, size_t i) {
 template <int B>
 DEV F12S eval_mul(const F12<AS, B>& f, const LineS& ln, const PSrc& ps, size_t i, bool skip) {
     constexpr int32_t ONE_R[LN] = {LZ_C_OUT_LIMBS};
-    const auto a0 = mul_fpr(ln.l0, ps.jac ? ld_Pc(ps, 2, i) : fq_const(ONE_R));
+    using A0 = decltype(mul_fpr(ln.l0, fq_const(ONE_R)));
+    A0 a0;
+    if (ps.form == kAffRp) a0 = fit<AN, A0::BV>(reduce(ln.l0));  // pair-uniform branch
+    else a0 = mul_fpr(ln.l0, ps.form == kJac ? ld_Pc(ps, 2, i) : fq_const(ONE_R));
     const auto a2 = mul_fpr(ln.l2, ld_Pc(ps, 0, i));
     const auto a3 = mul_fpr(ln.l3, ld_Pc(ps, 1, i));
     using L = decltype(a0);
@@ -166,7 +175,8 @@ static __device__ __noinline__ void t_check(const Tw* T, const uint32_t* prep, s
 }  // namespace
 
 // prep: SoA slots of soa.h; flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 pr = O, bit4 pair-1 P = O
-// cst: SigG2 -> g~ affine (24 words); SigG1 -> g~ lines (68 x 72 words); unused by kTwin.
+// cst: SigG2 -> g~ affine in the lazy R' form (24 words, cck_lazy_form); SigG1 -> g~ lines (68 x 72
+// words); unused by kTwin.
 // The Miller value of credential i goes to fout as SoA element foff + i of stride fstride.  kTwin (RLC
 // credentials): the one pair of credentials 2j and 2j + 1, laid out as pairs 0 and 1 of element j
 // (rlc.hip twin_slot; the second skipped when n is odd); their product goes to element foff + j.
@@ -189,14 +199,14 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
     const bool skip1 = kTwin ? (2 * i + 1 >= n || (flags[2 * i + 1] & 5u) != 0) : (fl & 18u) != 0;
     PSrc ps0, ps1;
     if (kTwin) {
-        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, kSigG2};
-        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kSigG2};
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, kSigG2 ? kJac : kAffR};
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kSigG2 ? kJac : kAffR};
     } else if (kSigG2) {
-        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, true};
-        ps1 = PSrc{cst, 1, 0, false};
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, kJac};
+        ps1 = PSrc{cst, 1, 0, kAffRp};
     } else {
-        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, false};
-        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, false};
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, kAffRp};  // the SigG1 preps write sigma in R' form
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kAffRp};
     }
     const Soa S{const_cast<uint32_t*>(prep), n};
     // both T's parked in LDS between their uses

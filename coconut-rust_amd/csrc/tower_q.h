@@ -48,6 +48,55 @@ DEV bool quad_all(bool own) {
     return o != 0;
 }
 
+// ---------------------------------------------------------------- masked half operations
+// lane 4i + 2j + h: pair j, half h.  Masks of the lanes an operation runs on (exec narrowed inside one asm
+// statement and restored, as lazy.h neg_re14: the other lanes keep their values).
+constexpr uint64_t kP0Re = 0x1111111111111111ull, kP0Im = 0x2222222222222222ull;  // pair 0, re / im half
+constexpr uint64_t kRe = 0x5555555555555555ull, kIm = 0xAAAAAAAAAAAAAAAAull;      // every re / im half
+// 7 limbs: x <- x - s on the lanes of mre, x + s on the lanes of mim
+DEV void addsub_ops7(int32_t* x, const int32_t* s, uint64_t mre, uint64_t mim) {
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "s_and_b64 exec, %0, %15\n\t"
+        "v_sub_u32 %1, %1, %8\n\tv_sub_u32 %2, %2, %9\n\tv_sub_u32 %3, %3, %10\n\tv_sub_u32 %4, %4, %11\n\t"
+        "v_sub_u32 %5, %5, %12\n\tv_sub_u32 %6, %6, %13\n\tv_sub_u32 %7, %7, %14\n\t"
+        "s_and_b64 exec, %0, %16\n\t"
+        "v_add_u32 %1, %1, %8\n\tv_add_u32 %2, %2, %9\n\tv_add_u32 %3, %3, %10\n\tv_add_u32 %4, %4, %11\n\t"
+        "v_add_u32 %5, %5, %12\n\tv_add_u32 %6, %6, %13\n\tv_add_u32 %7, %7, %14\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(save), "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6])
+        : "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]), "v"(s[6]), "s"(mre), "s"(mim));
+}
+// x + i y (i y = -y_im + y_re i: the partner's half of y, negated on the re half)
+template <int A1, int B1, int A2, int B2>
+DEV F2<A1 + A2, B1 + B2> add_i(const F2<A1, B1>& x, const F2<A2, B2>& y) {
+    F2<A1 + A2, B1 + B2> r;
+    int32_t s[LN];
+#pragma unroll
+    for (int k = 0; k < LN; k++) {
+        r.c.v[k] = x.c.v[k];
+        s[k] = swp(y.c.v[k]);
+    }
+    addsub_ops7(r.c.v, s, kRe, kIm);
+    addsub_ops7(r.c.v + 7, s + 7, kRe, kIm);
+    return r;
+}
+// xi x = x + i x on pair 0, x on pair 1 (this lane's half)
+template <int A, int B>
+DEV F2<2 * A, 2 * B> xi_pair0(const F2<A, B>& x) {
+    F2<2 * A, 2 * B> r;
+    int32_t s[LN];
+#pragma unroll
+    for (int k = 0; k < LN; k++) {
+        r.c.v[k] = x.c.v[k];
+        s[k] = swp(x.c.v[k]);
+    }
+    addsub_ops7(r.c.v, s, kP0Re, kP0Im);
+    addsub_ops7(r.c.v + 7, s + 7, kP0Re, kP0Im);
+    return r;
+}
+
 // ---------------------------------------------------------------- inversion, one per quad
 // field.h fp_inv_int with the quad's four lanes holding the same input: the divstep iteration's four
 // vectors f, g, d, e sit one per lane (lane & 3 = 0 f, 1 g, 2 d, 3 e; partners f/g and d/e over DPP

@@ -51,6 +51,38 @@ def test_compressed_squaring_and_decompression():
         assert decompress(*st) == cur
 
 
+def quad_comp_sqr(V, W):
+    """fexp_q.hip qz_sqr as the quad runs it: pair j holds (V_j, W_j) = (c0, b0) | (b1, c1); each pair
+    squares S1 = V, S2 = W, S3 = W + V' (primes: the other pair), then X = (S3 - S2)' - S1 (times xi on
+    pair 0), T = S1' + S2 + i B with B = S1' | S2, V <- 3T - 2V, W <- 3X + 2W."""
+    s, xi, add, sub = B.f2_sqr, B.f2_mul_xi, B.f2_add, B.f2_sub
+    mul_i = lambda y: B.f2_mul(y, (0, 1))  # noqa: E731
+    S1 = [s(V[j]) for j in (0, 1)]
+    S2 = [s(W[j]) for j in (0, 1)]
+    S3 = [s(add(W[j], V[1 - j])) for j in (0, 1)]
+    E = [sub(S3[j], S2[j]) for j in (0, 1)]
+    nV, nW = [None, None], [None, None]
+    for j in (0, 1):
+        X = sub(E[1 - j], S1[j])
+        Xs = add(X, mul_i(X)) if j == 0 else X
+        Bv = S1[1 - j] if j == 0 else S2[j]
+        T = add(add(S1[1 - j], S2[j]), mul_i(Bv))
+        nV[j] = sub(_k(T, 3), _k(V[j], 2))
+        nW[j] = add(_k(Xs, 3), _k(W[j], 2))
+    assert add(X, mul_i(X)) == xi(X)  # xi = 1 + i
+    return nV, nW
+
+
+def test_quad_compressed_squaring_matches():
+    cur = _cyclotomic(7)
+    b0, b1, c0, c1 = cur[1], cur[4], cur[2], cur[5]
+    V, W = [c0, b1], [b0, c1]
+    for _ in range(8):
+        cur = B.f12_sqr(cur)
+        V, W = quad_comp_sqr(V, W)
+        assert (W[0], V[1], V[0], W[1]) == (cur[1], cur[4], cur[2], cur[5])
+
+
 def test_pow_x_schedule():
     """|x| = 2^63 + 2^62 + 2^60 + 2^57 + 2^48 + 2^16: the kernel's snapshot/Granger-Scott split."""
     x_abs = 0xD201000000010000

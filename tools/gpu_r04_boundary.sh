@@ -11,3 +11,10 @@ cat "$OUT/smoke.log"
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/verify.json" 2> "$OUT/verify.err" || { tail "$OUT/verify.err"; exit 1; }
 timeout -k 10 300 python -u bench.py --mode verify-pervk --steps 5 --warmup 1 > "$OUT/pervk.json" 2> "$OUT/pervk.err" || { tail "$OUT/pervk.err"; exit 1; }
 timeout -k 10 300 python -u bench.py --mode verify-pervk-g1 --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/pervk_g1.json" 2> "$OUT/pervk_g1.err" || { tail "$OUT/pervk_g1.err"; exit 1; }
+for k in 1 2; do
+  for v in prev cur; do
+    lib=$(pwd)/coconut-rust_amd/libcoconut_hip.so
+    [ $v = prev ] && lib=$(pwd)/coconut-rust_amd/libcoconut_hip_prev.so
+    COCONUT_HIP_LIB=$lib timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-pcie > "$OUT/ab_verify_$v.$k.json" 2> "$OUT/ab_verify_$v.$k.err" || exit 1
+  done
+done
