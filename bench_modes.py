@@ -122,45 +122,45 @@ def make_pok_batch(ctx, mode, n, q=32, revealed=REVEALED, seed=5, bad_every=16):
 
 
 def make_pervk_batch(ctx, mode, n, q, seed, bad_every=16):
-    """n credentials, each under ITS OWN verkey (x_i, y_ij random; X~_i = x_i g~, Y~_ij = y_ij g~ built by
-    the product's cc_fixed_base_mul), sigma_1 = k G, sigma_2 = k (x_i + sum y_ij m_ij) G; every
-    bad_every-th corrupted, cycling sigma_2 + G / m_0 + 1 / sigma_2 under another credential's key."""
+    """n credentials, each under ITS OWN verkey (x_i, y_ij uniform in Fr; X~_i = x_i g~, Y~_ij = y_ij g~
+    built by the product's cc_fixed_base_mul), uniform messages in Fr, sigma_1 = k G,
+    sigma_2 = k (x_i + sum y_ij m_ij) G; every bad_every-th corrupted, cycling sigma_2 + G / m_0 + 1 /
+    sigma_2 under another credential's key."""
     import coconut
     rng = np.random.default_rng(seed)
     og, sg = (1, 2) if mode == 0 else (2, 1)
     gen = {1: coconut.G1_GENERATOR, 2: coconut.G2_GENERATOR}
-    gk = int(rng.integers(1, 2**62))
+    gk = _fr(rng) or 1
     g_tilde = coconut.fixed_base_mul(ctx, og, gen[og], _be(gk))
-    sk = rng.integers(1, 2**62, size=(n, q + 1), dtype=np.int64)
-    msgs = rng.integers(0, 2**62, size=(n, q), dtype=np.int64)
-    ks = rng.integers(1, 2**62, size=n, dtype=np.int64)
-    vk_sc, e1, e2 = [], [], []
+    vk_sc, e1, e2, mb = [], [], [], []
     expect = np.ones(n, np.uint8)
+    sks = [[_fr(rng) for _ in range(q + 1)] for _ in range(n)]
     for i in range(n):
-        row = [int(v) for v in sk[i]]
-        m = [int(v) for v in msgs[i]]
+        row = sks[i]
+        m = [_fr(rng) for _ in range(q)]  # the messages the verifier is given
+        k = _fr(rng) or 1
         vk_sc.extend(v * gk % R for v in row)
-        x = row[0]
-        if bad_every and i % bad_every == bad_every - 1:
+        x, signed = row[0], m
+        kind = (i // bad_every) % 3 if bad_every and i % bad_every == bad_every - 1 else -1
+        if kind >= 0:
             expect[i] = 0
-            kind = (i // bad_every) % 3
-            if kind == 1:
-                m = [m[0] + 1] + m[1:]
-            elif kind == 2:
-                x = int(sk[(i + 1) % n][0])
-        e = int(ks[i]) * (x + sum(y * mm for y, mm in zip(row[1:], m))) % R
-        if bad_every and i % bad_every == bad_every - 1 and (i // bad_every) % 3 == 0:
-            e = (e + 1) % R
-        e1.append(_be(int(ks[i])))
+        if kind == 1:
+            signed = [(m[0] + 1) % R] + m[1:]  # signed over m_0 + 1
+        elif kind == 2:
+            x = sks[(i + 1) % n][0]  # signed under another credential's x
+        e = k * (x + sum(y * mm for y, mm in zip(row[1:], signed))) % R
+        if kind == 0:
+            e = (e + 1) % R  # sigma_2 + G
+        e1.append(_be(k))
         e2.append(_be(e))
+        mb.append(b"".join(_be(v) for v in m))
     ob = 97 if og == 1 else 192
     vk = coconut.fixed_base_mul(ctx, og, gen[og], b"".join(_be(v) for v in vk_sc))
     X = b"".join(vk[(i * (q + 1)) * ob:(i * (q + 1) + 1) * ob] for i in range(n))
     Y = b"".join(vk[(i * (q + 1) + 1) * ob:(i + 1) * (q + 1) * ob] for i in range(n))
     s1 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e1))
     s2 = coconut.fixed_base_mul(ctx, sg, gen[sg], b"".join(e2))
-    mb = b"".join(_be(int(v)) for v in msgs.reshape(-1))
-    return dict(X=X, Y=Y, g_tilde=g_tilde, s1=s1, s2=s2, msgs=mb, expect=expect)
+    return dict(X=X, Y=Y, g_tilde=g_tilde, s1=s1, s2=s2, msgs=b"".join(mb), expect=expect)
 
 
 def _timed(args, step, dev, dist, ctx):

@@ -43,18 +43,16 @@ size_t cck_prep_var_words(int mode, size_t n, size_t q);
 int cck_prep_var(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_vkX,
                  const uint8_t* d_vkY, const uint8_t* d_msgs, uint32_t* d_scratch, uint32_t* d_prep,
                  uint32_t* d_flags, hipStream_t st);
-int cck_miller_lz_g2(int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+int cck_miller_lz_g2(int twin, size_t n, size_t pstride, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
-int cck_miller_lz_g1(int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+int cck_miller_lz_g1(int twin, size_t n, size_t pstride, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
 size_t cck_fold_words(int mode, size_t n);
 int cck_fold_pseudo();
 int cck_fold_window(int mode, size_t n, uint32_t* d_work, const uint8_t* d_finf, uint32_t* d_prep2,
                     uint32_t* d_flags2, hipStream_t st);
-int cck_miller_wide(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f, size_t fstride,
-                    size_t foff, hipStream_t st);
 int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok,
              int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
              uint32_t* d_flags2, hipStream_t st);
@@ -72,13 +70,15 @@ int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uin
                      uint8_t* d_outX, uint8_t* d_outY, uint32_t* d_err, hipStream_t st);
 int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
                   uint8_t* d_out, hipStream_t st);
-int cck_prep_rlc(int mode, int part, size_t n, int q, uint64_t base_index, const uint32_t* d_key,
+int cck_prep_rlc(int mode, int part, size_t n, size_t ps, int q, uint64_t base_index, const uint32_t* d_key,
                  const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits,
                  const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, uint32_t* d_pts,
                  int8_t* d_dig, hipStream_t st);
 int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any, uint32_t* d_partial,
                    hipStream_t st);
 int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t* d_flag, hipStream_t st);
+int cck_rlc_append(size_t n, size_t ps, int nps, const uint32_t* d_prep2, const uint32_t* d_flags2, uint32_t* d_prep,
+                   uint32_t* d_flags, hipStream_t st);
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
                  const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
@@ -220,22 +220,17 @@ struct StreamOrder {
 // [0, n) of stride n.
 static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, const uint32_t* d_const,
                       uint32_t* d_f, hipStream_t st) {
-    return mode == 0 ? cck_miller_lz_g2(0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st)
-                     : cck_miller_lz_g1(0, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st);
+    return mode == 0 ? cck_miller_lz_g2(0, n, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st)
+                     : cck_miller_lz_g1(0, n, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st);
 }
-// the RLC credentials: pair 0 only (their second pairs are folded, fold.hip), two credentials per
-// lane pair through the shared-squaring loop: (n + 1) / 2 Miller values, each the product of two
-// credentials' (the RLC multiplies them all), to SoA elements [0, (n + 1) / 2) of stride fstride
-static int cck_miller_twin(int mode, size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
+// the RLC credentials (pair 0 only: their second pairs are folded, fold.hip) and the fold's window
+// pairs appended after them (k_rlc_append), two per lane pair through the shared-squaring loop:
+// (n + 1) / 2 Miller values, each the product of two pairs' (the RLC multiplies them all), to SoA
+// elements [0, (n + 1) / 2) of stride fstride; the prep SoA has stride ps
+static int cck_miller_twin(int mode, size_t n, size_t ps, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
                            size_t fstride, uint32_t* d_qcheck, hipStream_t st) {
-    return mode == 0 ? cck_miller_lz_g2(1, n, d_prep, d_flags, nullptr, d_f, fstride, 0, d_qcheck, st)
-                     : cck_miller_lz_g1(1, n, d_prep, d_flags, nullptr, d_f, fstride, 0, nullptr, st);
-}
-// the RLC fold's pseudo-credentials: one (Q, P) pair each, Q affine G2 and P in evaluation form
-// (either group mode: the fold writes exactly that), one wave each in the wide form (fexp_pl.hip)
-static int cck_miller_pairs(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
-                            size_t fstride, size_t foff, hipStream_t st) {
-    return cck_miller_wide(n, d_prep, d_flags, d_f, fstride, foff, st);
+    return mode == 0 ? cck_miller_lz_g2(1, n, ps, d_prep, d_flags, nullptr, d_f, fstride, 0, d_qcheck, st)
+                     : cck_miller_lz_g1(1, n, ps, d_prep, d_flags, nullptr, d_f, fstride, 0, nullptr, st);
 }
 
 static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }
@@ -682,11 +677,12 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
         HIPCK(hipMemcpyAsync(d_partial, kOne, sizeof(kOne), hipMemcpyHostToDevice, st));
         return CC_OK;
     }
-    cc_status s = ensure_work(c, n);
-    if (s) return s;
     const size_t NPS = (size_t)cck_fold_pseudo();  // fold pseudo-credentials (one per window, one pair each)
-    const size_t M = (n + 1) / 2;  // the credentials' Miller values (two credentials each)
-    const size_t N = M + NPS;      // Miller values: the credentials', then the pseudo-credentials'
+    const size_t NT = n + NPS;       // pairs of the twin Miller launch: the credentials', then the windows'
+    const size_t N = (NT + 1) / 2;   // Miller values (two pairs each)
+    const size_t PS = NT;            // prep SoA stride (>= N elements)
+    cc_status s = ensure_work(c, NT);
+    if (s) return s;
     if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4) || c->fbuf.ensure(N * 144 * 4) ||
         c->scratch.ensure(((N + 1) / 2) * 144 * 4 + n * 12 * 4 * 72) || c->rlc_pts.ensure(n * 48 * 4) ||
         c->rlc_dig.ensure(16 * n) || c->rlc_work.ensure(cck_fold_words(c->mode, n) * 4) ||
@@ -698,7 +694,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     auto prep_part = [&](int part) {
-        return cck_prep_rlc(c->mode, part, n, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
+        return cck_prep_rlc(c->mode, part, n, PS, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
                             c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
                             c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), c->rlc_pts.as<uint32_t>(),
                             c->rlc_dig.as<int8_t>(), st);
@@ -712,11 +708,9 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     }
     // The second pairs become 16 window pairs (fold.hip).  The fold's short kernels run alone
     // (behind a full launch each would wait milliseconds for a free slot); its window sums (16 waves)
-    // and the window pairs' Miller launch (16 waves in the wide form) then run on the high-priority
-    // side stream beside the delta MSM (which fills half the wave slots), and pair 0 of every
-    // credential (two per lane pair: 2,048 waves, exactly the chip's wave slots) starts once both are
-    // done — a wave still holding a slot would push one of its waves into a second round.  Both
-    // Miller launches write disjoint ranges of fbuf (stride N).
+    // then run on the high-priority side stream beside the delta MSM and are appended to the
+    // credentials' pairs (k_rlc_append), so the one two-pairs-per-loop Miller launch (2,048 waves at
+    // 131,072 credentials: the chip's wave slots) covers them; it starts once both are done.
     KCK(cck_fold(c->mode, n, c->rlc_dig.as<int8_t>(), c->rlc_pts.as<uint32_t>(), c->rlc_work.as<uint32_t>(),
                  c->rlc_fixed_ok ? 1 : 0, (int)q, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(),
                  c->rlc_prep2.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_flags2.as<uint32_t>(), st));
@@ -728,8 +722,8 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     }
     KCK(cck_fold_window(c->mode, n, c->rlc_work.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_prep2.as<uint32_t>(),
                         c->rlc_flags2.as<uint32_t>(), side));
-    KCK(cck_miller_pairs(NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(), c->fbuf.as<uint32_t>(), N, M,
-                         side));
+    KCK(cck_rlc_append(n, PS, (int)NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(),
+                       c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), side));
     KCK(prep_part(1));  // delta X~ + sum (delta m_j) Y~_j
     if (side != st) {
         HIPCK(hipEventRecord(c->ev_join, side));
@@ -737,7 +731,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     }
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     // SigG2: sigma_1's subgroup test comes from this loop's T (a failure raises rlc_any: fallback)
-    KCK(cck_miller_twin(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), c->fbuf.as<uint32_t>(), N,
+    KCK(cck_miller_twin(c->mode, NT, PS, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), c->fbuf.as<uint32_t>(), N,
                         c->mode == 0 ? c->rlc_any.as<uint32_t>() : nullptr, st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_rlc_reduce(N, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,

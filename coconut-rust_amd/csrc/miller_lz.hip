@@ -174,7 +174,8 @@ static __device__ __noinline__ void t_check(const Tw* T, const uint32_t* prep, s
 
 }  // namespace
 
-// prep: SoA slots of soa.h; flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 pr = O, bit4 pair-1 P = O
+// prep: SoA slots of soa.h, stride ps (>= the elements read); flags: bit0 sigma_1 = O, bit1 sigma_2 = O,
+// bit2 pr = O, bit4 pair-1 P = O
 // cst: SigG2 -> g~ affine in the lazy R' form (24 words, cck_lazy_form); SigG1 -> g~ lines (68 x 72
 // words); unused by kTwin.
 // The Miller value of credential i goes to fout as SoA element foff + i of stride fstride.  kTwin (RLC
@@ -183,7 +184,7 @@ static __device__ __noinline__ void t_check(const Tw* T, const uint32_t* prep, s
 // qcheck (kTwin, SigG2): each credential's Q (sigma_1) gets the G2 subgroup test from the loop's own T
 // (curve_pl.h miller_t_in_subgroup); a failure sets *qcheck.
 template <int SIG, bool kTwin>
-__global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __restrict__ prep,
+__global__ __launch_bounds__(MB, 2) void k_miller(size_t n, size_t ps, const uint32_t* __restrict__ prep,
                                                const uint32_t* __restrict__ flags, const uint32_t* __restrict__ cst,
                                                uint32_t* __restrict__ fout, size_t fstride, size_t foff,
                                                uint32_t* __restrict__ qcheck) {
@@ -199,16 +200,16 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
     const bool skip1 = kTwin ? (2 * i + 1 >= n || (flags[2 * i + 1] & 5u) != 0) : (fl & 18u) != 0;
     PSrc ps0, ps1;
     if (kTwin) {
-        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, kSigG2 ? kJac : kAffR};
-        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kSigG2 ? kJac : kAffR};
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * ps, ps, 1, kSigG2 ? kJac : kAffR};
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * ps, ps, 1, kSigG2 ? kJac : kAffR};
     } else if (kSigG2) {
-        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, kJac};
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * ps, ps, 1, kJac};
         ps1 = PSrc{cst, 1, 0, kAffRp};
     } else {
-        ps0 = PSrc{prep + (size_t)S_P1 * NL * n, n, 1, kAffRp};  // the SigG1 preps write sigma in R' form
-        ps1 = PSrc{prep + (size_t)S_P2 * NL * n, n, 1, kAffRp};
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * ps, ps, 1, kAffRp};  // the SigG1 preps write sigma in R' form
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * ps, ps, 1, kAffRp};
     }
-    const Soa S{const_cast<uint32_t*>(prep), n};
+    const Soa S{const_cast<uint32_t*>(prep), ps};
     // both T's parked in LDS between their uses
     Tw T;
     {
@@ -249,7 +250,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
                 StepState st;
                 st.f = f;
                 if (!const_line) st.T = unpark(lds, k);
-                miller_add(&st, prep, n, k ? S_Q2 : S_Q1, i, const_line ? gl : nullptr, k ? ps1 : ps0,
+                miller_add(&st, prep, ps, k ? S_Q2 : S_Q1, i, const_line ? gl : nullptr, k ? ps1 : ps0,
                            k ? skip1 : skip0);
                 if (const_line) gl += 72;
                 else park(lds, k, st.T);
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
         for (int k = 0; k < NP; k++) {
             if (k ? skip1 : skip0) continue;  // pair-uniform
             const Tw Tk = unpark(lds, k);
-            t_check(&Tk, prep, n, k ? S_Q2 : S_Q1, i, qcheck);
+            t_check(&Tk, prep, ps, k ? S_Q2 : S_Q1, i, qcheck);
         }
     }
     f = f12_conj(f);
@@ -282,22 +283,22 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, const uint32_t* __re
 #endif
 
 // twin: two credentials per lane pair (their one pair each), one Miller value (their product) per
-// two credentials; otherwise two pairs per credential.  The m Miller values (m = n, twin:
+// two credentials; otherwise two pairs per credential.  pstride: the prep SoA's stride.  The m Miller values (m = n, twin:
 // ceil(n / 2)) go to SoA elements [foff, foff + m) of stride fstride (>= foff + m); d_qcheck (twin,
 // SigG2, or null): the sigma_1 subgroup tests from the loop's T
-extern "C" int CC_MILLER_LAUNCH(int twin, size_t n, const uint32_t* d_prep, const uint32_t* d_flags,
+extern "C" int CC_MILLER_LAUNCH(int twin, size_t n, size_t pstride, const uint32_t* d_prep, const uint32_t* d_flags,
                                 const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff,
                                 uint32_t* d_qcheck, hipStream_t st) {
     if (!n) return 0;
     const size_t m = twin ? (n + 1) / 2 : n;
-    if (fstride < foff + m) return -1;
+    if (fstride < foff + m || pstride < m) return -1;
     constexpr int MB = cc::lz::MB;
     dim3 g((unsigned)((2 * m + MB - 1) / MB)), b(MB);
     if (twin)
-        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, true>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, true>), g, b, 0, st, n, pstride, d_prep, d_flags, d_const, d_f,
                            fstride, foff, d_qcheck);
     else
-        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, false>), g, b, 0, st, n, d_prep, d_flags, d_const, d_f,
+        hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, false>), g, b, 0, st, n, pstride, d_prep, d_flags, d_const, d_f,
                            fstride, foff, d_qcheck);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -75,7 +75,7 @@ DEV void st_aff_aos(uint32_t* p, const Aff<F>& a) {
 // pair 0's Q; h = 1: the fold point -sigma_2); sigma_2's subgroup test runs on the pair-lane Fp2
 // (curve_pl.h: 3 Fp a lane for a Jacobian G2 point) — sigma_1's comes free from the Miller loop's T;
 // each lane writes 8 of delta's 16 digits.
-__global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t base_index,
+__global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, size_t ps, uint64_t base_index,
                                                             const uint32_t* __restrict__ key,
                                                             const uint8_t* __restrict__ s1b,
                                                             const uint8_t* __restrict__ s2b,
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t b
     const size_t i = g >> 1;
     const int h = (int)(g & 1);
     if (i >= n) return;  // pair-uniform
-    const Soa S{prep, n};
+    const Soa S{prep, ps};
     uint32_t fl = 0;
     Aff<Fp2> a;
     if (!g2_decode(a, (h ? s2b : s1b) + i * 192)) fl |= h ? 2u : 1u;
@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg2(size_t n, uint64_t b
     }
 }
 
-__global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, int q, uint64_t base_index,
+__global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, size_t ps, int q, uint64_t base_index,
                                                           const uint32_t* __restrict__ key,
                                                           const uint8_t* __restrict__ msgs,
                                                           const uint32_t* __restrict__ table, int wbits,
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, int q, uint6
                                                           uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
     const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const Soa S{prep, n};
+    const Soa S{prep, ps};
     uint32_t kk[NR], d[NR], w4[4];
     for (int k = 0; k < 8; k++) kk[k] = key[k];
     rlc_delta_signed(d, w4, kk, base_index + i);
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, int q, uint6
 }
 
 // one credential per lane pair: lane h decodes and subgroup-checks sigma_{h+1} (one-lane G1)
-__global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, uint64_t base_index,
+__global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, size_t ps, uint64_t base_index,
                                                             const uint32_t* __restrict__ key,
                                                             const uint8_t* __restrict__ s1b,
                                                             const uint8_t* __restrict__ s2b,
@@ -161,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, uint64_t b
     const size_t i = g >> 1;
     const int h = (int)(g & 1);
     if (i >= n) return;  // pair-uniform
-    const Soa S{prep, n};
+    const Soa S{prep, ps};
     uint32_t fl = 0;
     Aff<Fp> a;
     if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, uint64_t b
 }
 
 // one credential per lane PAIR: the G2 MSM on the pair-lane Fp2 (curve_pl.h ft_add_g2)
-__global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg1(size_t n, int q, uint64_t base_index,
+__global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg1(size_t n, size_t ps, int q, uint64_t base_index,
                                                           const uint32_t* __restrict__ key,
                                                           const uint8_t* __restrict__ msgs,
                                                           const uint32_t* __restrict__ table, int wbits,
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg1(size_t n, int q, uint6
     const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
     const size_t i = g >> 1;
     if (i >= n) return;  // pair-uniform
-    const Soa S{prep, n};
+    const Soa S{prep, ps};
     uint32_t kk[NR], d[NR], w4[4];
     for (int k = 0; k < 8; k++) kk[k] = key[k];
     rlc_delta_signed(d, w4, kk, base_index + i);
@@ -269,13 +269,38 @@ __global__ void k_rlc_combine(size_t k, const uint32_t* __restrict__ parts, uint
     *flag = fl ? 1u : 0u;
 }
 
+// The fold's 16 window pairs (fold.hip: pseudo-credential w's pair 0 in prep2, stride FW, and its skip
+// flag) appended as credentials n .. n + 15 of the twin layout, so the credentials' two-per-loop Miller
+// launch runs them too (no separate launch for 16 pairs on the critical path)
+__global__ void k_rlc_append(size_t n, size_t ps, int nps, const uint32_t* __restrict__ prep2,
+                             const uint32_t* __restrict__ flags2, uint32_t* __restrict__ prep,
+                             uint32_t* __restrict__ flags) {
+    const int w = threadIdx.x;
+    if (w >= nps) return;
+    const size_t c = n + (size_t)w;
+    const Soa S{prep, ps}, S2{const_cast<uint32_t*>(prep2), (size_t)nps};
+    const int q = twin_slot(S_Q1, S_Q2, c), p = twin_slot(S_P1, S_P2, c);
+    for (int k = 0; k < 4; k++) {
+        Fp v;
+        ld_fp(v, S2, S_Q1 + k, w);
+        st_fp(S, q + k, c >> 1, v);
+    }
+    for (int k = 0; k < 3; k++) {
+        Fp v;
+        ld_fp(v, S2, S_P1 + k, w);
+        st_fp(S, p + k, c >> 1, v);
+    }
+    flags[c] = flags2[w] ? 1u : 0u;  // bit0: skip the pair
+}
+
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 extern "C" {
 
-// d_pts: n fold points (AoS affine: 48 words SigG2, 24 SigG1); d_dig: 16 x n digit bytes.
+// d_pts: n fold points (AoS affine: 48 words SigG2, 24 SigG1); d_dig: 16 x n digit bytes; ps: the prep
+// SoA's stride (>= (n + 16 + 1) / 2: the fold's window pairs are appended, k_rlc_append).
 // part 0: decode + subgroup checks + the fold's inputs; part 1: the delta-scaled MSM
-int cck_prep_rlc(int mode, int part, size_t n, int q, uint64_t base_index, const uint32_t* d_key,
+int cck_prep_rlc(int mode, int part, size_t n, size_t ps, int q, uint64_t base_index, const uint32_t* d_key,
                  const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits,
                  const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_any, uint32_t* d_pts,
                  int8_t* d_dig, hipStream_t st) {
@@ -283,17 +308,17 @@ int cck_prep_rlc(int mode, int part, size_t n, int q, uint64_t base_index, const
     const dim3 g2(nblocks(2 * n, 256)), g1(nblocks(n, 256)), b(256);
     if (part == 0) {
         if (mode == 0)
-            hipLaunchKernelGGL(k_rlc_check_sigg2, g2, b, 0, st, n, base_index, d_key, d_s1, d_s2, d_prep, d_flags,
+            hipLaunchKernelGGL(k_rlc_check_sigg2, g2, b, 0, st, n, ps, base_index, d_key, d_s1, d_s2, d_prep, d_flags,
                                d_any, d_pts, d_dig);
         else
-            hipLaunchKernelGGL(k_rlc_check_sigg1, g2, b, 0, st, n, base_index, d_key, d_s1, d_s2, d_prep, d_flags,
+            hipLaunchKernelGGL(k_rlc_check_sigg1, g2, b, 0, st, n, ps, base_index, d_key, d_s1, d_s2, d_prep, d_flags,
                                d_any, d_pts, d_dig);
     } else {
         if (mode == 0)
-            hipLaunchKernelGGL(k_rlc_msm_sigg2, g1, b, 0, st, n, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
+            hipLaunchKernelGGL(k_rlc_msm_sigg2, g1, b, 0, st, n, ps, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
                                d_prep, d_flags);
         else
-            hipLaunchKernelGGL(k_rlc_msm_sigg1, g2, b, 0, st, n, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
+            hipLaunchKernelGGL(k_rlc_msm_sigg1, g2, b, 0, st, n, ps, q, base_index, d_key, d_msgs, d_table, wbits, d_binf,
                                d_prep, d_flags);
     }
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -314,6 +339,12 @@ int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any
         dst = t;
     }
     hipLaunchKernelGGL(k_rlc_partial_out, dim3(1), dim3(192), 0, st, src, d_any, d_partial);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int cck_rlc_append(size_t n, size_t ps, int nps, const uint32_t* d_prep2, const uint32_t* d_flags2, uint32_t* d_prep,
+                   uint32_t* d_flags, hipStream_t st) {
+    hipLaunchKernelGGL(k_rlc_append, dim3(1), dim3(64), 0, st, n, ps, nps, d_prep2, d_flags2, d_prep, d_flags);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
