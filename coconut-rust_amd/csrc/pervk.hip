@@ -144,7 +144,7 @@ extern "C" {
 
 // scratch words of cck_prep_var for n credentials of q messages
 size_t cck_prep_var_words(int mode, size_t n, size_t q) {
-    return n * q * 8 + n * (mode == 0 ? straus_g1lz_words(q) : straus_lz_words(q)) + 64;
+    return straus_round32(n * q * 8) + n * (mode == 0 ? straus_g1lz_words(q) : straus_lz_words(q)) + 64;
 }
 
 // Per-credential-verkey prep: vkX n x OtherGroup, vkY n x q x OtherGroup, msgs n x q x 48 B;
@@ -154,7 +154,7 @@ int cck_prep_var(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* 
                  uint32_t* d_flags, hipStream_t st) {
     if (!n) return 0;
     uint32_t* scal = d_scratch;
-    uint32_t* straus = d_scratch + n * (size_t)q * 8;
+    uint32_t* straus = d_scratch + straus_round32(n * (size_t)q * 8);  // 128-byte-aligned task regions
     if (q) hipLaunchKernelGGL(k_scalars_w8, dim3(nblocks(n * (size_t)q, 256)), dim3(256), 0, st, n * (size_t)q, d_msgs, scal);
     if (mode == 0)
         hipLaunchKernelGGL(k_prep_sigg2_var, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_vkX,
