@@ -431,7 +431,7 @@ def bench_pervk(args):
         peak = peak_mad_per_s()
         sb, ob = (192, 97) if mode == 0 else (97, 192)
         kt = kernel_table(phase_ms, n, counts, 2 * sb + q * 48 + (q + 1) * ob, peak,
-                          "k_prep_sigg2_var" if mode == 0 else "k_prep_sigg1_var", None)
+                          "k_prep_sigg2_var" if mode == 0 else "k_prep_sigg1_var", args.mode)
         dom = max(kt, key=lambda k: kt[k]["ms"])
         total = sum(counts.values()) * MADS_PER_M * n
         out = {
@@ -454,6 +454,7 @@ def bench_pervk(args):
                          "whole_step_frac": round(total / (el / args.steps) / peak, 4)},
             "kernels": kt,
             "prep_over_miller": round(kt["prep"]["ms"] / kt["miller"]["ms"], 3) if kt["miller"]["ms"] else None,
+            "rocprof_kernels": __import__("bench").kernel_pmc_report(args.mode),
             "setup": {"synthetic_data_s": round(gen_s, 2)},
         }
         if not args.no_cpu_baseline and world == 1:

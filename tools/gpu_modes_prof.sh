@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 TAG=${1:-modes}
 shift || true
-MODES=${*:-verify verify-g1 rlc aggregate pok}
+MODES=${*:-verify verify-g1 verify-pervk rlc aggregate pok}
 export TMPDIR=/tmp
 for m in $MODES; do
   OUT=$R/gpurun_out/$TAG/$m
