@@ -539,7 +539,7 @@ def bench_verify(args, mode):
 def bench_rlc(args):
     """BASELINE config 3: q = 16 credentials verified in RLC batch mode.  Each rank owns 131,072
     credentials (2^20 over 8 GPUs); a step = per-rank partial (delta-weighted Miller product of the
-    slice) -> RCCL all-gather of the 580-byte partials -> one final exponentiation on every rank ->
+    slice) -> RCCL all-gather of the 3,716-byte partials -> one final exponentiation on every rank ->
     accept.  All credentials are valid, so the accept path is timed; the reject path (one corrupted
     credential -> every rank rejects -> per-credential fallback) is checked after the timed region."""
     import numpy as np

@@ -63,6 +63,7 @@ _SIGS = {
     "cc_sigreq_verify_batch": (c_int, [c_p, c_sz, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p]),
     "cc_vss_verify_batch": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_sz, c_p, c_p, c_p, c_p]),
     "cc_fixed_base_mul": (c_int, [c_p, c_int, c_p, c_sz, c_p, c_p]),
+    "cc_rlc_partial_words": (c_int, []),
     "cc_rlc_partial_device": (c_int, [c_p, c_sz, c_sz, ctypes.c_uint64, c_p, c_p, c_p, c_p, c_p, c_p]),
     "cc_rlc_finish_device": (c_int, [c_p, c_sz, c_p, c_p, c_p, c_p]),
     "cc_last_timing": (c_int, [c_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float),

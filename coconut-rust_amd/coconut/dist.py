@@ -5,10 +5,11 @@ The batch shards by credential (credentials are independent):
 
 * per-credential mode — every rank verifies its own contiguous slice; no collective on the data
   path (verdicts stay with the rank that owns the slice);
-* RLC mode — every rank reduces its slice to one 145-word partial (the Fp12 Miller product of its
-  delta-weighted pairs + an identity flag, ``cc_rlc_partial_device``); ONE all-gather of the partials
-  (580 B per rank) is the only exchange; every rank multiplies the gathered partials and runs the
-  single final exponentiation (``cc_rlc_finish_device``), so all ranks reach the same accept/reject
+* RLC mode — every rank reduces its slice to one 929-word partial (the Fp12 Miller product of its
+  delta-weighted pairs, a fall-back flag and its 16 fold window sums, ``cc_rlc_partial_device``); ONE
+  all-gather of the partials (3,716 B per rank) is the only exchange; every rank pairs the gathered
+  window sums with the fixed multiples of g~, multiplies everything and runs the single final
+  exponentiation (``cc_rlc_finish_device``), so all ranks reach the same accept/reject
   decision without a second collective.  On reject every rank falls back to per-credential
   verification of its own slice, so verdicts always equal the reference's
   (``Signature::verify``, reference src/signature.rs:473-478, per credential).
@@ -25,7 +26,10 @@ from typing import Optional
 
 import numpy as np
 
-PARTIAL_WORDS = 145  # 144 Fp12 Montgomery words + identity flag
+# 144 Fp12 Montgomery words, fall-back flag, 16 x (48-word affine window sum + identity flag):
+# CC_RLC_PARTIAL_WORDS of include/coconut_hip.h (= cc_rlc_partial_words(), checked by tests/test_capi.py)
+PARTIAL_WORDS = 929
+PARTIAL_FLAG = 144
 
 
 def shard_bounds(n: int, world: int, rank: int):
@@ -40,7 +44,7 @@ def _dist():
 
 def gather_partials(part, group=None):
     """All-gather the per-rank partials (one tensor of PARTIAL_WORDS int32 each) -> (stacked, k).
-    Over RCCL ("nccl") the device tensors are gathered in place (580 B per rank over xGMI); over gloo
+    Over RCCL ("nccl") the device tensors are gathered in place (3,716 B per rank over xGMI); over gloo
     (CPU transport: tests, hosts without RCCL) a device partial crosses through host memory and the
     gathered partials return to its device."""
     import torch
@@ -149,7 +153,10 @@ class DeviceEngine:
         reuses the slot of an unfinished batch waits for that batch's finish on the device."""
         import torch
         if self._fin_stream is None:
-            self._fin_stream = torch.cuda.Stream(self.dev)
+            # high priority: the finish's latency-bound launches (16 waves of window pairs per partial, the
+            # product tree, one final exponentiation) take wave slots ahead of the next partial's full
+            # launches instead of queueing behind them
+            self._fin_stream = torch.cuda.Stream(self.dev, priority=-1)
         fs = self._fin_stream
         allp = allp.contiguous()
         fs.wait_stream(torch.cuda.current_stream(self.dev))  # the gathered partials are ready

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/coconut_hip.h"
+#include "rlc_part.h"
 
 extern "C" {
 int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_out, uint32_t* d_inf, hipStream_t st);
@@ -51,11 +52,12 @@ int cck_miller_lz_g1(int twin, size_t n, size_t pstride, const uint32_t* d_prep,
                      hipStream_t st);
 size_t cck_fold_words(int mode, size_t n);
 int cck_fold_pseudo();
-int cck_fold_window(int mode, size_t n, uint32_t* d_work, const uint8_t* d_finf, uint32_t* d_prep2,
-                    uint32_t* d_flags2, hipStream_t st);
-int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok,
-             int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
-             uint32_t* d_flags2, hipStream_t st);
+int cck_fold_window(int mode, size_t n, uint32_t* d_work, uint32_t* d_partial, hipStream_t st);
+int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, hipStream_t st);
+int cck_fold_fixed(int mode, int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_pw,
+                   uint8_t* d_finf, hipStream_t st);
+int cck_miller_wide(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f, size_t fstride,
+                    size_t foff, hipStream_t st);
 int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
              uint8_t* d_gt, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
@@ -76,9 +78,8 @@ int cck_prep_rlc(int mode, int part, size_t n, size_t ps, int q, uint64_t base_i
                  int8_t* d_dig, hipStream_t st);
 int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any, uint32_t* d_partial,
                    hipStream_t st);
-int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t* d_flag, hipStream_t st);
-int cck_rlc_append(size_t n, size_t ps, int nps, const uint32_t* d_prep2, const uint32_t* d_flags2, uint32_t* d_prep,
-                   uint32_t* d_flags, hipStream_t st);
+int cck_rlc_gather(int mode, size_t k, const uint32_t* d_parts, const uint32_t* d_pw, const uint8_t* d_finf,
+                   uint32_t* d_fw, size_t fs, uint32_t* d_prep, uint32_t* d_flags2, uint32_t* d_flag, hipStream_t st);
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
                  const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
@@ -159,13 +160,16 @@ struct cc_ctx {
     DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, lag;  // vkb: per-credential-verkey MSM scratch
     // RLC batch mode: ChaCha20 key, identity flag word, partial / gathered partials, verdict
     DevBuf rlc_key, rlc_any, rlc_part, rlc_flag, rlc_accept;
-    DevBuf fin_f, fin_scratch;  // cc_rlc_finish_device's own buffers
+    // cc_rlc_finish_device's own buffers: Fp12 values (partial products, window pairs' Miller values),
+    // the product tree's other half / the one-element fexp's scratch, the window pairs' prep and skip
+    // flags, the combined product
+    DevBuf fin_f, fin_scratch, fin_prep, fin_flags2, fin_part;
     hipEvent_t ev_fin = nullptr;  // end of the last finish: finishes of one context run in call order
     bool fin_recorded = false;
-    // RLC g~-side fold (fold.hip): fold points, delta digits, sort/partials/bucket workspace, the 16
-    // pseudo-credentials' prep SoA (window sums + the fixed points P_w = (256^w) g~) and flags
-    DevBuf rlc_pts, rlc_dig, rlc_work, rlc_prep2, rlc_finf, rlc_flags2;
-    bool rlc_fixed_ok = false;  // P_w in rlc_prep2 match the current tables
+    // RLC g~-side fold (fold.hip): fold points, delta digits, sort/partials/bucket workspace; the fixed
+    // points P_w = (256^w) g~ of the window pairs (SoA, built with the verkey tables) and their
+    // identity flags
+    DevBuf rlc_pts, rlc_dig, rlc_work, rlc_pw, rlc_finf;
     DevBuf pok_idx;  // revealed indices of the last PoK batch
     // issuer table (cc_set_issuers): sorted ids, decoded verkeys, per-base 8-bit window tables
     size_t iss_n = 0, iss_q = 0;
@@ -189,7 +193,7 @@ struct cc_ctx {
     // per GPU (ncclCommInitAll, this process drives every device); empty for a single-device context
     std::vector<cc_ctx*> peers;
     std::vector<ncclComm_t> comms;
-    DevBuf rlc_gath;  // per peer: gathered partials (ndev x 145 words)
+    DevBuf rlc_gath;  // per peer: gathered partials (ndev x RLC_PART_WORDS words)
 };
 
 // Every *_device entry point may run on a caller stream while the context's workspaces (prep, flags,
@@ -223,8 +227,8 @@ static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t
     return mode == 0 ? cck_miller_lz_g2(0, n, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st)
                      : cck_miller_lz_g1(0, n, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st);
 }
-// the RLC credentials (pair 0 only: their second pairs are folded, fold.hip) and the fold's window
-// pairs appended after them (k_rlc_append), two per lane pair through the shared-squaring loop:
+// the RLC credentials (pair 0 only: their second pairs are folded, fold.hip), two per lane pair
+// through the shared-squaring loop:
 // (n + 1) / 2 Miller values, each the product of two pairs' (the RLC multiplies them all), to SoA
 // elements [0, (n + 1) / 2) of stride fstride; the prep SoA has stride ps
 static int cck_miller_twin(int mode, size_t n, size_t ps, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
@@ -273,6 +277,9 @@ const char* cc_status_str(int s) {
 #endif
 const char* cc_version(void) { return "coconut-mi355x 0.2.0 (gfx950) src " CC_SRC_HASH; }
 
+static_assert(CC_RLC_PARTIAL_WORDS == RLC_PART_WORDS, "coconut_hip.h and rlc_part.h disagree");
+int cc_rlc_partial_words(void) { return RLC_PART_WORDS; }
+
 cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
     if (!out || (mode != CC_SIG_G2 && mode != CC_SIG_G1)) return CC_ERR_DECODE;
     int ndev = 0;
@@ -317,8 +324,8 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->gtilde_lz, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->lag,
-                      &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->fin_f, &c->fin_scratch, &c->pok_idx, &c->rlc_gath,
-                      &c->rlc_pts, &c->rlc_dig, &c->rlc_work, &c->rlc_prep2, &c->rlc_finf, &c->rlc_flags2,
+                      &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->fin_f, &c->fin_scratch, &c->fin_prep, &c->fin_flags2, &c->fin_part, &c->pok_idx, &c->rlc_gath,
+                      &c->rlc_pts, &c->rlc_dig, &c->rlc_work, &c->rlc_pw, &c->rlc_finf,
                       &c->iss_ids, &c->iss_aff, &c->iss_inf, &c->iss_table, &c->agg_scratch, &c->dev_err};
     for (auto* b : bufs) b->release();
     for (auto& b : c->in_aux) b.release();
@@ -391,7 +398,6 @@ static cc_status rebuild_tables(cc_ctx* c) {
     int og = oth_group(c->mode);
     size_t aw = aff_words(og);
     int nb = (int)c->q + 2;
-    c->rlc_fixed_ok = false;
     int wb = c->force_vk_bits;
     // the old table is released first so its memory counts as free
     c->table.release();
@@ -428,6 +434,13 @@ static cc_status rebuild_tables(cc_ctx* c) {
     if (pw.ensure((size_t)nb * tab_nwin(c->wbits) * (og == 1 ? 36 : 72) * 4)) return CC_ERR_HIP;
     KCK(cck_build_table(og, nb, c->wbits, c->vk_aff.as<uint32_t>() + aw, c->table_inf.as<uint32_t>(), pw.as<uint32_t>(),
                         c->table.as<uint32_t>(), 1, c->stream));
+    // the RLC window pairs' fixed points P_w = (256^w) g~ (g~ = base q); an RLC finish still running on
+    // another stream reads them, so the rewrite waits for it
+    if (c->rlc_pw.ensure((size_t)PREP_SLOTS * 12 * RLC_WINDOWS * 4) || c->rlc_finf.ensure(RLC_WINDOWS))
+        return CC_ERR_HIP;
+    if (c->fin_recorded) HIPCK(hipStreamWaitEvent(c->stream, c->ev_fin, 0));
+    KCK(cck_fold_fixed(c->mode, (int)c->q, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(),
+                       c->rlc_pw.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->stream));
     HIPCK(hipStreamSynchronize(c->stream));
     pw.release();
     return CC_OK;
@@ -669,25 +682,26 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     StreamOrder order(c, st);
     if (!n) {
         // empty shard (a batch smaller than the rank count): the neutral partial — Fp12 one (Montgomery
-        // one in slot 0, zeros elsewhere) and a clear identity flag — so every rank still joins the
-        // all-gather and the product over ranks is unchanged
+        // one in slot 0, zeros elsewhere), a clear fall-back flag and 16 identity window sums — so every
+        // rank still joins the all-gather and the product over ranks is unchanged
         static const uint32_t kOne[12] = {0x03a9fb84u, 0xc57400d2u, 0x629c4a23u, 0x6147acdeu, 0x7e6d26cbu, 0x6b0f4b0bu,
                                           0xc2b7d6e1u, 0x91ecbde7u, 0x4fdd80b8u, 0xd56a23c3u, 0xf3a0d636u, 0x13317c30u};
-        HIPCK(hipMemsetAsync(d_partial, 0, 145 * 4, st));
-        HIPCK(hipMemcpyAsync(d_partial, kOne, sizeof(kOne), hipMemcpyHostToDevice, st));
+        static const std::vector<uint32_t> kNeutral = [] {
+            std::vector<uint32_t> v(RLC_PART_WORDS, 0u);
+            memcpy(v.data(), kOne, sizeof(kOne));
+            for (int w = 0; w < RLC_WINDOWS; w++) v[RLC_WIN_OFF + RLC_WIN_WORDS * w + 48] = 1u;
+            return v;
+        }();
+        HIPCK(hipMemcpyAsync(d_partial, kNeutral.data(), RLC_PART_WORDS * 4, hipMemcpyHostToDevice, st));
         return CC_OK;
     }
-    const size_t NPS = (size_t)cck_fold_pseudo();  // fold pseudo-credentials (one per window, one pair each)
-    const size_t NT = n + NPS;       // pairs of the twin Miller launch: the credentials', then the windows'
-    const size_t N = (NT + 1) / 2;   // Miller values (two pairs each)
-    const size_t PS = NT;            // prep SoA stride (>= N elements)
-    cc_status s = ensure_work(c, NT);
+    const size_t N = (n + 1) / 2;  // Miller values (two credentials' pairs each)
+    const size_t PS = N;           // prep SoA stride
+    cc_status s = ensure_work(c, n);
     if (s) return s;
     if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4) || c->fbuf.ensure(N * 144 * 4) ||
         c->scratch.ensure(((N + 1) / 2) * 144 * 4 + n * 12 * 4 * 72) || c->rlc_pts.ensure(n * 48 * 4) ||
-        c->rlc_dig.ensure(16 * n) || c->rlc_work.ensure(cck_fold_words(c->mode, n) * 4) ||
-        c->rlc_prep2.ensure((size_t)PREP_SLOTS * 12 * NPS * 4) || c->rlc_finf.ensure(2 * NPS) ||
-        c->rlc_flags2.ensure(NPS * 4))
+        c->rlc_dig.ensure(16 * n) || c->rlc_work.ensure(cck_fold_words(c->mode, n) * 4))
         return CC_ERR_HIP;
     memcpy(c->rlc_key_host, seed32, 32);
     HIPCK(hipMemcpyAsync(c->rlc_key.p, c->rlc_key_host, 32, hipMemcpyHostToDevice, st));
@@ -706,36 +720,31 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
         static const uint32_t one = 1;
         HIPCK(hipMemcpyAsync(c->rlc_any.p, &one, 4, hipMemcpyHostToDevice, st));
     }
-    // The second pairs become 16 window pairs (fold.hip).  The fold's short kernels run alone
-    // (behind a full launch each would wait milliseconds for a free slot); its window sums (16 waves)
-    // then run on the high-priority side stream beside the delta MSM and are appended to the
-    // credentials' pairs (k_rlc_append), so the one two-pairs-per-loop Miller launch (2,048 waves at
-    // 131,072 credentials: the chip's wave slots) covers them; it starts once both are done.
-    KCK(cck_fold(c->mode, n, c->rlc_dig.as<int8_t>(), c->rlc_pts.as<uint32_t>(), c->rlc_work.as<uint32_t>(),
-                 c->rlc_fixed_ok ? 1 : 0, (int)q, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(),
-                 c->rlc_prep2.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_flags2.as<uint32_t>(), st));
-    c->rlc_fixed_ok = true;
+    // The second pairs fold into 16 window sums S_w (fold.hip).  The fold's short kernels run alone
+    // (behind a full launch each would wait milliseconds for a free slot); the window sums (16 waves)
+    // then run on the high-priority side stream beside the delta MSM and land in the partial's window
+    // section; their pairs e(S_w, P_w) are evaluated in the finish, once per batch over every shard
+    // (rlc_part.h), so the credentials' two-per-loop Miller launch stays at (n + 1) / 2 loops (2,048
+    // waves at 131,072 credentials: the chip's wave slots).
+    KCK(cck_fold(c->mode, n, c->rlc_dig.as<int8_t>(), c->rlc_pts.as<uint32_t>(), c->rlc_work.as<uint32_t>(), st));
     hipStream_t side = c->side ? c->side : st;
     if (side != st) {
         HIPCK(hipEventRecord(c->ev_fork, st));
         HIPCK(hipStreamWaitEvent(side, c->ev_fork, 0));
     }
-    KCK(cck_fold_window(c->mode, n, c->rlc_work.as<uint32_t>(), c->rlc_finf.as<uint8_t>(), c->rlc_prep2.as<uint32_t>(),
-                        c->rlc_flags2.as<uint32_t>(), side));
-    KCK(cck_rlc_append(n, PS, (int)NPS, c->rlc_prep2.as<uint32_t>(), c->rlc_flags2.as<uint32_t>(),
-                       c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), side));
+    KCK(cck_fold_window(c->mode, n, c->rlc_work.as<uint32_t>(), d_partial, side));
     KCK(prep_part(1));  // delta X~ + sum (delta m_j) Y~_j
-    if (side != st) {
-        HIPCK(hipEventRecord(c->ev_join, side));
-        HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));
-    }
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     // SigG2: sigma_1's subgroup test comes from this loop's T (a failure raises rlc_any: fallback)
-    KCK(cck_miller_twin(c->mode, NT, PS, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), c->fbuf.as<uint32_t>(), N,
+    KCK(cck_miller_twin(c->mode, n, PS, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), c->fbuf.as<uint32_t>(), N,
                         c->mode == 0 ? c->rlc_any.as<uint32_t>() : nullptr, st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_rlc_reduce(N, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,
                        st));
+    if (side != st) {  // the window section is part of the partial: the call ends when both are written
+        HIPCK(hipEventRecord(c->ev_join, side));
+        HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));
+    }
     if (c->timing) {
         (void)hipEventRecord(c->ev[3], st);
         collect_timing(c);
@@ -747,20 +756,35 @@ cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_parti
                                uint8_t* d_gt, void* stream) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || !nparts || !d_partials || !d_accept) return CC_ERR_DECODE;
+    if (!c->have_params || !c->have_vk) return CC_ERR_STATE;  // the window pairs' P_w come with the verkey
     HIPCK(hipSetDevice(c->device));
-    // the finish owns its buffers (combined product, the one-element fexp's scratch, flag) and touches no
-    // other context state, so it is NOT ordered against the context's stream: on a caller stream it may
+    // the finish owns its buffers (Fp12 values, window-pair operands, fexp scratch, flag) and reads only
+    // the verkey's P_w, so it is NOT ordered against the context's stream: on a caller stream it may
     // overlap the next batch's cc_rlc_partial_device (the caller orders d_partials itself).  Finishes of
     // one context are ordered among themselves (ev_fin): two finishes on different streams never share
-    // the buffers at the same time, whichever engines or streams issue them.
-    if (c->rlc_flag.ensure(4) || c->fin_f.ensure(12 * 12 * 4) || c->fin_scratch.ensure(2 * 72 * 12 * 4))
+    // the buffers at the same time, whichever engines or streams issue them; a verkey change waits for
+    // the last finish before it rewrites P_w.
+    const size_t k = nparts, NW = (size_t)RLC_WINDOWS * k, NF = k + NW;
+    if (c->rlc_flag.ensure(4) || c->fin_f.ensure(NF * 144 * 4) ||
+        c->fin_scratch.ensure(std::max(((NF + 1) / 2) * 144 * 4, (size_t)2 * 72 * 12 * 4)) ||
+        c->fin_prep.ensure((size_t)PREP_SLOTS * 12 * NW * 4) || c->fin_flags2.ensure(NW * 4) ||
+        c->fin_part.ensure(RLC_PART_WORDS * 4))
         return CC_ERR_HIP;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     if (c->fin_recorded) HIPCK(hipStreamWaitEvent(st, c->ev_fin, 0));
-    KCK(cck_rlc_combine(nparts, d_partials, c->fin_f.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), st));
-    // one final exponentiation; flags[0] bit0 (a sigma was the identity somewhere) forces a reject
-    KCK(cck_fexp(1, c->fin_f.as<uint32_t>(), c->fin_scratch.as<uint32_t>(), c->rlc_flag.as<uint32_t>(), d_accept,
-                 d_gt, st));
+    // the partials' products (elements 0 .. k-1) and every shard's 16 window pairs e(S_w, P_w), one wave
+    // each (latency-bound: one loop's length for any k up to 16 GPUs), to elements k .. 17 k - 1; the
+    // product tree multiplies all 17 k; one final exponentiation, whose flag (a sigma was the identity or
+    // outside the subgroup somewhere) forces a reject
+    KCK(cck_rlc_gather(c->mode, k, d_partials, c->rlc_pw.as<uint32_t>(), c->rlc_finf.as<uint8_t>(),
+                       c->fin_f.as<uint32_t>(), NF, c->fin_prep.as<uint32_t>(), c->fin_flags2.as<uint32_t>(),
+                       c->rlc_flag.as<uint32_t>(), st));
+    KCK(cck_miller_wide(NW, c->fin_prep.as<uint32_t>(), c->fin_flags2.as<uint32_t>(), c->fin_f.as<uint32_t>(), NF, k,
+                        st));
+    KCK(cck_rlc_reduce(NF, c->fin_f.as<uint32_t>(), c->fin_scratch.as<uint32_t>(), c->rlc_flag.as<uint32_t>(),
+                       c->fin_part.as<uint32_t>(), st));
+    KCK(cck_fexp(1, c->fin_part.as<uint32_t>(), c->fin_scratch.as<uint32_t>(), c->fin_part.as<uint32_t>() + RLC_FLAG,
+                 d_accept, d_gt, st));
     HIPCK(hipEventRecord(c->ev_fin, st));
     c->fin_recorded = true;
     return CC_OK;
@@ -770,7 +794,7 @@ cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_parti
 static cc_status rlc_host(cc_ctx* c, size_t n, size_t q, uint8_t* accept) {
     uint8_t seed[32];
     if (fresh_seed(seed)) return CC_ERR_HIP;
-    if (c->rlc_part.ensure(145 * 4) || c->rlc_accept.ensure(1)) return CC_ERR_HIP;
+    if (c->rlc_part.ensure(RLC_PART_WORDS * 4) || c->rlc_accept.ensure(1)) return CC_ERR_HIP;
     cc_status s = cc_rlc_partial_device(c, n, q, 0, seed, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(),
                                         c->in_msgs.as<uint8_t>(), c->rlc_part.as<uint32_t>(), c->stream);
     if (s) return s;
@@ -1544,7 +1568,7 @@ static cc_status for_shards(cc_ctx* c, size_t n, F f) {
 extern "C" {
 
 // Shard by credential over the device set.  Per-credential mode: every device verifies its slice, no
-// collective.  RLC mode (shared verkey): every device reduces its slice to one 145-word partial, ONE
+// collective.  RLC mode (shared verkey): every device reduces its slice to one RLC_PART_WORDS-word partial, ONE
 // ncclAllGather over xGMI exchanges them, every device multiplies the gathered partials and runs the
 // single final exponentiation; on reject every device falls back to per-credential verification.
 static cc_status multi_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, const uint8_t* s2,
@@ -1561,7 +1585,7 @@ static cc_status multi_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, 
             const size_t m = hi - lo;
             HIPCK(hipSetDevice(p->device));
             if (p->in_s1.ensure(m * sb + 16) || p->in_s2.ensure(m * sb + 16) || p->in_msgs.ensure(m * q * 48 + 16) ||
-                p->rlc_part.ensure(145 * 4) || p->rlc_gath.ensure(k * 145 * 4) || p->rlc_accept.ensure(1))
+                p->rlc_part.ensure(RLC_PART_WORDS * 4) || p->rlc_gath.ensure(k * RLC_PART_WORDS * 4) || p->rlc_accept.ensure(1))
                 return CC_ERR_HIP;
             if (m) {
                 HIPCK(hipMemcpyAsync(p->in_s1.p, s1 + lo * sb, m * sb, hipMemcpyHostToDevice, p->stream));
@@ -1576,7 +1600,7 @@ static cc_status multi_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, 
         if (ncclGroupStart() != ncclSuccess) return CC_ERR_RCCL;
         for (size_t d = 0; d < k; d++) {
             cc_ctx* p = c->peers[d];
-            if (ncclAllGather(p->rlc_part.p, p->rlc_gath.p, 145, ncclUint32, c->comms[d], p->stream) != ncclSuccess) {
+            if (ncclAllGather(p->rlc_part.p, p->rlc_gath.p, RLC_PART_WORDS, ncclUint32, c->comms[d], p->stream) != ncclSuccess) {
                 ncclGroupEnd();
                 return CC_ERR_RCCL;
             }

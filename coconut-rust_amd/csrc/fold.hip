@@ -26,21 +26,22 @@
 //   k_fold_window_g2pl                            Fp2 (curve_pl.h): one LANE PAIR per chunk / 32 pairs
 //                                                 per bucket or window, 2 waves/SIMD where the one-lane
 //                                                 G2 forms need 448-512 registers (1 wave/SIMD)
-//   k_fold_fixed<F>                             : the fixed points P_w (once per verkey)
+//   k_fold_fixed<F>                             : the fixed points P_w (once per verkey, cck_fold_fixed)
 // X_i = -sigma_2,i (AoS affine in the lazy field's form, fixed.h fp_to_lazy_form; written by the RLC
-// prep); S_w lands in the pseudo-credentials' prep SoA (soa.h slots, stride FW; window w =
-// pseudo-credential w, pair 0) as the Q side (SigG2: S in G2) or the P side (SigG1: S in G1), P_w on
-// the other side.
+// prep); S_w lands in the shard's partial (rlc_part.h: affine words + identity flag per window), and
+// the finish pairs every shard's S_w with P_w (rlc.hip k_rlc_gather, then k_miller_wide): SigG2 S in
+// G2 (the Q side), SigG1 S in G1 (the P side), P_w on the other side.
 #include "codec.h"
 #include "curve_pl.h"
 #include "fixed.h"
+#include "rlc_part.h"
 #include "soa.h"
 
 using namespace cc;
 
 namespace {
 
-constexpr int FW = 16;        // windows: signed base-256 digits of delta
+constexpr int FW = RLC_WINDOWS;  // windows: signed base-256 digits of delta
 constexpr int FD = 128;       // |digit| values per window
 constexpr int FB = FW * FD;   // buckets
 constexpr int FS = 16;        // list entries per chunk (one lane)
@@ -189,10 +190,9 @@ __global__ __launch_bounds__(64) void k_fold_reduce(const uint32_t* __restrict__
 
 // one wave per window (one lane per CK = 2 digits): lane t's share of S_w = sum_d d B_d over the
 // digits d = CK t + k + 1 (k < CK) is U + [CK t] T with U = sum_k (k + 1) B and T = sum_k B (running
-// sums from the top digit down), on the lazy field; a butterfly adds the lanes.  S_w, affine, becomes
-// pseudo-credential w (P side: SigG1, S in G1); flags2[w]: skip the pair (S_w = O or P_w = O)
-__global__ __launch_bounds__(64) void k_fold_window(const uint32_t* __restrict__ bkt, const uint8_t* __restrict__ fixed_inf,
-                                                    uint32_t* __restrict__ prep2, uint32_t* __restrict__ flags2) {
+// sums from the top digit down), on the lazy field; a butterfly adds the lanes.  S_w (SigG1: in G1),
+// affine, and its identity flag go to the partial's window w (rlc_part.h)
+__global__ __launch_bounds__(64) void k_fold_window(const uint32_t* __restrict__ bkt, uint32_t* __restrict__ part) {
     constexpr int JW = sizeof(Jac<Fp>) / 4, CK = FD / 64;
     const int w = blockIdx.x, t = threadIdx.x;
     lz::JG run = lz::jg_inf(), u = lz::jg_inf(), v = lz::jg_inf();
@@ -215,8 +215,15 @@ __global__ __launch_bounds__(64) void k_fold_window(const uint32_t* __restrict__
     if (threadIdx.x != 0) return;
     Aff<Fp> a;
     const bool fin = jac_to_aff(a, acc);
-    st_as_p(Soa{prep2, FW}, w, a);
-    flags2[w] = (!fin || fixed_inf[w]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
+    uint32_t* o = part + RLC_WIN_OFF + RLC_WIN_WORDS * w;
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+        o[k] = fin ? a.x.v[k] : 0u;
+        o[NL + k] = fin ? a.y.v[k] : 0u;
+        o[2 * NL + k] = 0u;
+        o[3 * NL + k] = 0u;
+    }
+    o[4 * NL] = fin ? 0u : 1u;  // e(O, .) = 1: the finish skips the pair
 }
 
 // k_fold_sum for G2 points on the pair-lane Fp2: one lane pair per chunk, each lane adds its halves.
@@ -268,12 +275,11 @@ __global__ __launch_bounds__(64, 2) void k_fold_reduce_g2pl(const uint32_t* __re
     if (threadIdx.x < 2) st_jac_aos<pl::Fp2>(bkt + (size_t)b * JW + h * HW, acc);
 }
 
-// k_fold_window for G2 buckets on the pair-lane Fp2 (one lane pair per CK = 4 digits), S_w as the
-// Q side (SigG2).  The lane pair's share runs on the lazy pair-lane field (curve_lz.h): latency-bound
-// (16 waves), and beside the delta MSM's waves every dependent step counts.
-__global__ __launch_bounds__(64, 2) void k_fold_window_g2pl(const uint32_t* __restrict__ bkt,
-                                                           const uint8_t* __restrict__ fixed_inf,
-                                                           uint32_t* __restrict__ prep2, uint32_t* __restrict__ flags2) {
+// k_fold_window for G2 buckets on the pair-lane Fp2 (one lane pair per CK = 4 digits), S_w in G2
+// (SigG2).  The lane pair's share runs on the lazy pair-lane field (curve_lz.h): latency-bound (16
+// waves), and beside the delta MSM's waves every dependent step counts.  Lane h of pair 0 writes the
+// h-halves (x.a / x.b, y.a / y.b) of the partial's window w.
+__global__ __launch_bounds__(64, 2) void k_fold_window_g2pl(const uint32_t* __restrict__ bkt, uint32_t* __restrict__ part) {
     constexpr int JW = sizeof(Jac<Fp2>) / 4, HW = sizeof(Jac<pl::Fp2>) / 4, CK = FD / 32;
     const int w = blockIdx.x, t = threadIdx.x >> 1;  // pair-uniform
     const int h = (int)pl::half_id();
@@ -296,17 +302,20 @@ __global__ __launch_bounds__(64, 2) void k_fold_window_g2pl(const uint32_t* __re
     pl::pair_group_sum<64>(acc);
     if (threadIdx.x >= 2) return;
     Aff<pl::Fp2> a;
-    const bool fin = jac_to_aff(a, acc);
-    const Soa S{prep2, FW};
-    pl::st_f2(S, S_Q1, w, a.x);
-    pl::st_f2(S, S_Q1 + 2, w, a.y);
-    if (!h) flags2[w] = (!fin || fixed_inf[w]) ? 1u : 0u;  // e(O, .) = 1: skip the pair
+    const bool fin = jac_to_aff(a, acc);  // pair-uniform
+    uint32_t* o = part + RLC_WIN_OFF + RLC_WIN_WORDS * w;
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+        o[NL * h + k] = fin ? a.x.c.v[k] : 0u;
+        o[2 * NL + NL * h + k] = fin ? a.y.c.v[k] : 0u;
+    }
+    if (!h) o[4 * NL] = fin ? 0u : 1u;  // e(O, .) = 1: the finish skips the pair
 }
 
 // P_w = (256^w) g~ from g~'s fixed-base table (base index q of the verkey tables); G is g~'s field
 template <class G>
 __global__ __launch_bounds__(64) void k_fold_fixed(int q, const uint32_t* __restrict__ table, int wbits,
-                                                   const uint32_t* __restrict__ binf, uint32_t* __restrict__ prep2,
+                                                   const uint32_t* __restrict__ binf, uint32_t* __restrict__ pw,
                                                    uint8_t* __restrict__ fixed_inf) {
     const int w = threadIdx.x;
     if (w >= FW) return;
@@ -318,7 +327,7 @@ __global__ __launch_bounds__(64) void k_fold_fixed(int q, const uint32_t* __rest
     Aff<G> a;
     const bool fin = jac_to_aff(a, acc);
     fixed_inf[w] = fin ? 0 : 1;
-    const Soa S{prep2, FW};
+    const Soa S{pw, FW};
     if constexpr (sizeof(G) == sizeof(Fp)) st_as_p(S, w, a);  // SigG2: g~ in G1
     else st_as_q(S, w, a);                                     // SigG1: g~ in G2
 }
@@ -353,25 +362,26 @@ size_t cck_fold_words(int mode, size_t n) {
 
 int cck_fold_pseudo() { return FW; }
 
-// mode 0 (SigG2): X_i in G2 (AoS affine, 48 words), g~ in G1; mode 1: X_i in G1 (24 words), g~ in G2.
-// d_dig: [FW][n] int8 digits (0 for credentials to leave out).  fixed_ok = 0 recomputes P_w into
-// d_prep2 and their identity flags into d_finf (FW bytes); both persist between calls.
-// d_prep2: PREP_SLOTS x FW SoA; d_flags2: FW words (pair-0 skip flags of the pseudo-credentials),
-// both written by cck_fold_window, which the host launches after this.
-int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, int fixed_ok, int q,
-             const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_prep2, uint8_t* d_finf,
-             uint32_t* d_flags2, hipStream_t st) {
+// P_w = (256^w) g~, w < 16, from the verkey tables (g~ = base q): d_pw (PREP_SLOTS x FW SoA, soa.h:
+// SigG2 the P side in evaluation form (x, y, 1), SigG1 the Q side) and their identity flags d_finf
+// (FW bytes); once per verkey (cc_set_verkey), read by every finish
+int cck_fold_fixed(int mode, int q, const uint32_t* d_table, int wbits, const uint32_t* d_binf, uint32_t* d_pw,
+                   uint8_t* d_finf, hipStream_t st) {
+    if (mode == 0)
+        hipLaunchKernelGGL(k_fold_fixed<Fp>, dim3(1), dim3(64), 0, st, q, d_table, wbits, d_binf, d_pw, d_finf);
+    else
+        hipLaunchKernelGGL(k_fold_fixed<Fp2>, dim3(1), dim3(64), 0, st, q, d_table, wbits, d_binf, d_pw, d_finf);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// mode 0 (SigG2): X_i in G2 (AoS affine, 48 words); mode 1: X_i in G1 (24 words).
+// d_dig: [FW][n] int8 digits (0 for credentials to leave out).  The bucket sums; cck_fold_window, which
+// the host launches after this, forms the window sums.
+int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uint32_t* d_work, hipStream_t st) {
     if (!n) return -1;
     const size_t mc = fold_maxchunks(n);
     const FoldWork fw = fold_work(mode, n, d_work);
     uint32_t *cnt = fw.cnt, *off = fw.off, *cur = fw.cur, *list = fw.list, *part = fw.part, *bkt = fw.bkt;
-    uint8_t* finf = d_finf;
-    if (!fixed_ok) {
-        if (mode == 0)
-            hipLaunchKernelGGL(k_fold_fixed<Fp>, dim3(1), dim3(64), 0, st, q, d_table, wbits, d_binf, d_prep2, finf);
-        else
-            hipLaunchKernelGGL(k_fold_fixed<Fp2>, dim3(1), dim3(64), 0, st, q, d_table, wbits, d_binf, d_prep2, finf);
-    }
     if (hipMemsetAsync(cnt, 0, FB * 4, st) != hipSuccess || hipMemsetAsync(list, 0xff, mc * FS * 4, st) != hipSuccess)
         return -1;
     const dim3 gw(nblocks(n, 256) < 64 ? nblocks(n, 256) : 64, FW);
@@ -389,15 +399,14 @@ int cck_fold(int mode, size_t n, const int8_t* d_dig, const uint32_t* d_pts, uin
 }
 
 // the fold's last step, after cck_fold (16 waves, latency-bound: the host runs it beside other
-// work): the window sums S_w and the pseudo-credentials' prep SoA and flags
-int cck_fold_window(int mode, size_t n, uint32_t* d_work, const uint8_t* d_finf, uint32_t* d_prep2,
-                    uint32_t* d_flags2, hipStream_t st) {
+// work): the window sums S_w into the partial's window section (rlc_part.h)
+int cck_fold_window(int mode, size_t n, uint32_t* d_work, uint32_t* d_partial, hipStream_t st) {
     if (!n) return -1;
     uint32_t* bkt = fold_work(mode, n, d_work).bkt;
     if (mode == 0)
-        hipLaunchKernelGGL(k_fold_window_g2pl, dim3(FW), dim3(64), 0, st, bkt, d_finf, d_prep2, d_flags2);
+        hipLaunchKernelGGL(k_fold_window_g2pl, dim3(FW), dim3(64), 0, st, bkt, d_partial);
     else
-        hipLaunchKernelGGL(k_fold_window, dim3(FW), dim3(64), 0, st, bkt, d_finf, d_prep2, d_flags2);
+        hipLaunchKernelGGL(k_fold_window, dim3(FW), dim3(64), 0, st, bkt, d_partial);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

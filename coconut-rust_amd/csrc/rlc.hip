@@ -19,13 +19,16 @@
 //                                         (delta X + sum (delta m_j) Y_j) of pair 0 in the Miller
 //                                         kernels' SoA layout (soa.h)
 //   k_f12_reduce                        : one level of the pairwise product tree of Fp12 values
-//   k_rlc_partial_out / k_rlc_combine   : 145-word partial (Fp12 Montgomery words + identity flag),
-//                                         and the product of gathered partials ahead of k_fexp
+//   k_rlc_partial_out                   : the partial's product and flag words (rlc_part.h; the fold
+//                                         writes its window section)
+//   k_rlc_gather                        : the finish's inputs from the gathered partials: their products
+//                                         and every shard's window pairs (S_w, P_w) for k_miller_wide
 #include "codec.h"
 #include "curve_pl.h"
 #include "fixed.h"
 #include "fr.h"
 #include "pairing.h"
+#include "rlc_part.h"
 #include "soa.h"
 #include "subgroup.h"
 
@@ -241,56 +244,65 @@ __global__ __launch_bounds__(256) void k_f12_reduce(size_t n_in, const uint32_t*
     pl::st_f12(O, t, a);
 }
 
-// 145-word partial: the batch's Miller product (one element, Montgomery words in slot order) and
-// the identity flag (any sigma = O in the batch)
+// the partial's product and flag words: the batch's Miller product (one element, Montgomery words in
+// slot order) and the fall-back flag (any sigma = O or outside the subgroup, or a bad verkey)
 __global__ void k_rlc_partial_out(const uint32_t* __restrict__ f1, const uint32_t* __restrict__ any,
                                   uint32_t* __restrict__ partial) {
     const int t = threadIdx.x;
-    if (t < 144) partial[t] = f1[t];
-    if (t == 144) partial[t] = *any ? 1u : 0u;
+    if (t < RLC_F12_WORDS) partial[t] = f1[t];
+    if (t == RLC_FLAG) partial[t] = *any ? 1u : 0u;
 }
 
-// product of k gathered partials -> fbuf (n = 1) and flags[0] (bit0 set if any part is flagged)
-__global__ void k_rlc_combine(size_t k, const uint32_t* __restrict__ parts, uint32_t* __restrict__ f1,
-                              uint32_t* __restrict__ flag) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    Fp12 acc;
-    uint32_t* w = reinterpret_cast<uint32_t*>(&acc);
-    for (int j = 0; j < 144; j++) w[j] = parts[j];
-    uint32_t fl = parts[144];
-    for (size_t p = 1; p < k; p++) {
-        Fp12 x;
-        uint32_t* v = reinterpret_cast<uint32_t*>(&x);
-        for (int j = 0; j < 144; j++) v[j] = parts[p * 145 + j];
-        fl |= parts[p * 145 + 144];
-        f12_mul(acc, acc, x);
+// The finish's inputs from k gathered partials (stride RLC_PART_WORDS), one block per partial r:
+//   fw element r (SoA stride fs)         : partial r's Miller product
+//   window pair e = 16 r + w (prep SoA of stride 16 k, soa.h slots; k_miller_wide's operands): S_w of
+//                                          partial r with P_w = (256^w) g~ (pw: SoA stride 16, finf: its
+//                                          identity flags); flags2[e] bit 0 skips it (S_w = O or P_w = O)
+//   flag (block 0)                       : OR of the partials' fall-back flags
+// SigG2: S_w in G2 is the Q side, P_w (G1, evaluation form (x, y, 1)) the P side; SigG1 the reverse.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rlc_gather(size_t k, const uint32_t* __restrict__ parts,
+                                                    const uint32_t* __restrict__ pw, const uint8_t* __restrict__ finf,
+                                                    uint32_t* __restrict__ fw, size_t fs, uint32_t* __restrict__ prep,
+                                                    uint32_t* __restrict__ flags2, uint32_t* __restrict__ flag) {
+    const size_t r = blockIdx.x;
+    const int t = threadIdx.x;
+    const uint32_t* P = parts + r * RLC_PART_WORDS;
+    if (t < RLC_F12_WORDS) fw[(size_t)t * fs + r] = P[t];
+    if (t >= RLC_F12_WORDS && t < RLC_F12_WORDS + RLC_WINDOWS) {
+        const int w = t - RLC_F12_WORDS;
+        const size_t e = RLC_WINDOWS * r + w;
+        const uint32_t* win = P + RLC_WIN_OFF + RLC_WIN_WORDS * w;
+        const Soa S{prep, RLC_WINDOWS * k}, W{const_cast<uint32_t*>(pw), (size_t)RLC_WINDOWS};
+        Fp v[4];
+        for (int j = 0; j < 4; j++)
+            for (int l = 0; l < NL; l++) v[j].v[l] = win[NL * j + l];
+        if (MODE == 0) {  // S_w: affine G2 as Q; P_w: G1 in evaluation form as P
+            for (int j = 0; j < 4; j++) st_fp(S, S_Q1 + j, e, v[j]);
+            for (int j = 0; j < 3; j++) {
+                Fp x;
+                ld_fp(x, W, S_P1 + j, w);
+                st_fp(S, S_P1 + j, e, x);
+            }
+        } else {  // S_w: G1 (x, y, 1) as P; P_w: affine G2 as Q
+            Fp one;
+            fp_one(one);
+            st_fp(S, S_P1, e, v[0]);
+            st_fp(S, S_P1 + 1, e, v[1]);
+            st_fp(S, S_P1 + 2, e, one);
+            for (int j = 0; j < 4; j++) {
+                Fp x;
+                ld_fp(x, W, S_Q1 + j, w);
+                st_fp(S, S_Q1 + j, e, x);
+            }
+        }
+        flags2[e] = (win[4 * NL] || finf[w]) ? 1u : 0u;
     }
-    for (int j = 0; j < 144; j++) f1[j] = w[j];
-    *flag = fl ? 1u : 0u;
-}
-
-// The fold's 16 window pairs (fold.hip: pseudo-credential w's pair 0 in prep2, stride FW, and its skip
-// flag) appended as credentials n .. n + 15 of the twin layout, so the credentials' two-per-loop Miller
-// launch runs them too (no separate launch for 16 pairs on the critical path)
-__global__ void k_rlc_append(size_t n, size_t ps, int nps, const uint32_t* __restrict__ prep2,
-                             const uint32_t* __restrict__ flags2, uint32_t* __restrict__ prep,
-                             uint32_t* __restrict__ flags) {
-    const int w = threadIdx.x;
-    if (w >= nps) return;
-    const size_t c = n + (size_t)w;
-    const Soa S{prep, ps}, S2{const_cast<uint32_t*>(prep2), (size_t)nps};
-    const int q = twin_slot(S_Q1, S_Q2, c), p = twin_slot(S_P1, S_P2, c);
-    for (int k = 0; k < 4; k++) {
-        Fp v;
-        ld_fp(v, S2, S_Q1 + k, w);
-        st_fp(S, q + k, c >> 1, v);
+    if (r == 0 && t == 255) {
+        uint32_t fl = 0;
+        for (size_t p = 0; p < k; p++) fl |= parts[p * RLC_PART_WORDS + RLC_FLAG];
+        *flag = fl ? 1u : 0u;
     }
-    for (int k = 0; k < 3; k++) {
-        Fp v;
-        ld_fp(v, S2, S_P1 + k, w);
-        st_fp(S, p + k, c >> 1, v);
-    }
-    flags[c] = flags2[w] ? 1u : 0u;  // bit0: skip the pair
 }
 
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
@@ -298,7 +310,7 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 extern "C" {
 
 // d_pts: n fold points (AoS affine: 48 words SigG2, 24 SigG1); d_dig: 16 x n digit bytes; ps: the prep
-// SoA's stride (>= (n + 16 + 1) / 2: the fold's window pairs are appended, k_rlc_append).
+// SoA's stride (>= (n + 1) / 2: credentials 2t and 2t + 1 share Miller loop t, twin_slot).
 // part 0: decode + subgroup checks + the fold's inputs; part 1: the delta-scaled MSM
 int cck_prep_rlc(int mode, int part, size_t n, size_t ps, int q, uint64_t base_index, const uint32_t* d_key,
                  const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs, const uint32_t* d_table, int wbits,
@@ -324,8 +336,8 @@ int cck_prep_rlc(int mode, int part, size_t n, size_t ps, int q, uint64_t base_i
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// reduce n SoA Fp12 values in `a` to one, ping-ponging with `b` (each >= n * 144 words);
-// writes the 145-word partial
+// reduce n SoA Fp12 values in `a` to one, ping-ponging with `b` (`a` n, `b` (n + 1) / 2 elements of
+// 144 words); writes the partial's product and flag words (rlc_part.h)
 int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any, uint32_t* d_partial,
                    hipStream_t st) {
     if (!n) return -1;
@@ -342,14 +354,20 @@ int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int cck_rlc_append(size_t n, size_t ps, int nps, const uint32_t* d_prep2, const uint32_t* d_flags2, uint32_t* d_prep,
-                   uint32_t* d_flags, hipStream_t st) {
-    hipLaunchKernelGGL(k_rlc_append, dim3(1), dim3(64), 0, st, n, ps, nps, d_prep2, d_flags2, d_prep, d_flags);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
+int cck_rlc_partial_words() { return RLC_PART_WORDS; }
 
-int cck_rlc_combine(size_t k, const uint32_t* d_parts, uint32_t* d_f1, uint32_t* d_flag, hipStream_t st) {
-    hipLaunchKernelGGL(k_rlc_combine, dim3(1), dim3(64), 0, st, k, d_parts, d_f1, d_flag);
+// the finish's inputs (k_rlc_gather): d_fw >= 17 k Fp12 elements of stride fs (partial products at
+// 0 .. k-1; k_miller_wide's window values go to k .. 17 k - 1), d_prep a 16 k-element prep SoA,
+// d_flags2 16 k words, d_flag one word
+int cck_rlc_gather(int mode, size_t k, const uint32_t* d_parts, const uint32_t* d_pw, const uint8_t* d_finf,
+                   uint32_t* d_fw, size_t fs, uint32_t* d_prep, uint32_t* d_flags2, uint32_t* d_flag, hipStream_t st) {
+    if (!k || fs < (RLC_WINDOWS + 1) * k) return -1;
+    if (mode == 0)
+        hipLaunchKernelGGL(k_rlc_gather<0>, dim3((unsigned)k), dim3(256), 0, st, k, d_parts, d_pw, d_finf, d_fw, fs,
+                           d_prep, d_flags2, d_flag);
+    else
+        hipLaunchKernelGGL(k_rlc_gather<1>, dim3((unsigned)k), dim3(256), 0, st, k, d_parts, d_pw, d_finf, d_fw, fs,
+                           d_prep, d_flags2, d_flag);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

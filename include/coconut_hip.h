@@ -27,7 +27,7 @@
  * A context made by cc_ctx_create_multi spans a device set (one single-device context and one RCCL
  * communicator per GPU, one host thread per GPU during a call): cc_set_params / cc_set_verkey apply
  * to every device and cc_verify_batch shards the batch by credential over the set (RLC mode: one
- * ncclAllGather of 580-byte partials over xGMI); the other entry points run on the
+ * ncclAllGather of 3,716-byte partials over xGMI); the other entry points run on the
  * set's first device.
  * Streams: the *_device entry points take a caller stream; the library orders it against the
  * context's own stream (which the host entry points use) with events at entry and exit, so calls on
@@ -75,10 +75,11 @@ cc_status cc_ctx_mode(const cc_ctx* ctx, int* mode_out);
 cc_status cc_set_params(cc_ctx* ctx, const uint8_t* g_tilde);
 
 /* Shared verkey (X~, Y~[q]) for cc_verify_batch with vk == NULL: builds fixed-base tables on the
- * device (one-time cost, reported separately from batch throughput): the widest of 22 / 20 / 16-bit
- * windows whose q + 2 bases' tables fit 40 % of the free HBM (at most 96 GiB), else 8-bit windows.
- * On any failure the
- * context is left WITHOUT a verkey (verify / RLC / PoK calls then return CC_ERR_STATE). */
+ * device (one-time cost, reported separately from batch throughput): the widest of 22 / 20 / 18 / 16 /
+ * 14 / 12 / 10-bit windows whose q + 2 bases' tables fit 4 GiB and 40 % of the free HBM, else 8-bit
+ * windows (cc_set_table_bits forces a width).  The same verkey again (bytes and width unchanged) is a
+ * no-op.  On any failure the context is left WITHOUT a verkey (verify / RLC / PoK calls then return
+ * CC_ERR_STATE). */
 cc_status cc_set_verkey(cc_ctx* ctx, const uint8_t* X, const uint8_t* Y, size_t q);
 
 /* Window widths of the fixed-base tables built by later cc_set_verkey / cc_set_issuers calls:
@@ -117,23 +118,28 @@ cc_status cc_verify_batch_pervk_device(cc_ctx* ctx, size_t n, size_t q, const ui
                                        const uint8_t* d_vk_Y, uint8_t* d_verdicts, uint8_t* d_gt_or_null,
                                        void* stream);
 
-/* RLC batch mode, multi-GPU form.  Each GPU reduces its shard to one 145-word
- * partial (Fp12 Miller product in the library's Montgomery words + an identity flag); the caller
- * gathers the partials of all GPUs (RCCL all-gather over xGMI, or any transport) and every GPU
- * finishes with ONE final exponentiation:
+/* RLC batch mode, multi-GPU form.  Each GPU reduces its shard to one partial of
+ * CC_RLC_PARTIAL_WORDS u32 (= cc_rlc_partial_words(): the Fp12 Miller product in the library's
+ * Montgomery words, a fall-back flag, and the shard's 16 fold window sums, affine with identity
+ * flags); the caller gathers the partials of all GPUs (RCCL all-gather over xGMI, or any transport)
+ * and every GPU finishes with 16 window pairs per partial and ONE final exponentiation:
  *   cc_rlc_partial_device: deltas = ChaCha20(seed32, base_index + i), i < n (shared verkey only);
- *                          d_partial: 145 x u32 device buffer; n = 0 (an empty shard) writes the
- *                          neutral partial (Fp12 one, flag clear) so the rank still joins the gather.
- *   cc_rlc_finish_device : product of nparts partials (nparts x 145 u32, device), final
- *                          exponentiation; *d_accept = 1 iff the whole batch verifies (then every
- *                          per-credential verdict is 1); 0 means "fall back to per-credential
- *                          verification" (a bad or identity credential somewhere).  d_gt optional
- *                          (576 B, GT of the combined product).
+ *                          d_partial: CC_RLC_PARTIAL_WORDS x u32 device buffer; n = 0 (an empty
+ *                          shard) writes the neutral partial (Fp12 one, flag clear, identity window
+ *                          sums) so the rank still joins the gather.
+ *   cc_rlc_finish_device : nparts partials (nparts x CC_RLC_PARTIAL_WORDS u32, device): their window
+ *                          pairs, the product, the final exponentiation; *d_accept = 1 iff the whole
+ *                          batch verifies (then every per-credential verdict is 1); 0 means "fall back
+ *                          to per-credential verification" (a bad or identity credential somewhere).
+ *                          d_gt optional (576 B, GT of the combined product).  Needs the verkey of the
+ *                          partials (its g~ multiples); a cc_set_verkey waits for running finishes.
  * Both are asynchronous on `stream` (NULL: the context stream).  The partial is ordered against the
  * context's other work; the finish owns its buffers and is NOT, so on a second stream it may overlap
  * the next batch's partial (the caller orders d_partials before it, and two finishes of one context
  * one after the other).  cc_verify_batch(..., rlc = 1) runs the single-GPU form with a fresh seed
  * from /dev/urandom and falls back by itself. */
+#define CC_RLC_PARTIAL_WORDS 929
+int cc_rlc_partial_words(void);
 cc_status cc_rlc_partial_device(cc_ctx* ctx, size_t n, size_t q, uint64_t base_index, const uint8_t* seed32,
                                 const uint8_t* d_sigma1, const uint8_t* d_sigma2, const uint8_t* d_msgs,
                                 uint32_t* d_partial, void* stream);

@@ -1,5 +1,5 @@
 """One rank of tests/test_gpu_dist.py (started as a child process BEFORE it touches the GPU): builds
-a DeviceEngine on GPU 0 over its half of a q = 16 batch, all-gathers the real 145-word RLC partials
+a DeviceEngine on GPU 0 over its half of a q = 16 batch, all-gathers the real 929-word RLC partials
 over gloo (host memory), finishes with one final exponentiation, falls back per credential on
 reject, and writes its verdicts + fallback flag to <out>/r<rank>.npy.
 

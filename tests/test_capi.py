@@ -40,6 +40,15 @@ def test_status_strings_and_version():
     assert b"gfx950" in lib.cc_version()
 
 
+def test_rlc_partial_size_agrees_with_the_python_side():
+    """The partial's size (rlc_part.h: Fp12 product, flag, 16 window sums) as the library exports it is the
+    one coconut/dist.py gathers and the header declares."""
+    from coconut._lib import lib
+    from coconut.dist import PARTIAL_WORDS
+    hdr = open(os.path.join(ROOT, "include", "coconut_hip.h")).read()
+    assert lib.cc_rlc_partial_words() == PARTIAL_WORDS == int(re.search(r"CC_RLC_PARTIAL_WORDS (\d+)", hdr).group(1))
+
+
 def test_null_and_bad_arguments_rejected_without_gpu():
     from coconut._lib import lib
     assert lib.cc_ctx_create(0, 7, None) == -4        # bad mode / null out

@@ -1,7 +1,7 @@
 """Multi-rank control flow of coconut/dist.py on CPU: world_size 2 over the gloo backend.
 
 The device engine is replaced by a CPU engine whose per-credential verdicts come from the C oracle
-(test infrastructure) and whose 145-word partial carries the shard's "not all valid" flag, so these
+(test infrastructure) and whose PARTIAL_WORDS-word partial carries the shard's "not all valid" flag, so these
 tests exercise exactly the production sharding, all-gather and collective accept/fallback logic
 (`verify_sharded`, `rlc_accept`, `gather_partials`) without a GPU.  The GPU form of the same flow
 (real partials, one final exponentiation) is tests/test_gpu_parity.py::test_rlc_partials_*.
@@ -50,15 +50,16 @@ class OracleEngine:
         self.fell_back = False
 
     def partial(self):
-        from coconut.dist import PARTIAL_WORDS
+        from coconut.dist import PARTIAL_FLAG, PARTIAL_WORDS
         t = torch.zeros(PARTIAL_WORDS, dtype=torch.int32)
-        t[:self.n] = torch.from_numpy(self._v.astype(np.int32))[:PARTIAL_WORDS - 1]
-        t[PARTIAL_WORDS - 1] = 0 if self._v.all() else 1
+        t[:self.n] = torch.from_numpy(self._v.astype(np.int32))[:PARTIAL_FLAG]
+        t[PARTIAL_FLAG] = 0 if self._v.all() else 1
         return t
 
     def finish(self, allp, k):
-        assert tuple(allp.shape) == (k, 145)
-        return bool((allp[:, 144] == 0).all())
+        from coconut.dist import PARTIAL_FLAG, PARTIAL_WORDS
+        assert tuple(allp.shape) == (k, PARTIAL_WORDS)
+        return bool((allp[:, PARTIAL_FLAG] == 0).all())
 
     def per_credential(self):
         self.fell_back = True

@@ -1,6 +1,6 @@
 """The multi-process RLC path on a real GPU: two rank
 processes, started as children BEFORE either touches the GPU, each drive a DeviceEngine on GPU 0 over
-half of a q = 16 batch, all-gather the REAL 145-word partials over gloo (host memory: one box has
+half of a q = 16 batch, all-gather the REAL 929-word partials over gloo (host memory: one box has
 one GPU, so RCCL over xGMI between two GPUs is unmeasured on hardware here), and finish with one final
 exponentiation each.  Valid batch: both ranks accept.  One swapped sigma_2 in rank 1's slice: both
 ranks reject (one gathered decision) and the per-credential fallback verdicts equal construction."""
