@@ -178,10 +178,11 @@ DEV JG jg_add_aff(const JG& p, const AG& q) {
     const auto i = smul<4>(hh);
     const auto j = mulr1(h, i);
     const auto v = mulr1(p.x, i);
-    const auto X3 = sub(sub(sqrr1(rr), j), add(v, v));
-    const auto Y3 = sub(mulr1(rr, sub(v, X3)), smul<2>(mulr1(p.y, j)));
+    const FR X3 = reduce(sub(sub(sqrr1(rr), j), add(v, v)));
+    // Y3 = rr (v - X3) - 2 y j = 2 (r0 (v - X3) - y j): both products under one reduction
+    const auto Y3 = smul<2>(mul2(r0, sub(v, X3), neg(p.y), j));
     const auto Z3 = sub(sub(sqrr1(add(p.z, h)), z1z1), hh);
-    return {reduce(X3), reduce(Y3), reduce(Z3)};
+    return {X3, reduce(Y3), reduce(Z3)};
 }
 
 // add-2007-bl: general Jacobian addition with the exceptional cases
@@ -201,10 +202,10 @@ DEV JG jg_add(const JG& p, const JG& q) {
     const auto i = sqrr1(add(h, h));
     const auto j = mulr1(h, i);
     const auto v = mulr1(u1, i);
-    const auto X3 = sub(sub(sqrr1(rr), j), add(v, v));
-    const auto Y3 = sub(mulr1(rr, sub(v, X3)), smul<2>(mulr1(s1, j)));
+    const FR X3 = reduce(sub(sub(sqrr1(rr), j), add(v, v)));
+    const auto Y3 = smul<2>(mul2(r0, sub(v, X3), neg(s1), j));  // 2 (r0 (v - X3) - s1 j), one reduction
     const auto Z3 = mulr1(sub(sub(sqrr1(add(p.z, q.z)), z1z1), z2z2), h);
-    return {reduce(X3), reduce(Y3), reduce(Z3)};
+    return {X3, reduce(Y3), reduce(Z3)};
 }
 
 // storage form (curve.h Jac<Fp>, canonical, R = 2^406) <-> lazy R' form

@@ -123,6 +123,7 @@ DEV W14 lz_mont(const int32_t a[LN], const int32_t b[LN], const int32_t c[LN], c
     return r;
 }
 
+
 // a^2 / R' mod p for a one-lane value: product scanning over the upper triangle only (column k:
 // sum over i < j of (2 a_i) a_j, plus a_{k/2}^2), 105 product mads instead of 196.  Column bound: at
 // most 7 doubled cross terms and one square, 15 A^2 2^40 in all, so A^2 <= 498,000 (AMAX1S).
@@ -282,6 +283,24 @@ static __device__ __noinline__ W14 lz_sqr1_call(LZ_L14(a)) {
     return lz_sqr1(A);
 }
 DEV W14 lz_sqr1_c(const W14& x) { return lz_sqr1_call(LZ_E14(x)); }
+// a wave-uniform false the compiler cannot see through (field.h cc_opaque_false)
+DEV bool lz_opaque_false() {
+    uint32_t x;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(x));
+    return x != 0;
+}
+// a sum of two one-lane products under one reduction (the G1 point formulas' Y3), inlined: as a call
+// the four 14-limb operands exceed the 32 argument registers and would pass through scratch (the
+// pair-lane Fp2 form of the same sum, measured: more scratch in the G2 kernels, slower)
+DEV W14 lz_mul2_c(W14 x, W14 y, W14 z, W14 w) {
+    W14 r;
+    do {
+#pragma unroll
+        for (int k = 0; k < LN; k++) asm volatile("" : "+v"(x.v[k]), "+v"(y.v[k]), "+v"(z.v[k]), "+v"(w.v[k]));
+        r = lz_mont<2>(x.v, y.v, z.v, w.v);
+    } while (lz_opaque_false());
+    return r;
+}
 
 template <int A, int B>
 DEV W14 w14(const Fq<A, B>& x) {
@@ -581,12 +600,6 @@ DEV F2<AN, bprod(4LL * B * B)> sqr(const F2<A, B>& x) {
     static_assert(4LL * A * A <= AMAX, "f2 sqr: limb bound");
     return {fq<bprod(4LL * B * B)>(lz_f2_sqr_c(w14(x.c)))};
 }
-// a wave-uniform false the compiler cannot see through (field.h cc_opaque_false)
-DEV bool lz_opaque_false() {
-    uint32_t x;
-    asm volatile("s_mov_b32 %0, 0" : "=s"(x));
-    return x != 0;
-}
 // x^2 with the multiplication inlined (its own basic block): for small hot loops whose whole body then
 // runs without call boundaries (no values saved around calls)
 template <int A, int B>
@@ -610,6 +623,13 @@ template <int A1, int B1, int A2, int B2>
 DEV Fq<AN, bprod((long long)B1 * B2)> mul(const Fq<A1, B1>& x, const Fq<A2, B2>& y) {
     static_assert((long long)A1 * A2 <= AMAX, "fp mul: limb bound");
     return fq<bprod((long long)B1 * B2)>(lz_mul_c(w14(x), w14(y)));
+}
+// one-lane x y + z w, one reduction for both products
+template <int A1, int B1, int A2, int B2, int A3, int B3, int A4, int B4>
+DEV Fq<AN, bprod((long long)B1 * B2 + (long long)B3 * B4)> mul2(const Fq<A1, B1>& x, const Fq<A2, B2>& y,
+                                                               const Fq<A3, B3>& z, const Fq<A4, B4>& w) {
+    static_assert((long long)A1 * A2 + (long long)A3 * A4 <= AMAX, "fp mul2: limb bound");
+    return fq<bprod((long long)B1 * B2 + (long long)B3 * B4)>(lz_mul2_c(w14(x), w14(y), w14(z), w14(w)));
 }
 // one-lane x^2 (upper-triangle product scanning)
 template <int A, int B>
