@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_split(size_t n, int q, int 
                 FT<FO>::neg(Ta.y, Ta.y);
                 jac_add_aff(acc, acc, Ta);
             }
-            // J' = X~ + J + sum_revealed Y~_i m_i; P1 = J' in line-evaluation form (X Z, Y, Z^3)
+            // J' = X~ + J + sum_revealed Y~_i m_i; P1 = J' affine in the R' form (the Miller loop's kAffRp)
             Jac<FO> jp;
             if (Xinf) {
                 jac_set_inf(jp);
@@ -476,15 +476,14 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_split(size_t n, int q, int 
                 const int h = (int)rev_idx[z];
                 if (!binf[h]) ft_add_lz(lj, m.v, table, wbits, h, 0, nwin);
             }
-            jp = lz::jg_to(lj);
-            if (jac_is_inf(jp)) fl |= 4u;
-            Fp t;
-            fp_mul(t, jp.x, jp.z);
-            st_fp(S, S_P1, i, t);
-            st_fp(S, S_P1 + 1, i, jp.y);
-            fp_sqr(t, jp.z);
-            fp_mul(t, t, jp.z);
-            st_fp(S, S_P1 + 2, i, t);
+            if (lz::jg_is_inf(lj)) {
+                fl |= 4u;
+            } else {
+                Fp x, y;
+                lz::jg_to_aff_rp(x, y, lj);
+                st_fp(S, S_P1, i, x);
+                st_fp(S, S_P1 + 1, i, y);
+            }
         }
     }
     if (roleB) {

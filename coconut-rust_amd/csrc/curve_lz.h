@@ -208,6 +208,16 @@ DEV JG jg_add(const JG& p, const JG& q) {
     return {X3, reduce(Y3), reduce(Z3)};
 }
 
+// p (not the identity) -> affine (x, y) in the R' form, canonical 12 x 32 words: the Miller loop's
+// affine-R' operand (miller_lz.hip: its line's l0 needs no product, no Z to load).  One inversion
+// (field.h divsteps) and four products.
+DEV void jg_to_aff_rp(Fp& x, Fp& y, const JG& p) {
+    const auto zi = inv(p.z);
+    const auto zi2 = sqrr1(zi);
+    x = canon(mulr1(p.x, zi2));
+    y = canon(mulr1(p.y, mulr1(zi2, zi)));
+}
+
 // storage form (curve.h Jac<Fp>, canonical, R = 2^406) <-> lazy R' form
 DEV JG jg_from(const Jac<Fp>& a) { return {reduce(in_r(a.x)), reduce(in_r(a.y)), reduce(in_r(a.z))}; }
 DEV Jac<Fp> jg_to(const JG& a) { return {out_r(a.x), out_r(a.y), out_r(a.z)}; }

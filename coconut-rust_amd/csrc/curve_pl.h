@@ -97,7 +97,7 @@ DEV bool miller_t_in_subgroup(const G2Proj& T, const Aff<Fp2>& q) {
 // x.a | x.b | y.a | y.b, 12 words each; the verkey and issuer tables, k_table_fill): each lane loads its
 // own halves, the sum runs on the lazy pair-lane field (curve_lz.h)
 DEV void ft_add_g2_lz(lz::JL& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j,
-                      int w0, int w1) {
+                      int w0, int w1, bool negate = false) {  // negate: acc -= k B_j
     constexpr int EW = sizeof(cc::Aff<cc::Fp2>) / 4;
     const int h = (int)half_id();
     const size_t went = ft_went(wbits);
@@ -116,7 +116,8 @@ DEV void ft_add_g2_lz(lz::JL& acc, const uint32_t k[8], const uint32_t* __restri
             o |= x.v[c] | y.v[c];
         }
         if (pair_all(o == 0)) continue;  // (0, 0): an identity entry
-        acc = lz::jl_add_aff_c(acc, lz::F2<lz::AN, lz::BC>{lz::from_fp(x)}, lz::F2<lz::AN, lz::BC>{lz::from_fp(y)});
+        const lz::F2<lz::AN, lz::BC> ly{lz::from_fp(y)};
+        acc = lz::jl_add_aff_c(acc, lz::F2<lz::AN, lz::BC>{lz::from_fp(x)}, negate ? lz::neg(ly) : ly);
     }
 }
 // storage-form (canonical, R = 2^406) pair-lane Jacobian points <-> the lazy field's (curve_lz.h)

@@ -58,7 +58,7 @@ DEV bool ft_is_empty(const Aff<F>& a) {
 // 12 x 32 words; k_table_fill rescales them), so the lazy G1 mixed addition (curve_lz.h) loads an
 // entry with shifts only.  acc += (k over windows [w0, w1)) * B_j on a lazy accumulator:
 DEV void ft_add_lz(lz::JG& acc, const uint32_t k[8], const uint32_t* __restrict__ table, int wbits, int j, int w0,
-                   int w1) {
+                   int w1, bool negate = false) {  // negate: acc -= k B_j
     constexpr int EW = sizeof(Aff<Fp>) / 4;
     const size_t went = ft_went(wbits);
     const uint32_t* tj = table + (size_t)j * ft_base_words<Fp>(wbits);
@@ -69,7 +69,8 @@ DEV void ft_add_lz(lz::JG& acc, const uint32_t k[8], const uint32_t* __restrict_
         Aff<Fp> e;
         ft_load<Fp>(e, tj + ((size_t)w * went + d - 1) * EW);
         if (ft_is_empty(e)) continue;
-        acc = lz::jg_add_aff(acc, lz::AG{lz::from_fp(e.x), lz::from_fp(e.y)});
+        const auto y = lz::from_fp(e.y);
+        acc = lz::jg_add_aff(acc, lz::AG{lz::from_fp(e.x), negate ? lz::neg(y) : y});
     }
 }
 

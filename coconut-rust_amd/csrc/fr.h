@@ -305,4 +305,18 @@ DEV void rlc_delta_signed(uint32_t d[NR], uint32_t dig[4], const uint32_t key[8]
     }
 }
 
+// delta's magnitude and sign from its canonical residue d: |delta| < 2^136 (16 signed base-256 digits),
+// so a residue with a nonzero word above bit 160 is r - |delta|.  delta X~ then runs over the
+// magnitude's windows only (8-byte scalar: 7 of 12 windows at 22 bits) with the table entries negated.
+DEV bool rlc_delta_abs(uint32_t a[NR], const uint32_t d[NR]) {
+    const bool neg = (d[5] | d[6] | d[7]) != 0;
+    uint32_t br = 0;
+#pragma unroll
+    for (int k = 0; k < NR; k++) {
+        const uint32_t t = __builtin_subc(rl(k), d[k], br, &br);
+        a[k] = neg ? t : d[k];
+    }
+    return neg;
+}
+
 }  // namespace cc

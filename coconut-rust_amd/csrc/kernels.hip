@@ -314,18 +314,14 @@ __global__ __launch_bounds__(256) void k_prep_sigg2_pair(size_t n, int q, const 
         o = t;
     }
     jac_add(pr, pr, o);  // (even half) + (odd half) on both lanes
-    if (jac_is_inf(pr)) fl |= 4u;
-    Fp t;
-    if (!h) {
-        fp_mul(t, pr.x, pr.z);
-        st_fp(S, S_P1, i, t);
-        st_fp(S, S_P1 + 1, i, pr.y);
-        flags[i] = fl;
-    } else {
-        fp_sqr(t, pr.z);
-        fp_mul(t, t, pr.z);
-        st_fp(S, S_P1 + 2, i, t);
+    if (jac_is_inf(pr)) {
+        fl |= 4u;
+    } else {  // pr affine in the R' form (the Miller loop's kAffRp operand): x on the even lane, y on the odd
+        Fp x, y;
+        lz::jg_to_aff_rp(x, y, lz::jg_from(pr));
+        st_fp(S, S_P1 + h, i, h ? y : x);
     }
+    if (!h) flags[i] = fl;
 }
 
 

@@ -12,7 +12,8 @@
 // Both group modes run one credential per lane PAIR, the layout the Miller loop and the shared-verkey
 // preps use:
 //   SigG2 (verkey in G1): lane h decodes sigma_{h+1} and runs the lazy one-lane G1 Straus over the
-//     bases Y~_j with j = h mod 2 (lane 0 also adds X~); the two partial sums meet by DPP.
+//     bases Y~_j with j = h mod 2 (lane 0 also adds X~); the two partial sums meet by DPP; pr is written
+//     affine in the R' form.
 //   SigG1 (verkey in G2): lane h decodes sigma_{h+1}; the pair runs the G2 Straus on the lazy pair-lane
 //     field over every Y~_j (straus_g2lz_pair) and adds X~.
 // The prep writes the SoA operands of kernels.hip's k_prep_*_pair, so k_miller / k_fexp finish.
@@ -80,18 +81,14 @@ __global__ __launch_bounds__(256, 2) void k_prep_sigg2_var(size_t n, int q, cons
         o = t;
     }
     jac_add(pr, pr, o);  // (even lane's sum) + (odd lane's sum), the same operand order on both lanes
-    if (jac_is_inf(pr)) fl |= 4u;
-    Fp t;
-    if (!h) {
-        fp_mul(t, pr.x, pr.z);
-        st_fp(S, S_P1, i, t);
-        st_fp(S, S_P1 + 1, i, pr.y);
-        flags[i] = fl;
-    } else {
-        fp_sqr(t, pr.z);
-        fp_mul(t, t, pr.z);
-        st_fp(S, S_P1 + 2, i, t);
+    if (jac_is_inf(pr)) {
+        fl |= 4u;
+    } else {  // affine in the R' form (the Miller loop's kAffRp operand): x on the even lane, y on the odd
+        Fp x, y;
+        lz::jg_to_aff_rp(x, y, lz::jg_from(pr));
+        st_fp(S, S_P1 + h, i, h ? y : x);
     }
+    if (!h) flags[i] = fl;
 }
 
 // SigG1, per-credential verkey (G2 bases on the lazy pair-lane field), one credential per lane pair

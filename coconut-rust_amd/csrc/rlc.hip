@@ -17,7 +17,7 @@
 //   k_rlc_check_* / k_rlc_msm_*        : decode, subgroup checks and the fold's inputs (-sigma_2,
 //                                         delta's digits); the delta-scaled fixed-base MSM
 //                                         (delta X + sum (delta m_j) Y_j) of pair 0 in the Miller
-//                                         kernels' SoA layout (soa.h)
+//                                         kernels' SoA layout (soa.h; G1 points affine in the R' form)
 //   k_f12_reduce                        : one level of the pairwise product tree of Fp12 values
 //   k_rlc_partial_out                   : the partial's product and flag words (rlc_part.h; the fold
 //                                         writes its window section)
@@ -36,17 +36,6 @@ using namespace cc;
 
 namespace {
 
-// G1 Jacobian -> line-evaluation form (X Z, Y, Z^3) in three SoA slots
-DEV void st_eval(const Soa& S, int slot, size_t i, const Jac<Fp>& P) {
-    Fp t;
-    fp_mul(t, P.x, P.z);
-    st_fp(S, slot, i, t);
-    st_fp(S, slot + 1, i, P.y);
-    fp_sqr(t, P.z);
-    fp_mul(t, t, P.z);
-    st_fp(S, slot + 2, i, t);
-}
-
 // The RLC keeps one pair per credential and runs two credentials per Miller loop (miller_lz.hip
 // kTwin): credential i's pair goes to SoA element i / 2 of the verify layout's pair-0 slots (even i)
 // or pair-1 slots (odd i), so the loop loads both pairs exactly as a verify loop does (coalesced).
@@ -58,8 +47,8 @@ DEV int twin_slot(int s0, int s1, size_t i) { return (i & 1) ? s1 : s0; }
 // flags: bit0 sigma_1 = O, bit1 sigma_2 = O, bit2 delta pr = O, bit5 sigma outside the subgroup.
 // Per credential: its Miller pair (sigma_1 with delta pr, SoA slots of soa.h, twin_slot), the fold
 // point X_i = -sigma_2,i (AoS affine, pts) and delta's 16 signed digits (dig[w * n + i]; all zero when
-// sigma_2 is the identity, which fails the batch anyway).  delta X~ runs over all windows: delta is
-// used mod r (fr.h rlc_delta_signed).
+// sigma_2 is the identity, which fails the batch anyway).  delta X~ runs as +-|delta| X~ over the
+// magnitude's windows (fr.h rlc_delta_abs); the products delta m_j use delta mod r.
 
 template <class F>
 DEV void st_aff_aos(uint32_t* p, const Aff<F>& a) {
@@ -138,7 +127,11 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, size_t ps, i
     rlc_delta_signed(d, w4, kk, base_index + i);
     lz::JG a = lz::jg_inf();  // the sum on the lazy field (fixed.h ft_add_lz)
     const int nwin = ft_nwin(wbits);
-    if (!binf[q + 1]) ft_add_lz(a, d, table, wbits, q + 1, 0, nwin);  // delta X~
+    if (!binf[q + 1]) {  // delta X~ as +-|delta| X~ (fr.h rlc_delta_abs)
+        uint32_t da[NR];
+        const bool neg = rlc_delta_abs(da, d);
+        ft_add_lz(a, da, table, wbits, q + 1, 0, nwin, neg);
+    }
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
@@ -147,9 +140,14 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg2(size_t n, size_t ps, i
         fr_mul_canon(dm, d, m.v);
         ft_add_lz(a, dm, table, wbits, j, 0, nwin);
     }
-    const Jac<Fp> acc = lz::jg_to(a);
-    if (jac_is_inf(acc)) flags[i] |= 4u;
-    st_eval(S, twin_slot(S_P1, S_P2, i), i >> 1, acc);
+    if (lz::jg_is_inf(a)) {
+        flags[i] |= 4u;
+    } else {  // affine in the R' form (the Miller loop's kAffRp operand)
+        Fp x, y;
+        lz::jg_to_aff_rp(x, y, a);
+        st_fp(S, twin_slot(S_P1, S_P2, i), i >> 1, x);
+        st_fp(S, twin_slot(S_P1, S_P2, i) + 1, i >> 1, y);
+    }
 }
 
 // one credential per lane pair: lane h decodes and subgroup-checks sigma_{h+1} (one-lane G1)
@@ -169,7 +167,9 @@ __global__ __launch_bounds__(256, 2) void k_rlc_check_sigg1(size_t n, size_t ps,
     Aff<Fp> a;
     if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
     else if (!g1_in_subgroup(a)) fl |= 32u;
-    if (!h) {
+    if (!h) {  // sigma_1 as the P side, affine in the R' form (the Miller loop's kAffRp operand)
+        fp_to_lazy_form(a.x);
+        fp_to_lazy_form(a.y);
         st_fp(S, twin_slot(S_P1, S_P2, i), i >> 1, a.x);
         st_fp(S, twin_slot(S_P1, S_P2, i) + 1, i >> 1, a.y);
     } else {
@@ -208,7 +208,11 @@ __global__ __launch_bounds__(256, 2) void k_rlc_msm_sigg1(size_t n, size_t ps, i
     rlc_delta_signed(d, w4, kk, base_index + i);
     lz::JL la = lz::jl_inf();  // the sum on the lazy pair-lane field (curve_pl.h ft_add_g2_lz)
     const int nwin = ft_nwin(wbits);
-    if (!binf[q + 1]) pl::ft_add_g2_lz(la, d, table, wbits, q + 1, 0, nwin);
+    if (!binf[q + 1]) {  // delta X~ as +-|delta| X~ (fr.h rlc_delta_abs)
+        uint32_t da[NR];
+        const bool neg = rlc_delta_abs(da, d);
+        pl::ft_add_g2_lz(la, da, table, wbits, q + 1, 0, nwin, neg);
+    }
     for (int j = 0; j < q; j++) {
         if (binf[j]) continue;
         Fr m;
