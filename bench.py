@@ -675,8 +675,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--backend", choices=["nccl", "gloo"], default=None,
                     help="torch.distributed backend for --gpus N (default nccl = RCCL; gloo: CPU skeleton tests)")
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=100)  # ~2.3 s timed at config 2: long enough to see from outside
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=0, help="credentials per GPU per step (0 = the config's size)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) rate")

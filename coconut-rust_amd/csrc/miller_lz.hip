@@ -3,22 +3,23 @@
 // reference src/lib.rs:13).  Replaces miller_pl.hip (same launchers, same SoA
 // inputs and outputs); one credential per PAIR of adjacent lanes as there.
 //
-//   SigG2: pair 0 = (sigma_1, pr); pair 1 = (-sigma_2, g~): g~ a constant.
-//   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2).
-//   Every G1 point (pr, g~, sigma) arrives affine in the lazy field's R' form (x R' mod p, canonical):
-//   a line's l2 x and l3 y come out unscaled and l0 needs no product.
+//   SigG2: pair 0 = (sigma_1, pr) with pr in Jacobian-evaluation form (XZ, Y, Z^3);
+//          pair 1 = (-sigma_2, g~): g~ affine constant.
+//   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2); sigma_1,
+//          -sigma_2 arrive in the lazy R' form (kAffRp: no product for l0).
 //   RLC mode keeps pair 0 of every credential (its second pairs are folded, fold.hip) and runs TWO
 //   credentials through the 2-pair loop (kTwin): the RLC only needs the product of the credentials'
 //   Miller values, and the shared squaring halves the Fp12 work per credential (5,696 Fp
 //   multiplications against 6,800 for a loop of its own).  The fold's 16 window pairs run in the
 //   wide one-wave form (fexp_pl.hip k_miller_wide).
 //
-// Representation boundary: the prep SoA holds the twist points as canonical 12 x 32 values in R =
-// 2^406 form, moved to R' form once (in_r: T's start and the addition steps' Q), and the G1 points in
-// R' form already (the preps' fp_to_lazy_form / curve_lz.h jg_to_aff_rp).  The doubling step's 4x
-// scale of T leaves the pairing unchanged (lines are homogeneous of degree 2 in T; a line scaled by an
-// Fp constant is killed by the final exponentiation's easy part).  The Miller value leaves in R form,
-// canonical (out_r), for k_fexp.
+// Representation boundary: the prep SoA holds canonical 12 x 32 values in R = 2^406 form.  The twist
+// points are moved to R' form once (in_r: T's start and the addition steps' Q).  The G1 evaluation
+// coordinates are NOT converted: multiplied in R form straight into the R'-form line, every
+// coefficient of a line comes out scaled by the same 2^14 (R / R'), and affine points use the constant
+// R mod p as their Z; a line scaled by an Fp constant leaves the pairing unchanged (the final
+// exponentiation's easy part kills Fp^*), as does the doubling step's 4x scale of T (lines are
+// homogeneous of degree 2 in T).  The Miller value leaves in R form, canonical (out_r), for k_fexp.
 #ifndef CC_MILLER_SIG
 #define CC_MILLER_SIG 2
 #endif
@@ -46,10 +47,16 @@ using LineS = Line<F2L, F2L, F2L>;
 template <class L>
 DEV LineS fit_line(const L& l) { return {fit<AS, BL>(l.l0), fit<AS, BL>(l.l2), fit<AS, BL>(l.l3)}; }
 
-// where a pair's G1 point lives: affine (x, y) in the R' form, word (slot * NL + limb) * n + i * is
+// where a pair's G1 evaluation point lives: word (slot * NL + limb) * n + i * is.  form:
+//   kJac    (XZ, Y, Z^3), R form: every line coefficient scaled by 2^14 (header)
+//   kAffR   affine (x, y), R form: l0 times R mod p (the affine Z), scale 2^14
+//   kAffRp  affine (x, y) in the lazy field's R' form (x R' mod p, canonical): l2 x, l3 y come out
+//           unscaled and l0 needs no product (SigG2's constant g~: one Fp product less per step)
+enum { kJac = 0, kAffR = 1, kAffRp = 2 };
 struct PSrc {
     const uint32_t* p;
     size_t n, is;
+    int form;
 };
 
 DEV Fq<AN, BC> ld_Pc(const PSrc& s, int slot, size_t i) {
@@ -59,19 +66,22 @@ DEV Fq<AN, BC> ld_Pc(const PSrc& s, int slot, size_t i) {
     return from_fp(x);
 }
 
-// f * line(P).  A skipped pair (identity argument: e(O, Q) = e(P, O) = 1) multiplies by the unit line
-// (1, 0, 0) instead of returning early: the product's type bound then holds on every path (f's value
-// bound only shrinks through a multiplication), and the lanes of a mixed wave would wait for the
-// others anyway.
+// f * line(P), the line scaled by 2^14 (header).  A skipped pair (identity argument: e(O, Q) =
+// e(P, O) = 1) multiplies by the unit line (1, 0, 0) instead of returning early: the product's type
+// bound then holds on every path (f's value bound only shrinks through a multiplication), and the
+// lanes of a mixed wave would wait for the others anyway.
 template <int B>
 DEV F12S eval_mul(const F12<AS, B>& f, const LineS& ln, const PSrc& ps, size_t i, bool skip) {
-    const auto r0 = reduce(ln.l0);
+    constexpr int32_t ONE_R[LN] = {LZ_C_OUT_LIMBS};
+    using A0 = decltype(mul_fpr(ln.l0, fq_const(ONE_R)));
+    A0 a0;
+    if (ps.form == kAffRp) a0 = fit<AN, A0::BV>(reduce(ln.l0));  // pair-uniform branch
+    else a0 = mul_fpr(ln.l0, ps.form == kJac ? ld_Pc(ps, 2, i) : fq_const(ONE_R));
     const auto a2 = mul_fpr(ln.l2, ld_Pc(ps, 0, i));
     const auto a3 = mul_fpr(ln.l3, ld_Pc(ps, 1, i));
-    using L = decltype(a2);
-    const auto a0 = fit<AN, L::BV>(r0);
+    using L = decltype(a0);
     const L one = fit<AN, L::BV>(f2_one()), zero = fit<AN, L::BV>(f2_zero());
-    return fit<AS, BF>(f12_mul_line(f, L{sel(skip, one.c, a0.c)}, L{sel(skip, zero.c, a2.c)},
+    return fit<AS, BF>(f12_mul_line(f, L{sel(skip, one.c, a0.c)}, L{sel(skip, zero.c, fit<AN, L::BV>(a2).c)},
                                     L{sel(skip, zero.c, fit<AN, L::BV>(a3).c)}));
 }
 
@@ -177,7 +187,7 @@ template <int SIG, bool kTwin>
 __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, size_t ps, const uint32_t* __restrict__ prep,
                                                const uint32_t* __restrict__ flags, const uint32_t* __restrict__ cst,
                                                uint32_t* __restrict__ fout, size_t fstride, size_t foff,
-                                               uint32_t* __restrict__ qcheck) {
+                                               uint32_t* __restrict__ qcheck, int pform) {
     constexpr int NP = 2;  // pairs per loop
     __shared__ int32_t lds[2 * TP][MB];
     const size_t i = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;  // lane pair: credential (twin: pair)
@@ -188,8 +198,20 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, size_t ps, const uin
     const uint32_t fl = flags[kTwin ? 2 * i : i];
     const bool skip0 = (fl & 5u) != 0;
     const bool skip1 = kTwin ? (2 * i + 1 >= n || (flags[2 * i + 1] & 5u) != 0) : (fl & 18u) != 0;
-    const PSrc ps0{prep + (size_t)S_P1 * NL * ps, ps, 1};
-    const PSrc ps1 = (kSigG2 && !kTwin) ? PSrc{cst, 1, 0} : PSrc{prep + (size_t)S_P2 * NL * ps, ps, 1};
+    // pform: the form of the preps' P (kAffRp), a kernel argument so that both eval_mul paths stay
+    // compiled as one runtime branch: with the branch folded away the loop's registers allocate
+    // differently and spill more (measured: +80 static scratch instructions, Miller +4 %)
+    PSrc ps0, ps1;
+    if (kTwin) {
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * ps, ps, 1, pform};
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * ps, ps, 1, pform};
+    } else if (kSigG2) {
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * ps, ps, 1, pform};
+        ps1 = PSrc{cst, 1, 0, kAffRp};
+    } else {
+        ps0 = PSrc{prep + (size_t)S_P1 * NL * ps, ps, 1, pform};
+        ps1 = PSrc{prep + (size_t)S_P2 * NL * ps, ps, 1, pform};
+    }
     const Soa S{const_cast<uint32_t*>(prep), ps};
     // both T's parked in LDS between their uses
     Tw T;
@@ -277,9 +299,9 @@ extern "C" int CC_MILLER_LAUNCH(int twin, size_t n, size_t pstride, const uint32
     dim3 g((unsigned)((2 * m + MB - 1) / MB)), b(MB);
     if (twin)
         hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, true>), g, b, 0, st, n, pstride, d_prep, d_flags, d_const, d_f,
-                           fstride, foff, d_qcheck);
+                           fstride, foff, d_qcheck, (int)cc::lz::kAffRp);
     else
         hipLaunchKernelGGL((cc::lz::k_miller<CC_MILLER_SIG, false>), g, b, 0, st, n, pstride, d_prep, d_flags, d_const, d_f,
-                           fstride, foff, d_qcheck);
+                           fstride, foff, d_qcheck, (int)cc::lz::kAffRp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
