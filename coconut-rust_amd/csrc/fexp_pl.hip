@@ -668,8 +668,35 @@ __global__ __launch_bounds__(64, 1) void k_miller_wide(size_t n, const uint32_t*
     if (threadIdx.x < 2) st_f12(Soa{fout, fstride}, foff + i, f);
 }
 
+// one level of the RLC product tree in the wide form: out[t] = in[2t] in[2t+1] (in[2t] alone for an odd
+// tail), one wave per product, the 18 Fp2 products on the wave's lane pairs at once.  The tree's short
+// levels are latency-bound (k_f12_reduce: one product on one lane pair, ~45 us a level whatever its
+// width); here a level holds about one Fp2 product's latency.
+__global__ __launch_bounds__(64, 2) void k_f12_reduce_wide(size_t n_in, const uint32_t* __restrict__ in,
+                                                          uint32_t* __restrict__ out) {
+    const size_t t = blockIdx.x;
+    const size_t n_out = (n_in + 1) / 2;
+    if (t >= n_out) return;  // wave-uniform
+    const Soa I{const_cast<uint32_t*>(in), n_in}, O{out, n_out};
+    Fp12 a;
+    ld_f12(a, I, 2 * t);
+    if (2 * t + 1 < n_in) {
+        Fp12 b;
+        ld_f12(b, I, 2 * t + 1);
+        f12_mul_wide(a, a, b);
+    }
+    if (threadIdx.x < 2) st_f12(O, t, a);
+}
+
 }  // namespace pl
 }  // namespace cc
+
+// one level of the product tree, wide form (k_f12_reduce_wide): (n + 1) / 2 waves
+extern "C" int cck_f12_reduce_wide(size_t n, const uint32_t* d_in, uint32_t* d_out, hipStream_t st) {
+    if (n < 2) return -1;
+    hipLaunchKernelGGL(cc::pl::k_f12_reduce_wide, dim3((unsigned)((n + 1) / 2)), dim3(64), 0, st, n, d_in, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 

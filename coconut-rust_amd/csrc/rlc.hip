@@ -18,7 +18,8 @@
 //                                         delta's digits); the delta-scaled fixed-base MSM
 //                                         (delta X + sum (delta m_j) Y_j) of pair 0 in the Miller
 //                                         kernels' SoA layout (soa.h; G1 points affine in the R' form)
-//   k_f12_reduce                        : one level of the pairwise product tree of Fp12 values
+//   k_f12_reduce                        : one level of the pairwise product tree of Fp12 values (the
+//                                         short levels: fexp_pl.hip k_f12_reduce_wide)
 //   k_rlc_partial_out                   : the partial's product and flag words (rlc_part.h; the fold
 //                                         writes its window section)
 //   k_rlc_gather                        : the finish's inputs from the gathered partials: their products
@@ -311,6 +312,13 @@ __global__ __launch_bounds__(256) void k_rlc_gather(size_t k, const uint32_t* __
 
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
+extern "C" int cck_f12_reduce_wide(size_t n, const uint32_t* d_in, uint32_t* d_out, hipStream_t st);
+
+// levels with at most this many products run in the wide form (one wave a product): the packed form
+// holds ~47 us a level (one product's latency on one lane pair) up to 16,384 products, the wide form
+// ~17 us up to 256 products, 24 / 35 / 48 us at 512 / 1,024 / 2,048 (profiles/r04/rlc_wide_tree)
+constexpr size_t kWideLevel = 1024;
+
 extern "C" {
 
 // d_pts: n fold points (AoS affine: 48 words SigG2, 24 SigG1); d_dig: 16 x n digit bytes; ps: the prep
@@ -348,7 +356,11 @@ int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any
     uint32_t *src = d_a, *dst = d_b;
     while (n > 1) {
         const size_t n_out = (n + 1) / 2;
-        hipLaunchKernelGGL(k_f12_reduce, dim3(nblocks(2 * n_out, 256)), dim3(256), 0, st, n, src, dst);
+        if (n_out <= kWideLevel) {
+            if (cck_f12_reduce_wide(n, src, dst, st)) return -1;
+        } else {
+            hipLaunchKernelGGL(k_f12_reduce, dim3(nblocks(2 * n_out, 256)), dim3(256), 0, st, n, src, dst);
+        }
         n = n_out;
         uint32_t* t = src;
         src = dst;
