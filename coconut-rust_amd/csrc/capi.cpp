@@ -70,6 +70,7 @@ int cck_msm_straus(int group, size_t ntask, size_t t, const uint8_t* d_pts, size
 int cck_vk_agg_fixed(int group, size_t n, size_t len, size_t t, int q, const uint64_t* d_ids, const uint32_t* d_l,
                      const uint64_t* d_iss_ids, int n_iss, const uint32_t* d_table, int wbits, const uint32_t* d_binf,
                      uint8_t* d_outX, uint8_t* d_outY, uint32_t* d_err, hipStream_t st);
+int cck_copy_rows(size_t n, size_t sb, const uint8_t* d_src, size_t pitch, uint8_t* d_dst, hipStream_t st);
 int cck_fixed_mul(int group, size_t n, const uint8_t* d_ks, const uint32_t* d_table, uint32_t base_inf,
                   uint8_t* d_out, hipStream_t st);
 int cck_prep_rlc(int mode, int part, size_t n, size_t ps, int q, uint64_t base_index, const uint32_t* d_key,
@@ -906,7 +907,7 @@ static cc_status launch_sig_aggregate(cc_ctx* c, size_t n, size_t len, size_t t,
     KCK(cck_msm_straus(sg, n, t, d_s2, len * sb, 0, sb, c->lag.as<uint32_t>(), 1, c->agg_scratch.as<uint32_t>(), d_o2, st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     // sigma_1 = sigs[0].sigma_1 (signature.rs:452): strided device copy of entry 0
-    HIPCK(hipMemcpy2DAsync(d_o1, sb, d_s1, len * sb, sb, n, hipMemcpyDeviceToDevice, st));
+    KCK(cck_copy_rows(n, sb, d_s1, len * sb, d_o1, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }
@@ -1342,7 +1343,7 @@ cc_status cc_aggregate_credential_batch_device(cc_ctx* c, size_t n, size_t len, 
     KCK(cck_vk_agg_fixed(oth_group(c->mode), n, len, t, (int)c->iss_q, d_ids, c->lag.as<uint32_t>(),
                          c->iss_ids.as<uint64_t>(), (int)c->iss_n, c->iss_table.as<uint32_t>(), c->iss_wbits,
                          c->iss_inf.as<uint32_t>(), d_outX, d_outY, c->dev_err.as<uint32_t>(), side));
-    HIPCK(hipMemcpy2DAsync(d_out_s1, sb, d_s1, len * sb, sb, n, hipMemcpyDeviceToDevice, st));
+    KCK(cck_copy_rows(n, sb, d_s1, len * sb, d_out_s1, st));  // sigma_1 = sigs[0].sigma_1 (signature.rs:452)
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     if (side != st) {
         HIPCK(hipEventRecord(c->ev_join, side));
