@@ -695,33 +695,34 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_g1pl(size_t n, int q, int r
             slot++;
             if (!binf[hh]) pl::ft_add_g2_lz(la, k.v, table, wbits, hh, 0, nwin);
         }
-        acc = pl::jl_to_pl(la);
         fr_from_be48(k, chal + i * 48);
         if (Jok) {
-            constexpr int JW = sizeof(Jac<G2>) / 4;
-            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * JW + w) * 2 * n + g]; };
-            Jac<G2> t;
-            jac_from_aff(t, Ja);
+            // chal J in fixed 4-bit windows on the lazy pair-lane field (curve_lz.h), the table of d J,
+            // d = 1..15, in the scratch as lazy points (this lane's halves: 42 words an entry)
+            constexpr int LW = sizeof(lz::JL) / 4;
+            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * LW + w) * 2 * n + g]; };
+            const lz::AL Jl{lz::reduce(lz::in_r2(Ja.x)), lz::reduce(lz::in_r2(Ja.y))};
+            lz::JL t = lz::jl_from_aff(Jl);
 #pragma unroll 1
             for (int d = 1; d <= 15; d++) {
-                if (d > 1) jac_add_aff(t, t, Ja);
+                if (d > 1) t = lz::jl_add_aff(t, Jl);
                 const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
-                for (int w = 0; w < JW; w++) tab(d, w) = tw[w];
+                for (int w = 0; w < LW; w++) tab(d, w) = tw[w];
             }
-            Jac<G2> sacc;
-            jac_set_inf(sacc);
+            lz::JL sacc = lz::jl_inf();
 #pragma unroll 1
             for (int win = 63; win >= 0; win--) {
-                for (int b = 0; b < 4; b++) jac_dbl(sacc, sacc);
+                for (int b = 0; b < 4; b++) sacc = lz::jl_dbl(sacc);
                 const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
                 if (d) {
                     uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
-                    for (int w = 0; w < JW; w++) tw[w] = tab((int)d, w);
-                    jac_add(sacc, sacc, t);
+                    for (int w = 0; w < LW; w++) tw[w] = tab((int)d, w);
+                    sacc = lz::jl_add(sacc, t);
                 }
             }
-            jac_add(acc, acc, sacc);
+            la = lz::jl_add(la, sacc);
         }
+        acc = pl::jl_to_pl(la);
         Aff<Fp2> Tf;
         if (pl::pair_all(g2_decode(Tf, Tb + i * 192))) {
             Aff<G2> Ta;
@@ -874,7 +875,8 @@ int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const ui
                  const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_jtab, hipStream_t st) {
     if (!n) return 0;
     dim3 g(nblocks(n, 256)), b(256);
-    // d_jtab: 15 Jacobian points of the other group per element (<= 15 x 72 words a proof)
+    // d_jtab: 15 Jacobian points of the other group per element (<= 15 x 84 words a proof: SigG1's lazy
+    // pair-lane G2 points, 42 words a lane)
     if (mode == 0) {
         // hidden responses for role A: balance nwin (1 + split) + ~233 (chal J) against
         // nwin (hidden - split) + nwin r + ~10 (mixed-addition units)

@@ -581,11 +581,11 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
 
 static cc_status ensure_work(cc_ctx* c, size_t n) {
     size_t words = n * 12;  // one Fp slot
-    // scratch: the PoK prep's per-proof table of d J (15 Jacobian points, <= 15 x 72 words), and the
-    // one-element fexp's (fexp_pl.hip k_fexp1: 72 slots of 12 words); the batched fexp (fexp_q.hip)
-    // keeps its chain in registers
+    // scratch: the PoK prep's per-proof table of d J (15 Jacobian points, <= 15 x 84 words: SigG1's lazy
+    // G2 points), and the one-element fexp's (fexp_pl.hip k_fexp1: 72 slots of 12 words); the batched
+    // fexp (fexp_q.hip) keeps its chain in registers
     if (c->prep.ensure(words * 4 * PREP_SLOTS) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
-        c->scratch.ensure((n * 15 * 72 + 72 * 12) * 4) || c->verdicts.ensure(n))
+        c->scratch.ensure((n * 15 * 84 + 72 * 12) * 4) || c->verdicts.ensure(n))
         return CC_ERR_HIP;
     return CC_OK;
 }
