@@ -678,6 +678,9 @@ def main():
     ap.add_argument("--steps", type=int, default=100)  # ~2.3 s timed at config 2: long enough to see from outside
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=0, help="credentials per GPU per step (0 = the config's size)")
+    ap.add_argument("--iss-bits", type=int, default=None,
+                    help="issuer table window width for the aggregate modes (cc_set_table_bits; 0 = the "
+                         "library's <= 16 GiB choice; default: bench_modes.BENCH_ISS_BITS = 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) rate")
     ap.add_argument("--vk-bits", type=int, default=None,

@@ -186,6 +186,24 @@ def _timed(args, step, dev, dist, ctx):
     return _max_over_ranks(el, dist, dev), phase / max(args.steps, 1)
 
 
+# Issuer-table window width the aggregate modes opt into (cc_set_table_bits): 16-bit windows, 16 windows a
+# scalar — 70 GB of tables for 100 issuers x 7 G1 keys (SigG2), 141 GB for 7 G2 keys (SigG1), built in
+# 0.35 / 1.3 s at setup.  The library's default (<= 16 GiB) picks 13 / 12 bits (20 / 22 windows);
+# measured 16 against the default: config 4 +5.5 % (SigG2), +29 % (SigG1) (profiles/r04/issbits).
+BENCH_ISS_BITS = 16
+
+
+def iss_bits_for(args):
+    """Issuer-table window width (cc_set_table_bits): --iss-bits (0: the library's choice by memory), else
+    BENCH_ISS_BITS."""
+    b = getattr(args, "iss_bits", None)
+    return BENCH_ISS_BITS if b is None else b
+
+
+def iss_table_gib(bits, nbases, g2):
+    return round(nbases * -(-256 // bits) * ((1 << bits) - 1) * (192 if g2 else 96) / 2 ** 30, 1)
+
+
 def bench_aggregate(args):
     import torch
     import coconut
@@ -199,6 +217,7 @@ def bench_aggregate(args):
     b = make_aggregate_batch(ctx, sigm, n, seed=4000 + rank)
     gen_s = time.perf_counter() - t_set
     t_iss = time.perf_counter()
+    ctx.set_table_bits(0, iss_bits_for(args))
     ctx.set_issuers(b["iss"], b["X"], b["Y"], b["q"])
     iss_ms = (time.perf_counter() - t_iss) * 1e3
     t, q, sb, ob = b["t"], b["q"], b["sb"], b["ob"]
@@ -253,7 +272,8 @@ def bench_aggregate(args):
             "config": {"workload": f"config4: {n:,} credentials per GPU, t=67 of n=100 issuers, msg_count={q}, "
                                    + ("SigG1" if sigm else "SigG2"),
                        "credentials_per_gpu": n, "threshold": t, "issuers": 100,
-                       "parallelism": f"shard-by-credential x{world}", "issuer_table_bits": ctx.table_bits()[1]},
+                       "parallelism": f"shard-by-credential x{world}", "issuer_table_bits": ctx.table_bits()[1],
+                       "issuer_table_gib": iss_table_gib(ctx.table_bits()[1], 100 * (q + 1), bool(sigm))},
             **__import__("bench").lib_info(),
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 3),
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",

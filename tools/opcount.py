@@ -769,12 +769,16 @@ def fixed_sum(g, pts, scalars, wbits=8):
     return g.to_aff(acc)
 
 
-def aggregate_case(d, case, n_issuers=100):
+# issuer-table window width of the aggregate bench modes (bench_modes.py BENCH_ISS_BITS, cc_set_table_bits)
+BENCH_ISS_BITS = 16
+
+
+def aggregate_case(d, case, n_issuers=100, wb=None):
     """Signature::aggregate (Straus, SignatureGroup) + Verkey::aggregate (issuer tables, OtherGroup;
-    window width as cc_set_issuers picks it for n_issuers x (q + 1) bases)."""
+    window width wb, default as cc_set_issuers picks it for n_issuers x (q + 1) bases)."""
     gs, go = (G2, G1) if d["mode"] == "G2" else (G1, G2)
     t, q = d["threshold"], d["q"]
-    wb = issuer_wbits(n_issuers * (q + 1), go is G2)
+    wb = wb or issuer_wbits(n_issuers * (q + 1), go is G2)
     ids = case["ids"][:t]
     ls = [lagrange0(ids, i) for i in ids]
     s2 = [decode(gs, bytes.fromhex(h)) for h in case["sigma2"][:t]]
@@ -1009,14 +1013,14 @@ def main():
                                "mads_per_credential": {k: round(v * 288) for k, v in avg.items()}}
     with open(os.path.join(root, "tests", "golden", "aggregate_g2_t67_subsets.json")) as f:
         d = json.load(f)
-    sig, vkX, vkY, cnt = aggregate_case(d, d["cases"][0])
+    sig, vkX, vkY, cnt = aggregate_case(d, d["cases"][0], wb=BENCH_ISS_BITS)
     assert enc(G2, sig).hex() == d["cases"][0]["out_sigma2"] and enc(G1, vkX).hex() == d["cases"][0]["out_X"]
     res["configs"]["aggregate_sigg2_t67"] = {
         "credentials_averaged": 1, "M_per_credential": {k: round(v, 1) for k, v in cnt.items()},
         "mads_per_credential": {k: round(v * 288) for k, v in cnt.items()},
         "note": "straus_sigma2 = Signature::aggregate (67-point G2 Straus MSM); fixed_verkey = Verkey::aggregate "
-                "(q+1 = 7 67-point G1 fixed-base MSMs from the issuer tables, 13-bit windows: the width "
-                "cc_set_issuers picks for 100 issuers x 7 keys); case 0 of "
+                "(q+1 = 7 67-point G1 fixed-base MSMs from the issuer tables, 16-bit windows: the width the bench "
+                "opts into, BENCH_ISS_BITS; the library's <= 16 GiB default picks 13); case 0 of "
                 "tests/golden/aggregate_g2_t67_subsets.json, outputs checked against the fixture"}
     with open(os.path.join(root, "tests", "golden", "pok_g2_q32.json")) as f:
         d = json.load(f)
@@ -1074,14 +1078,15 @@ def main():
     # SigG1 forms of configs 4 and 5
     with open(os.path.join(root, "tests", "golden", "aggregate_g1_t67_subsets.json")) as f:
         d = json.load(f)
-    sig, vkX, vkY, cnt = aggregate_case(d, d["cases"][0])
+    sig, vkX, vkY, cnt = aggregate_case(d, d["cases"][0], wb=BENCH_ISS_BITS)
     assert enc(G1, sig).hex() == d["cases"][0]["out_sigma2"] and enc(G2, vkX).hex() == d["cases"][0]["out_X"]
     res["configs"]["aggregate_sigg1_t67"] = {
         "credentials_averaged": 1, "M_per_credential": {k: round(v, 1) for k, v in cnt.items()},
         "mads_per_credential": {k: round(v * 288) for k, v in cnt.items()},
         "note": "SigG1: straus_sigma2 = Signature::aggregate (67-point G1 Straus MSM); fixed_verkey = Verkey::aggregate "
-                "(q+1 = 7 67-point G2 fixed-base MSMs from the issuer tables at the width cc_set_issuers picks for "
-                "100 issuers x 7 G2 keys); case 0 of tests/golden/aggregate_g1_t67_subsets.json, outputs checked"}
+                "(q+1 = 7 67-point G2 fixed-base MSMs from the issuer tables, 16-bit windows: the width the bench "
+                "opts into, BENCH_ISS_BITS; the library's default picks 12); case 0 of "
+                "tests/golden/aggregate_g1_t67_subsets.json, outputs checked"}
     with open(os.path.join(root, "tests", "golden", "pok_g1_q32.json")) as f:
         d = json.load(f)
     VK_WBITS = 20
