@@ -626,8 +626,8 @@ def bench_rlc(args):
         out["kernels"] = kt
         rk = kernel_pmc_report("rlc")
         out["rocprof_kernels"] = rk
-        mk = next((v for k, v in (rk or {}).get("kernels", {}).items() if "k_miller" in k and "true>" in k), {})
-        out["roofline"] = {"bound": "valu-int", "kernel": "miller (two credentials per shared-squaring loop + window pairs)",
+        mk = next((v for k, v in (rk or {}).get("kernels", {}).items() if "k_miller4" in k), {})
+        out["roofline"] = {"bound": "valu-int", "kernel": "miller (k_miller4: four credentials per shared-squaring loop)",
                            "achieved": kt["miller"]["achieved_Tmad_s"], "peak": round(peak / 1e12, 3),
                            "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)", "frac": kt["miller"]["frac"],
                            "traffic": mk.get("hbm_bytes_per_launch"),

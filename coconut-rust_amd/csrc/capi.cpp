@@ -50,6 +50,10 @@ int cck_miller_lz_g2(int twin, size_t n, size_t pstride, const uint32_t* d_prep,
 int cck_miller_lz_g1(int twin, size_t n, size_t pstride, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
+int cck_miller4_lz_g2(size_t n, size_t pstride, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
+                      size_t fstride, size_t foff, uint32_t* d_qcheck, hipStream_t st);
+int cck_miller4_lz_g1(size_t n, size_t pstride, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
+                      size_t fstride, size_t foff, uint32_t* d_qcheck, hipStream_t st);
 size_t cck_fold_words(int mode, size_t n);
 int cck_fold_pseudo();
 int cck_fold_window(int mode, size_t n, uint32_t* d_work, uint32_t* d_partial, hipStream_t st);
@@ -228,14 +232,13 @@ static int cck_miller(int mode, size_t n, const uint32_t* d_prep, const uint32_t
     return mode == 0 ? cck_miller_lz_g2(0, n, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st)
                      : cck_miller_lz_g1(0, n, n, d_prep, d_flags, d_const, d_f, n, 0, nullptr, st);
 }
-// the RLC credentials (pair 0 only: their second pairs are folded, fold.hip), two per lane pair
-// through the shared-squaring loop:
-// (n + 1) / 2 Miller values, each the product of two pairs' (the RLC multiplies them all), to SoA
-// elements [0, (n + 1) / 2) of stride fstride; the prep SoA has stride ps
-static int cck_miller_twin(int mode, size_t n, size_t ps, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
+// the RLC credentials (pair 0 only: their second pairs are folded, fold.hip) four per lane pair
+// through the shared-squaring loop (k_miller4, 1 wave/SIMD): ceil(n / 4) Miller values, each the
+// product of four pairs' (the RLC multiplies them all), over the twin layout (prep stride ps >= ceil(n / 2))
+static int cck_miller_quad(int mode, size_t n, size_t ps, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f,
                            size_t fstride, uint32_t* d_qcheck, hipStream_t st) {
-    return mode == 0 ? cck_miller_lz_g2(1, n, ps, d_prep, d_flags, nullptr, d_f, fstride, 0, d_qcheck, st)
-                     : cck_miller_lz_g1(1, n, ps, d_prep, d_flags, nullptr, d_f, fstride, 0, nullptr, st);
+    return mode == 0 ? cck_miller4_lz_g2(n, ps, d_prep, d_flags, d_f, fstride, 0, d_qcheck, st)
+                     : cck_miller4_lz_g1(n, ps, d_prep, d_flags, d_f, fstride, 0, nullptr, st);
 }
 
 static inline int sig_bytes(int mode) { return mode == 0 ? 192 : 97; }
@@ -696,8 +699,8 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
         HIPCK(hipMemcpyAsync(d_partial, kNeutral.data(), RLC_PART_WORDS * 4, hipMemcpyHostToDevice, st));
         return CC_OK;
     }
-    const size_t N = (n + 1) / 2;  // Miller values (two credentials' pairs each)
-    const size_t PS = N;           // prep SoA stride
+    const size_t PS = (n + 1) / 2;  // prep SoA stride (the twin layout: credentials 2 t, 2 t + 1 at element t)
+    const size_t N = (n + 3) / 4;   // Miller values (four credentials' pairs each, k_miller4)
     cc_status s = ensure_work(c, n);
     if (s) return s;
     if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4) || c->fbuf.ensure(N * 144 * 4) ||
@@ -737,7 +740,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     KCK(prep_part(1));  // delta X~ + sum (delta m_j) Y~_j
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     // SigG2: sigma_1's subgroup test comes from this loop's T (a failure raises rlc_any: fallback)
-    KCK(cck_miller_twin(c->mode, n, PS, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), c->fbuf.as<uint32_t>(), N,
+    KCK(cck_miller_quad(c->mode, n, PS, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), c->fbuf.as<uint32_t>(), N,
                         c->mode == 0 ? c->rlc_any.as<uint32_t>() : nullptr, st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_rlc_reduce(N, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,

@@ -174,6 +174,7 @@ static __device__ __noinline__ void t_check(const Tw* T, const uint32_t* prep, s
 
 }  // namespace
 
+#ifndef CC_MILLER_QUAD
 // prep: SoA slots of soa.h, stride ps (>= the elements read); flags: bit0 sigma_1 = O, bit1 sigma_2 = O,
 // bit2 pr = O, bit4 pair-1 P = O
 // cst: SigG2 -> g~ affine in the lazy R' form (24 words, cck_lazy_form); SigG1 -> g~ lines (68 x 72
@@ -276,9 +277,100 @@ __global__ __launch_bounds__(MB, 2) void k_miller(size_t n, size_t ps, const uin
     for (int k = 0; k < 6; k++) st_fp(O, 2 * k + (int)half_id(), foff + i, out_r(v[k].c));
 }
 
+#else  // CC_MILLER_QUAD: its own object (Makefile miller4_*), so the 1-wave kernel's register budget does
+       // not reach the out-of-line helpers of the 2-wave kernels above
+// RLC, FOUR credentials' pairs per shared-squaring loop (twice kTwin's): the Fp12 squaring is shared by
+// four pairs instead of two (per credential 26 Fp2 products a step against 29).  Reads the twin layout
+// (credentials 4 j .. 4 j + 3 = pairs 0 / 1 of elements 2 j and 2 j + 1); the four T's are parked packed
+// in LDS (4 x 39 words a lane: the whole 160 KiB of a CU at 1 wave/SIMD, 256 lanes), the loop body is
+// the two-pair loop's with one pair at a time; the product of the four Miller values goes to element
+// foff + j.
+template <int SIG>
+__global__ __launch_bounds__(MB, 1) void k_miller4(size_t n, size_t ps, const uint32_t* __restrict__ prep,
+                                                const uint32_t* __restrict__ flags, uint32_t* __restrict__ fout,
+                                                size_t fstride, size_t foff, uint32_t* __restrict__ qcheck,
+                                                int pform) {
+    constexpr int NP = 4;
+    __shared__ int32_t lds[NP * TP][MB];
+    const size_t j = (blockIdx.x * (size_t)blockDim.x + threadIdx.x) >> 1;
+    if (j >= (n + 3) / 4) return;  // pair-uniform
+    const Soa S{const_cast<uint32_t*>(prep), ps};
+    uint32_t skipm = 0;  // bit k: pair k skipped (credential absent, or an identity argument)
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
+        const size_t c = 4 * j + k;
+        const bool in = c < n;
+        if (!in || (flags[in ? c : 0] & 5u) != 0) skipm |= 1u << k;
+        F2<AN, 17> qx, qy;
+        ld_q(qx, qy, S, (k & 1) ? S_Q2 : S_Q1, in ? c >> 1 : 0);
+        park(lds, k, t_from(qx, qy));
+    }
+    // pair k: credential 4 j + k at twin element 2 j + k / 2, slots pair (k & 1)
+    auto elem = [&](int k) -> size_t { return 4 * j + k < n ? 2 * j + (k >> 1) : 0; };
+    auto psrc = [&](int k) { return PSrc{prep + (size_t)((k & 1) ? S_P2 : S_P1) * NL * ps, ps, 1, pform}; };
+    F12S f = fit<AS, BF>(f12_one());
+#pragma unroll 1
+    for (int b = 62; b >= 0; b--) {
+        F12<AS, BS> g = b != 62 ? fit<AS, BS>(f12_sqr(f)) : fit<AS, BS>(f);
+#pragma unroll 1
+        for (int k = 0; k < NP; k++) {
+            Tw T = unpark(lds, k);
+            const LineS ln = fit_line(line_dbl(T));
+            park(lds, k, T);
+            g = fit<AS, BS>(eval_mul(g, ln, psrc(k), elem(k), (skipm >> k) & 1u));
+        }
+        f = narrow_to<BF>(g);
+        if ((X_ABS >> b) & 1ull) {
+#pragma unroll 1
+            for (int k = 0; k < NP; k++) {
+                StepState st;
+                st.f = f;
+                st.T = unpark(lds, k);
+                miller_add(&st, prep, ps, (k & 1) ? S_Q2 : S_Q1, elem(k), nullptr, psrc(k), (skipm >> k) & 1u);
+                park(lds, k, st.T);
+                f = st.f;
+            }
+        }
+    }
+    if (SIG == 2 && qcheck) {
+#pragma unroll 1
+        for (int k = 0; k < NP; k++) {
+            if ((skipm >> k) & 1u) continue;  // pair-uniform
+            const Tw Tk = unpark(lds, k);
+            t_check(&Tk, prep, ps, (k & 1) ? S_Q2 : S_Q1, elem(k), qcheck);
+        }
+    }
+    f = f12_conj(f);
+    const Soa O{fout, fstride};
+    const F2<AS, BF>* v = reinterpret_cast<const F2<AS, BF>*>(&f);
+#pragma unroll
+    for (int k = 0; k < 6; k++) st_fp(O, 2 * k + (int)half_id(), foff + j, out_r(v[k].c));
+}
+
+#endif  // CC_MILLER_QUAD
+
 }  // namespace lz
 }  // namespace cc
 
+#ifdef CC_MILLER_QUAD
+#if CC_MILLER_SIG == 2
+#define CC_MILLER4_LAUNCH cck_miller4_lz_g2
+#else
+#define CC_MILLER4_LAUNCH cck_miller4_lz_g1
+#endif
+// four credentials per lane pair (k_miller4) over the twin layout (pstride >= ceil(n / 2)): ceil(n / 4)
+// Miller values to SoA elements [foff, foff + m) of stride fstride; d_qcheck as the twin launch's
+extern "C" int CC_MILLER4_LAUNCH(size_t n, size_t pstride, const uint32_t* d_prep, const uint32_t* d_flags,
+                                 uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck, hipStream_t st) {
+    if (!n) return 0;
+    const size_t m = (n + 3) / 4;
+    if (fstride < foff + m || pstride < (n + 1) / 2) return -1;
+    constexpr int MB = cc::lz::MB;
+    hipLaunchKernelGGL((cc::lz::k_miller4<CC_MILLER_SIG>), dim3((unsigned)((2 * m + MB - 1) / MB)), dim3(MB), 0, st, n,
+                       pstride, d_prep, d_flags, d_f, fstride, foff, d_qcheck, (int)cc::lz::kAffRp);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#else
 #if CC_MILLER_SIG == 2
 #define CC_MILLER_LAUNCH cck_miller_lz_g2
 #else
@@ -305,3 +397,4 @@ extern "C" int CC_MILLER_LAUNCH(int twin, size_t n, size_t pstride, const uint32
                            fstride, foff, d_qcheck, (int)cc::lz::kAffRp);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+#endif  // CC_MILLER_QUAD

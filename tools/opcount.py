@@ -926,10 +926,10 @@ RLC_N, RLC_PSEUDO = 131072, 16  # credentials per GPU (config 3), fold pseudo-cr
 
 
 def rlc_sigg2(cred, vk_aff, gtil_aff, q, rnd):
-    """k_rlc_check_sigg2 + k_rlc_msm_sigg2 -> fold (fold.hip) -> k_miller<2,true> (two
-    credentials' first pairs per shared-squaring loop; + the 16 window pseudo-credentials' one-pair
-    loops, fexp_pl.hip k_miller_wide: the same products, spread over a wave) -> k_f12_reduce over
-    (RLC_N / 2 + RLC_PSEUDO) values; the batch's one final exponentiation is amortised over RLC_N.
+    """k_rlc_check_sigg2 + k_rlc_msm_sigg2 -> fold (fold.hip) -> k_miller4<2> (four
+    credentials' first pairs per shared-squaring loop) -> the product tree over RLC_N / 4 values; the
+    finish's 16 window pairs (one-pair loops, fexp_pl.hip k_miller_wide) and the batch's one final
+    exponentiation are outside the partial's phases (amortised over RLC_N they are < 0.1 %).
     delta is a random 128-bit value here (the counts do not depend on the key stream)."""
     counts = {}
     s1 = decode(G2, bytes.fromhex(cred["sigma1"]))
@@ -951,12 +951,14 @@ def rlc_sigg2(cred, vk_aff, gtil_aff, q, rnd):
     f = miller2([(s1, pe, False)])
     m1 = C.take()  # one pair alone: a window pseudo-credential
     f = miller2([(s1, pe, False), (s1, pe, False)])  # twin: two credentials, one loop
-    for _ in range(2):  # miller_t_in_subgroup per credential: psi(sigma_1) against its T, 2 Fp2 products + psi
-        f2_mul(s1[0], s1[0])
-        f2_mul(s1[0], s1[0])
-        f2_mul(s1[0], s1[0])
-        f2_mul(s1[0], s1[0])
     m2 = C.take() / 2
+    f = miller2([(s1, pe, False)] * 4)  # k_miller4: four credentials, one loop
+    for _ in range(4):  # miller_t_in_subgroup per credential: psi(sigma_1) against its T, 2 Fp2 products + psi
+        f2_mul(s1[0], s1[0])
+        f2_mul(s1[0], s1[0])
+        f2_mul(s1[0], s1[0])
+        f2_mul(s1[0], s1[0])
+    m4 = C.take() / 4
     # fold: one signed point per nonzero digit into a 16-entry chunk (the chunk's first addition is
     # free), then one Jacobian addition of the chunk partial into its bucket
     neg2 = (s2[0], f2_neg(s2[1]))
@@ -966,9 +968,9 @@ def rlc_sigg2(cred, vk_aff, gtil_aff, q, rnd):
     addj_m = C.take()
     fold = 16 * add_m * 15 / 16 + addj_m
     counts["prep"] = round(counts["prep"] + fold, 1)  # the fold runs between the checks and the MSM
-    counts["miller"] = round(m2 + m2 * RLC_PSEUDO / RLC_N, 1)  # the window pairs ride in the twin launch
+    counts["miller"] = round(m4, 1)
     f12_mul(f, f)
-    counts["reduce"] = round(C.take() * (RLC_N / 2 + RLC_PSEUDO) / RLC_N, 1)
+    counts["reduce"] = round(C.take() * (RLC_N / 4) / RLC_N, 1)
     counts["miller_twin_per_credential"] = m2
     counts["miller_one_pair"] = m1
     return counts
@@ -1049,11 +1051,7 @@ def main():
         "mads_per_credential": {k: round(sum(r[k] for r in rows) / len(rows) * 288) for k in rows[0]},
         "note": "valid credentials of tests/golden/verify_g2_q16.json; prep = decode + sigma_2's G2 subgroup check + "
                 "the fold's bucket additions + delta-scaled fixed-base MSM (sigma_1's check comes from the Miller "
-                "loop's T); miller = half a two-credential shared-squaring Miller loop (with both subgroup "
-                "tests) + the 16 window pairs (half a shared loop each, in the same launch) amortised over 131,072 "
-                "credentials (the fold's per-window bucket combination, ~30 G2 operations a lane on 16 "
-                "waves, is not counted: < 0.01 M a credential); reduce = the tree's Fp12 products over "
-                "65,536 + 16 values, per credential"}
+                "loop's T); miller = a quarter of a four-credential shared-squaring Miller loop (k_miller4, with the four subgroup tests); the finish's 16 window pairs and its one final exponentiation are amortised over 131,072 credentials (< 0.1 %) and not counted; reduce = the partial's product tree over 32,768 values, per credential"}
     # per-credential verkeys (Signature::verify with the caller's verkey; pervk.hip), q = 6
     VK_WBITS = 22
     for name, key, mode in (("verify_g2_q6_pervk.json", "verify_sigg2_q6_pervk", "G2"),
