@@ -7,11 +7,12 @@
 //          pair 1 = (-sigma_2, g~): g~ affine constant.
 //   SigG1: pair 0 = (pr [affine G2], sigma_1); pair 1 = (g~ [precomputed lines], -sigma_2); sigma_1,
 //          -sigma_2 arrive in the lazy R' form (kAffRp: no product for l0).
-//   RLC mode keeps pair 0 of every credential (its second pairs are folded, fold.hip) and runs TWO
-//   credentials through the 2-pair loop (kTwin): the RLC only needs the product of the credentials'
-//   Miller values, and the shared squaring halves the Fp12 work per credential (5,696 Fp
-//   multiplications against 6,800 for a loop of its own).  The fold's 16 window pairs run in the
-//   wide one-wave form (fexp_pl.hip k_miller_wide).
+//   RLC mode keeps pair 0 of every credential (its second pairs are folded, fold.hip) and runs FOUR
+//   credentials through one loop (k_miller4, built as its own object with CC_MILLER_QUAD; kTwin, two
+//   credentials through the 2-pair loop, is the round-3 form): the RLC only needs the product of the
+//   credentials' Miller values, and the shared squaring divides the Fp12 work per credential (5,002 Fp
+//   multiplications against 5,548 for two a loop, 6,664 for a loop of its own).  The fold's 16 window
+//   pairs run in the finish in the wide one-wave form (fexp_pl.hip k_miller_wide).
 //
 // Representation boundary: the prep SoA holds canonical 12 x 32 values in R = 2^406 form.  The twist
 // points are moved to R' form once (in_r: T's start and the addition steps' Q).  The G1 evaluation
