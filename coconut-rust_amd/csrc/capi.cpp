@@ -450,6 +450,24 @@ static cc_status rebuild_tables(cc_ctx* c) {
     return CC_OK;
 }
 
+// subgroup status of the verkey points (X~ || Y~, q + 1 encodings) and the context's g~: the RLC accepts
+// only when all are in the order-r subgroup.  Depends on g~ as well, so cc_set_params recomputes it
+// whenever it rebinds g~ under an existing verkey.
+static cc_status refresh_vk_subgroup(cc_ctx* c, const uint8_t* vk_all, size_t q) {
+    c->vk_subgroup = false;
+    const int og = oth_group(c->mode);
+    std::vector<uint8_t> st(q + 1);
+    cc_status s = subgroup_host(c, og, q + 1, vk_all, st.data());
+    if (s) return s;
+    uint8_t gst = 0;
+    s = subgroup_host(c, og, 1, c->gtilde_bytes.data(), &gst);
+    if (s) return s;
+    bool ok = gst == 2;
+    for (size_t k = 0; k <= q; k++) ok = ok && st[k] == 2;
+    c->vk_subgroup = ok;
+    return CC_OK;
+}
+
 cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
     if (!c || !g_tilde) return CC_ERR_DECODE;
     if (!c->peers.empty()) {
@@ -491,7 +509,8 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
         // refresh g~ slot of the verkey block and its table
         HIPCK(hipMemcpy(c->vk_aff.as<uint32_t>() + (c->q + 1) * aw, c->gtilde_aff.p, aw * 4, hipMemcpyDeviceToDevice));
         HIPCK(hipMemcpy(c->vk_inf.as<uint32_t>() + (c->q + 1), &c->gtilde_inf, 4, hipMemcpyHostToDevice));
-        cc_status st = rebuild_tables(c);
+        cc_status st = refresh_vk_subgroup(c, c->vk_bytes.data(), c->q);
+        if (!st) st = rebuild_tables(c);
         if (st) {
             c->have_vk = false;
             c->q = 0;
@@ -539,16 +558,8 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
     HIPCK(hipMemcpy(c->vk_inf.as<uint32_t>() + (q + 2), c->vk_inf.p, 4, hipMemcpyDeviceToDevice));
     HIPCK(hipMemcpy(&c->X_inf, c->vk_inf.p, 4, hipMemcpyDeviceToHost));
     {
-        // subgroup status of the verkey points and g~: RLC accepts only when all are in the subgroup
-        std::vector<uint8_t> st(q + 2);
-        cc_status s2 = subgroup_host(c, og, q + 1, all.data(), st.data());
+        cc_status s2 = refresh_vk_subgroup(c, all.data(), q);
         if (s2) return s2;
-        uint8_t gst = 0;
-        s2 = subgroup_host(c, og, 1, c->gtilde_bytes.data(), &gst);
-        if (s2) return s2;
-        bool ok = gst == 2;
-        for (size_t k = 0; k <= q; k++) ok = ok && st[k] == 2;
-        c->vk_subgroup = ok;
     }
     c->q = q;
     cc_status st = rebuild_tables(c);
@@ -1600,7 +1611,7 @@ static cc_status multi_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, 
                                          p->in_msgs.as<uint8_t>(), p->rlc_part.as<uint32_t>(), p->stream);
         });
         if (s) return s;
-        // the one exchange step: all-gather of the 580-byte partials
+        // the one exchange step: all-gather of the 3,716-byte (RLC_PART_WORDS = 929 words) partials
         if (ncclGroupStart() != ncclSuccess) return CC_ERR_RCCL;
         for (size_t d = 0; d < k; d++) {
             cc_ctx* p = c->peers[d];

@@ -207,15 +207,26 @@ def test_pok_verify_golden(ctxs, name):
             assert gts[576 * i:576 * (i + 1)].hex() == p["gt"], (i, p["kind"])
 
 
+def _full_fr(rng, n):
+    """n full-size Fr scalars (uniform below 2^254 < r: every 4-bit window, the top ones included,
+    carries non-zero digits) from a numpy Generator, as Python ints and as 48-byte big-endian rows."""
+    raw = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    raw[:, 0] &= 0x3F
+    rows = np.zeros((n, 48), np.uint8)
+    rows[:, 16:] = raw
+    b = rows.tobytes()
+    return [int.from_bytes(b[48 * i:48 * (i + 1)], "big") for i in range(n)], b
+
+
 def _gen_batch(mode, n, q, seed, bad_every=16):
     """Valid-by-construction credentials (sigma1 = k G, sigma2 = k (x + sum y m) G) generated by the
-    C oracle; every `bad_every`-th has sigma2 off by G.  Returns inputs and expected verdicts."""
+    C oracle with full-size Fr scalars (x, y_j, every message and k); every `bad_every`-th has sigma2
+    off by G.  Returns inputs and expected verdicts."""
     from oracle import coconut_ref as C
     oc = oracle_lib()
     rng = np.random.default_rng(seed)
     R = C.R
-    x = int(rng.integers(1, 2**62)) * 7919 % R
-    y = [int(rng.integers(1, 2**62)) * (j + 3) % R for j in range(q)]
+    (x, *y), _ = _full_fr(rng, q + 1)
     g_other = 1 if mode == 0 else 2  # OtherGroup generator (G1 for SigG2)
     sig_group = 2 if mode == 0 else 1
     ob, sb = (97, 192) if mode == 0 else (192, 97)
@@ -224,12 +235,14 @@ def _gen_batch(mode, n, q, seed, bad_every=16):
     pts = ctypes.create_string_buffer(ob * (q + 2))
     oc.oc_gen_mul(g_other, ctypes.c_size_t(q + 2), b"".join(s.to_bytes(48, "big") for s in scal), pts)
     X, Y, gtil = pts.raw[:ob], pts.raw[ob:ob * (q + 1)], pts.raw[ob * (q + 1):]
-    msgs = rng.integers(0, 2**63, size=(n, q), dtype=np.int64)
-    ks = rng.integers(1, 2**63, size=n, dtype=np.int64)
+    msgs, mb = _full_fr(rng, n * q)
+    ks, _ = _full_fr(rng, n)
     e1, e2, expect = [], [], np.ones(n, dtype=np.uint8)
     for i in range(n):
-        k = int(ks[i])
-        s = (x + sum(y[j] * int(msgs[i, j]) for j in range(q))) % R
+        k = ks[i] or 1
+        s = x
+        for j in range(q):
+            s += y[j] * msgs[i * q + j]
         e = k * s % R
         if i % bad_every == bad_every - 1:
             e = (e + 1) % R
@@ -241,7 +254,6 @@ def _gen_batch(mode, n, q, seed, bad_every=16):
     s2 = ctypes.create_string_buffer(sb * n)
     oc.oc_gen_mul_mt(sig_group, ctypes.c_size_t(n), b"".join(e1), s1, nth)
     oc.oc_gen_mul_mt(sig_group, ctypes.c_size_t(n), b"".join(e2), s2, nth)
-    mb = b"".join(int(m).to_bytes(48, "big") for m in msgs.reshape(-1))
     return dict(X=X, Y=Y, g_tilde=gtil, s1=s1.raw, s2=s2.raw, msgs=mb, expect=expect)
 
 
