@@ -129,6 +129,28 @@ DEV W14 lz_mont2_kara2(const int32_t a[LN], const int32_t c[LN], const int32_t b
     return r;
 }
 
+
+// variant 3: the shipped product scan with both products on ONE accumulator chain (lz_mont<2> keeps the
+// c d products on a second chain and adds it per column)
+DEV W14 lz_mont2_1chain(const int32_t a[LN], const int32_t b[LN], const int32_t c[LN], const int32_t d[LN]) {
+    int32_t m[LN];
+    W14 r;
+    int64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * LN - 1; k++) {
+#pragma unroll
+        for (int i = 0; i < LN; i++) {
+            const int j = k - i;
+            if (j < 0 || j >= LN) continue;
+            acc += (int64_t)a[i] * b[j];
+            acc += (int64_t)c[i] * d[j];
+        }
+        lz_redc_col(k, acc, m, r.v);
+    }
+    r.v[LN - 1] = (int32_t)acc;
+    return r;
+}
+
 template <int KV>
 DEV W14 f2_mul_kara_v(const W14& x, const W14& y) {
     int32_t xs[LN], b[LN], d[LN];
@@ -139,6 +161,7 @@ DEV W14 f2_mul_kara_v(const W14& x, const W14& y) {
         d[k] = bc_im(y.v[k]);
     }
     neg_re14(d);
+    if (KV == 3) return lz_mont2_1chain(x.v, b, xs, d);
     return KV == 1 ? lz_mont2_kara(x.v, b, xs, d) : lz_mont2_kara2(x.v, b, xs, d);
 }
 static __device__ __noinline__ W14 f2_mul_kara_call(LZ_L14(a), LZ_L14(b)) {
@@ -149,8 +172,13 @@ static __device__ __noinline__ W14 f2_mul_kara2_call(LZ_L14(a), LZ_L14(b)) {
     const W14 A = {{LZ_V14(a)}}, B = {{LZ_V14(b)}};
     return f2_mul_kara_v<2>(A, B);
 }
+static __device__ __noinline__ W14 f2_mul_1chain_call(LZ_L14(a), LZ_L14(b)) {
+    const W14 A = {{LZ_V14(a)}}, B = {{LZ_V14(b)}};
+    return f2_mul_kara_v<3>(A, B);
+}
 template <int KV>
 DEV W14 f2_mul_kara_c(const W14& x, const W14& y) {
+    if (KV == 3) return f2_mul_1chain_call(LZ_E14(x), LZ_E14(y));
     return KV == 1 ? f2_mul_kara_call(LZ_E14(x), LZ_E14(y)) : f2_mul_kara2_call(LZ_E14(x), LZ_E14(y));
 }
 
@@ -192,10 +220,11 @@ __global__ void k_check(uint32_t* bad, int n) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if ((int)(s >> 1) >= n) return;
     const W14 a = seed_w(s * 7 + 1), b = seed_w(s * 13 + 5);
-    const W14 r0 = lz_f2_mul_c(a, b), r1 = f2_mul_kara_c<1>(a, b), r2 = f2_mul_kara_c<2>(a, b);
+    const W14 r0 = lz_f2_mul_c(a, b), r1 = f2_mul_kara_c<1>(a, b), r2 = f2_mul_kara_c<2>(a, b),
+              r3 = f2_mul_kara_c<3>(a, b);
     uint32_t diff = 0;
 #pragma unroll
-    for (int k = 0; k < LN; k++) diff |= (uint32_t)(r0.v[k] ^ r1.v[k]) | (uint32_t)(r0.v[k] ^ r2.v[k]);
+    for (int k = 0; k < LN; k++) diff |= (uint32_t)(r0.v[k] ^ r1.v[k]) | (uint32_t)(r0.v[k] ^ r2.v[k]) | (uint32_t)(r0.v[k] ^ r3.v[k]);
     if (diff) atomicAdd(bad, 1u);
 }
 
@@ -235,9 +264,10 @@ int main() {
     hipMemcpy(&nb, bad, 4, hipMemcpyDeviceToHost);
     printf("{\"device\": \"%s\", \"cus\": %d, \"check_pairs\": %d, \"mismatches\": %u}\n", p.gcnArchName, cus, n, nb);
     for (int rep = 0; rep < 3; rep++) {
-        const double v0 = run<0>(d, cus, 64), v1 = run<1>(d, cus, 64), v2 = run<2>(d, cus, 64);
+        const double v0 = run<0>(d, cus, 256), v1 = run<1>(d, cus, 256), v2 = run<2>(d, cus, 256), v3 = run<3>(d, cus, 256);
         printf("{\"rep\": %d, \"f2_mul_shipped_per_s\": %.4e, \"karatsuba_LH_per_s\": %.4e, \"karatsuba_U_per_s\": %.4e, "
-               "\"ratio_LH\": %.4f, \"ratio_U\": %.4f}\n", rep, v0, v1, v2, v1 / v0, v2 / v0);
+               "\"one_chain_per_s\": %.4e, \"ratio_LH\": %.4f, \"ratio_U\": %.4f, \"ratio_one_chain\": %.4f}\n", rep, v0, v1,
+               v2, v3, v1 / v0, v2 / v0, v3 / v0);
     }
     hipFree(d);
     hipFree(bad);
