@@ -219,6 +219,39 @@ def _max_over_ranks(x, dist, dev):
     return float(t.item())
 
 
+def default_tables_leg(args, ctx, rebind, step, check, n, dev, dist, unit="credentials/s", table_kind="verkey"):
+    """The rate a drop-in caller gets with the library's DEFAULT table widths (cc_set_table_bits(0, 0):
+    verkey tables <= 4 GiB, issuer tables <= 16 GiB), measured in the same run after the headline's
+    timed region: rebind the tables at the default width, one warmup step, then min(args.steps, 10) timed
+    steps bracketed like the headline's (synchronize + barrier, max over ranks); the outputs are checked
+    again (check() must return True)."""
+    import torch
+    world = dist.get_world_size() if dist else 1
+    ctx.set_table_bits(0, 0)
+    t = time.perf_counter()
+    rebind()
+    build_ms = (time.perf_counter() - t) * 1e3
+    k = max(1, min(args.steps, 10))
+    step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    el = _max_over_ranks(time.perf_counter() - t0, dist, dev)
+    if not check():
+        raise SystemExit("default-table outputs disagree with construction — refusing to report a number")
+    bits = ctx.table_bits()
+    return {"value": round(n * world * k / el, 1), "unit": unit, "steps": k, "ms_per_step": round(el / k * 1e3, 3),
+            "table_bits": bits[0] if table_kind == "verkey" else bits[1], "tables": table_kind,
+            "table_build_ms": round(build_ms, 1),
+            "note": "library default widths (cc_set_table_bits(0, 0)): what a drop-in caller gets without opting in"}
+
+
 # ---------------------------------------------------------------- synthetic data (on the GPU)
 def rand_fr(rng):
     return int.from_bytes(rng.bytes(32), "big") % R_ORDER
@@ -473,6 +506,7 @@ def bench_verify(args, mode):
         raise SystemExit("verdicts disagree with construction — refusing to report a number")
     elapsed = _max_over_ranks(elapsed, dist, dev)
     value = n * world * args.steps / elapsed
+    opt_in = table_config(ctx, q)
     # PCIe-inclusive rate: the host-buffer entry point (H2D of the serialized batch + D2H of verdicts);
     # --no-pcie skips it (profiling runs: then every launch of the trace is a warmup or a timed step)
     pcie_rate = None
@@ -483,6 +517,9 @@ def bench_verify(args, mode):
             v = coconut.verify_batch(ctx, n, q, batch["s1"], batch["s2"], batch["msgs"])
         pcie_rate = n * reps / (time.perf_counter() - t)
         assert np.array_equal(v, batch["expect"])
+    dflt = default_tables_leg(args, ctx, lambda: ctx.set_verkey(batch["X"], batch["Y"]), step,
+                              lambda: np.array_equal(d_v.cpu().numpy(), batch["expect"]), n, dev, dist)
+    dflt.update(table_config(ctx, q))
     if rank == 0:
         key = "verify_sigg2_q6_shared_vk" if mode == 0 else "verify_sigg1_q6_shared_vk"
         counts = opcounts(key)
@@ -508,9 +545,10 @@ def bench_verify(args, mode):
             "config": {"workload": f"config2: batch of {n:,} Signature::verify per GPU, msg_count=6, shared "
                                    f"aggregated verkey, {layout}",
                        "credentials_per_gpu": n, "msg_count": q, "parallelism": f"shard-by-credential x{world}",
-                       **table_config(ctx, q), "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
+                       **opt_in, "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
             **lib_info(),
             "pairings_per_s": round(2 * value, 1),
+            "default_tables": dflt,
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),
@@ -525,7 +563,7 @@ def bench_verify(args, mode):
             "pcie_inclusive": {"value": round(pcie_rate, 1) if pcie_rate else None, "unit": "credentials/s",
                                "note": "cc_verify_batch with host buffers: H2D of the serialized batch + D2H "
                                        "of verdicts included (not `value`)"},
-            "setup": {"verkey_tables_ms": round(vk_ms, 1), "verkey_table_bits": ctx.table_bits()[0],
+            "setup": {"verkey_tables_ms": round(vk_ms, 1), "verkey_table_bits": opt_in["verkey_table_bits"],
                       "synthetic_data_s": round(setup_s, 2)},
         }
         if not args.no_cpu_baseline and world == 1:
@@ -600,6 +638,29 @@ def bench_rlc(args):
         raise SystemExit("RLC accepted a corrupted batch — refusing to report a number")
     elapsed = _max_over_ranks(elapsed, dist, dev)
     value = n * world * args.steps / elapsed
+    opt_in = table_config(ctx, q)
+    # one NON-pipelined decision, as a single cc_verify_batch(..., rlc=1) call pays it: partial -> all-gather
+    # -> finish -> accept on the host, nothing overlapped (the finish's one-wave kernels on the critical path)
+    lat = []
+    for _ in range(3 if args.steps else 0):
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        allp, k = gather_partials(eng.partial())
+        if not eng.finish(allp, k):
+            raise SystemExit("RLC rejected an all-valid batch — refusing to report a number")
+        lat.append(time.perf_counter() - t1)
+    single_ms = _max_over_ranks(min(lat), dist, dev) * 1e3 if lat else None
+
+    def rlc_step():
+        allp, k = gather_partials(eng.partial())
+        rlc_step.ok &= eng.finish(allp, k)
+    rlc_step.ok = True
+    dflt = default_tables_leg(args, ctx, lambda: ctx.set_verkey(batch["X"], batch["Y"]), rlc_step,
+                              lambda: rlc_step.ok, n, dev, dist)
+    dflt.update(table_config(ctx, q))
+    dflt["note"] += "; non-pipelined decisions (partial -> all-gather -> finish each step)"
     if rank == 0:
         phase_ms = phase / max(args.steps, 1)
         out = {
@@ -611,8 +672,13 @@ def bench_rlc(args):
             "config": {"workload": "config3: RLC batch verify, msg_count=16, shared verkey, SigG2",
                        "credentials_per_gpu": n, "msg_count": q,
                        "parallelism": f"shard-by-credential x{world} + RCCL all-gather of Fp12 partials",
-                       **table_config(ctx, q), "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
+                       **opt_in, "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
             **lib_info(),
+            "single_call_ms": round(single_ms, 3) if single_ms else None,
+            "single_call_note": "one non-pipelined RLC decision over the rank's credentials (partial -> "
+                                "all-gather -> finish -> host accept; best of 3): the latency a single "
+                                "cc_verify_batch(..., rlc=1) call pays",
+            "default_tables": dflt,
             "phase_ms": {"prep": round(phase_ms[0], 3), "miller": round(phase_ms[1], 3),
                          "reduce": round(phase_ms[2], 3)},
             "us_per_credential": round(elapsed / args.steps / n * 1e6, 4),

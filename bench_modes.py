@@ -250,6 +250,15 @@ def bench_aggregate(args):
     if not ok:
         raise SystemExit("aggregation outputs disagree with construction — refusing to report a number")
     value = n * world * args.steps / el
+    opt_bits = ctx.table_bits()[1]
+    from bench import default_tables_leg
+
+    def agg_ok():
+        return (bytes(o2.cpu().numpy()) == b["want_s2"] and bytes(oX.cpu().numpy()) == b["want_X"] * n
+                and bytes(oY.cpu().numpy()) == b["want_Y"] * n and not ctx.device_error(sh.value))
+    dflt = default_tables_leg(args, ctx, lambda: ctx.set_issuers(b["iss"], b["X"], b["Y"], b["q"]), step, agg_ok,
+                              n, dev, dist, table_kind="issuer")
+    dflt["issuer_table_gib"] = iss_table_gib(dflt["table_bits"], 100 * (q + 1), bool(sigm))
     if rank == 0:
         peak = peak_mad_per_s()
         # phases: Lagrange, Signature::aggregate (Verkey::aggregate runs concurrently on the side stream),
@@ -272,9 +281,10 @@ def bench_aggregate(args):
             "config": {"workload": f"config4: {n:,} credentials per GPU, t=67 of n=100 issuers, msg_count={q}, "
                                    + ("SigG1" if sigm else "SigG2"),
                        "credentials_per_gpu": n, "threshold": t, "issuers": 100,
-                       "parallelism": f"shard-by-credential x{world}", "issuer_table_bits": ctx.table_bits()[1],
-                       "issuer_table_gib": iss_table_gib(ctx.table_bits()[1], 100 * (q + 1), bool(sigm))},
+                       "parallelism": f"shard-by-credential x{world}", "issuer_table_bits": opt_bits,
+                       "issuer_table_gib": iss_table_gib(opt_bits, 100 * (q + 1), bool(sigm))},
             **__import__("bench").lib_info(),
+            "default_tables": dflt,
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 3),
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": round(ach / peak, 4),
@@ -360,6 +370,11 @@ def bench_pok(args):
     if not np.array_equal(d_v.cpu().numpy(), b["expect"]):
         raise SystemExit("PoK verdicts disagree with construction — refusing to report a number")
     value = n * world * args.steps / el
+    from bench import default_tables_leg, table_config
+    opt_in = table_config(ctx, q)
+    dflt = default_tables_leg(args, ctx, lambda: ctx.set_verkey(b["X"], b["Y"]), step,
+                              lambda: np.array_equal(d_v.cpu().numpy(), b["expect"]), n, dev, dist, unit="proofs/s")
+    dflt.update(table_config(ctx, q))
     if rank == 0:
         from bench import kernel_table, cpu_info, kernel_pmc_report
         peak = peak_mad_per_s()
@@ -375,16 +390,17 @@ def bench_pok(args):
             "data": "synthetic (seeded; proofs with known discrete logs built on the GPU; 1/16 bad response)",
             "config": {"workload": f"config5: {n:,} PoKOfSignatureProof::verify per GPU, q=32, revealed "
                                    f"{b['revealed']}, " + ("SigG1" if sigm else "SigG2"), "proofs_per_gpu": n,
-                       "parallelism": f"shard-by-proof x{world}", **__import__("bench").table_config(ctx, q),
+                       "parallelism": f"shard-by-proof x{world}", **opt_in,
                        "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
             **__import__("bench").lib_info(),
+            "default_tables": dflt,
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),
                          "traffic_unit": "HBM-side bytes per launch (PMC, 2 x FETCH_SIZE + WRITE_SIZE)"},
             "kernels": kt,
             "rocprof_kernels": kernel_pmc_report("pok-g1" if sigm else "pok"),
-            "setup": {"synthetic_data_s": round(gen_s, 2), "verkey_table_bits": ctx.table_bits()[0]},
+            "setup": {"synthetic_data_s": round(gen_s, 2), "verkey_table_bits": opt_in["verkey_table_bits"]},
         }
         if not args.no_cpu_baseline and world == 1:
             from bench import _oracle, cpu_pool_rate, cpu_report, host_threads

@@ -1344,6 +1344,9 @@ cc_status cc_aggregate_credential_batch_device(cc_ctx* c, size_t n, size_t len, 
         HIPCK(hipMemsetAsync(c->dev_err.p, 0, 4, st));
     }
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
+    // sigma_1 = sigs[0].sigma_1 (signature.rs:452): depends on neither MSM, so it goes first (behind the
+    // Straus launch's one round of wave slots it waited milliseconds for a free slot)
+    KCK(cck_copy_rows(n, sb, d_s1, len * sb, d_out_s1, st));
     KCK(cck_lagrange(n, len, t, d_ids, c->lag.as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     // the two MSMs share only the Lagrange coefficients: Signature::aggregate first on the caller's
@@ -1357,7 +1360,6 @@ cc_status cc_aggregate_credential_batch_device(cc_ctx* c, size_t n, size_t len, 
     KCK(cck_vk_agg_fixed(oth_group(c->mode), n, len, t, (int)c->iss_q, d_ids, c->lag.as<uint32_t>(),
                          c->iss_ids.as<uint64_t>(), (int)c->iss_n, c->iss_table.as<uint32_t>(), c->iss_wbits,
                          c->iss_inf.as<uint32_t>(), d_outX, d_outY, c->dev_err.as<uint32_t>(), side));
-    KCK(cck_copy_rows(n, sb, d_s1, len * sb, d_out_s1, st));  // sigma_1 = sigs[0].sigma_1 (signature.rs:452)
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     if (side != st) {
         HIPCK(hipEventRecord(c->ev_join, side));
