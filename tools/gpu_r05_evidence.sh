@@ -21,6 +21,11 @@ for m in $MODES; do
   timeout -k 10 600 python bench.py --mode $m --steps $steps --warmup 2 > "$OUT/bench_$m.json" 2> "$OUT/bench_$m.err"
   python3 -c "import json,sys; d=json.loads(open('$OUT/bench_$m.json').read().strip().splitlines()[-1]); print('$m', d['value'], d.get('default_tables',{}).get('value'), d.get('single_call_ms'))"
 done
+for k in ${INFLIGHT:-2 3}; do
+  echo "[ev] bench verify --inflight $k"
+  timeout -k 10 600 python bench.py --mode verify --steps 20 --warmup 2 --inflight $k --no-cpu-baseline > "$OUT/bench_verify_inflight$k.json" 2> "$OUT/bench_verify_inflight$k.err"
+  python3 -c "import json; d=json.loads(open('$OUT/bench_verify_inflight$k.json').read().strip().splitlines()[-1]); print('inflight $k', d['value'], d['ms_per_step'])"
+done
 if [ -x tools/ubench_f2kara ]; then
   echo "[ev] ubench_f2kara"
   timeout -k 10 120 ./tools/ubench_f2kara > "$OUT/ubench_f2kara.jsonl" 2>&1
