@@ -467,20 +467,16 @@ def bench_verify(args, mode):
     ctx.set_table_bits(vk_bits_for(args), 0)
     ctx.set_verkey(batch["X"], batch["Y"])
     vk_ms = (time.perf_counter() - t_vk) * 1e3
-    # --inflight K: K batches in flight, each on its own context (own workspaces and tables) and stream,
-    # steps issued round-robin, so one batch's kernel tails overlap the next batch's first kernels
-    ctxs = [ctx]
-    for _ in range(1, max(1, args.inflight)):
-        c2 = coconut.Context(local, coconut.GroupMode(mode))
-        c2.set_params(batch["g_tilde"])
-        c2.set_table_bits(vk_bits_for(args), 0)
-        c2.set_verkey(batch["X"], batch["Y"])
-        ctxs.append(c2)
+    # --inflight K: K batches in flight on ONE context (cc_set_concurrency: K workspace slots, one set of
+    # verkey tables) and K streams, steps issued round-robin, so one batch's kernel tails overlap the
+    # next batch's kernels
+    K = max(1, args.inflight)
+    ctx.set_concurrency(K)
     setup_s = time.perf_counter() - t_setup
     d_s1, d_s2, d_m = to_dev(batch["s1"], dev), to_dev(batch["s2"], dev), to_dev(batch["msgs"], dev)
-    d_vs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in ctxs]
+    d_vs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(K)]
     d_v = d_vs[0]
-    streams = [torch.cuda.Stream(dev) for _ in ctxs]
+    streams = [torch.cuda.Stream(dev) for _ in range(K)]
     for s_ in streams:
         s_.wait_stream(torch.cuda.current_stream(dev))
     shs = [ctypes.c_void_p(s_.cuda_stream) for s_ in streams]
@@ -489,9 +485,9 @@ def bench_verify(args, mode):
     rr = [0]
 
     def step():
-        k = rr[0] % len(ctxs)
+        k = rr[0] % K
         rr[0] += 1
-        st = lib.cc_verify_batch_device(ctxs[k].h, n, q, ctypes.c_void_p(d_s1.data_ptr()),
+        st = lib.cc_verify_batch_device(ctx.h, n, q, ctypes.c_void_p(d_s1.data_ptr()),
                                         ctypes.c_void_p(d_s2.data_ptr()), ctypes.c_void_p(d_m.data_ptr()),
                                         ctypes.c_void_p(d_vs[k].data_ptr()), None, shs[k])
         if st != 0:
@@ -501,7 +497,7 @@ def bench_verify(args, mode):
         step()
     torch.cuda.synchronize(dev)
     # phase timing (events + a host wait per call) only with one batch in flight: it would serialize them
-    timed_phases = len(ctxs) == 1
+    timed_phases = K == 1
     if timed_phases:
         ctx.timing(True)
     phase = np.zeros(3)
@@ -521,12 +517,12 @@ def bench_verify(args, mode):
     if args.steps + args.warmup == 0:
         step()
         torch.cuda.synchronize(dev)
-    for k in range(len(ctxs)):
+    for k in range(K):
         if rr[0] > k and not np.array_equal(d_vs[k].cpu().numpy(), batch["expect"]):
             raise SystemExit("verdicts disagree with construction — refusing to report a number")
-    for c2 in ctxs[1:]:
-        c2.close()
-    del ctxs[1:]
+    ctx.set_concurrency(1)
+    K = 1
+    rr[0] = 0
     if not timed_phases:  # the per-kernel table from a separate single-batch pass
         ctx.timing(True)
         for _ in range(min(args.steps, 5)):
@@ -575,7 +571,7 @@ def bench_verify(args, mode):
             "config": {"workload": f"config2: batch of {n:,} Signature::verify per GPU, msg_count=6, shared "
                                    f"aggregated verkey, {layout}",
                        "credentials_per_gpu": n, "msg_count": q, "parallelism": f"shard-by-credential x{world}",
-                       "batches_in_flight": len(ctxs),
+                       "batches_in_flight": max(1, args.inflight),
                        **opt_in, "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
             **lib_info(),
             "pairings_per_s": round(2 * value, 1),

@@ -40,6 +40,8 @@ _SIGS = {
     "cc_set_verkey": (c_int, [c_p, c_p, c_p, c_sz]),
     "cc_set_table_bits": (c_int, [c_p, c_int, c_int]),
     "cc_table_bits": (c_int, [c_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "cc_set_concurrency": (c_int, [c_p, c_int]),
+    "cc_concurrency": (c_int, [c_p, ctypes.POINTER(c_int)]),
     "cc_device_error": (c_int, [c_p, c_p, ctypes.POINTER(ctypes.c_uint32)]),
     "cc_verify_batch": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_int]),
     "cc_verify_batch_device": (c_int, [c_p, c_sz, c_sz, c_p, c_p, c_p, c_p, c_p, c_p]),

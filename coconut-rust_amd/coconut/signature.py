@@ -194,6 +194,16 @@ class Context:
         check(lib.cc_set_issuers(self.h, len(ids), q, ctypes.c_void_p(ids.ctypes.data), px, py), "cc_set_issuers")
         self._iss_q = q
 
+    def set_concurrency(self, slots: int):
+        """cc_set_concurrency: K verify batches in flight on K caller streams (workspace slots taken
+        round-robin by the *_device verify calls; 1 = every call ordered against every other)."""
+        check(lib.cc_set_concurrency(self.h, int(slots)), "cc_set_concurrency")
+
+    def concurrency(self) -> int:
+        v = ctypes.c_int(0)
+        check(lib.cc_concurrency(self.h, ctypes.byref(v)), "cc_concurrency")
+        return v.value
+
     def set_table_bits(self, verkey_bits: int = 0, issuer_bits: int = 0):
         """Window widths of the tables later set_verkey / set_issuers calls build (0: by memory)."""
         check(lib.cc_set_table_bits(self.h, verkey_bits, issuer_bits), "cc_set_table_bits")

@@ -134,6 +134,14 @@ struct DevBuf {
     }
 };
 
+// One in-flight verify batch's workspaces (cc_set_concurrency): the prep SoA, flags, Miller values and
+// the per-credential-verkey MSM scratch; `done` marks the end of the slot's last batch on its stream.
+struct VerifySlot {
+    DevBuf prep, flags, fbuf, vkb;
+    hipEvent_t done = nullptr;
+    bool recorded = false;
+};
+
 }  // namespace
 
 struct cc_ctx {
@@ -199,6 +207,15 @@ struct cc_ctx {
     std::vector<cc_ctx*> peers;
     std::vector<ncclComm_t> comms;
     DevBuf rlc_gath;  // per peer: gathered partials (ndev x RLC_PART_WORDS words)
+    // concurrent verify batches (cc_set_concurrency): with K > 1 slots, cc_verify_batch_device /
+    // cc_verify_batch_pervk_device calls take the slots round-robin and are ordered only after the
+    // context's earlier work (tables, params) and the same slot's previous batch, so K batches on K
+    // caller streams overlap.  Slot 0 is the context's own prep / flags / fbuf / vkb; vslots holds
+    // slots 1 .. K-1.  Every other entry point first waits for every slot's last batch.
+    int concurrency = 1;
+    int vslot_next = 0;
+    VerifySlot slot0;  // only its event fields: the buffers are the context's
+    std::vector<VerifySlot*> vslots;
 };
 
 // Every *_device entry point may run on a caller stream while the context's workspaces (prep, flags,
@@ -206,10 +223,25 @@ struct cc_ctx {
 // c->stream.  StreamOrder makes the caller's stream wait for everything already queued on c->stream
 // at entry, and c->stream wait for the call's work at exit, so calls on any mix of streams touch the
 // workspaces in program order (two device calls on different streams are chained through c->stream).
+// stream st waits (on the device) for every concurrent verify slot's last batch
+static void wait_slots(cc_ctx* c, hipStream_t st) {
+    if (c->slot0.recorded) (void)hipStreamWaitEvent(st, c->slot0.done, 0);
+    for (VerifySlot* v : c->vslots)
+        if (v->recorded) (void)hipStreamWaitEvent(st, v->done, 0);
+}
+// the host waits for every concurrent verify slot's last batch (before buffers a slot may still read
+// are freed or rebuilt: tables, params, workspaces)
+static void drain_slots(cc_ctx* c) {
+    if (c->slot0.recorded) (void)hipEventSynchronize(c->slot0.done);
+    for (VerifySlot* v : c->vslots)
+        if (v->recorded) (void)hipEventSynchronize(v->done);
+}
+
 struct StreamOrder {
     cc_ctx* c;
     hipStream_t st;
     StreamOrder(cc_ctx* c_, hipStream_t s) : c(c_), st(s) {
+        wait_slots(c, st);
         if (st != c->stream) {
             (void)hipEventRecord(c->ev_order, c->stream);
             (void)hipStreamWaitEvent(st, c->ev_order, 0);
@@ -324,7 +356,18 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
         return CC_OK;
     }
     (void)hipSetDevice(c->device);
+    drain_slots(c);
     (void)hipStreamSynchronize(c->stream);
+    for (VerifySlot* v : c->vslots) {
+        v->prep.release();
+        v->flags.release();
+        v->fbuf.release();
+        v->vkb.release();
+        if (v->done) (void)hipEventDestroy(v->done);
+        delete v;
+    }
+    c->vslots.clear();
+    if (c->slot0.done) (void)hipEventDestroy(c->slot0.done);
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->gtilde_lz, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->lag,
@@ -483,6 +526,7 @@ cc_status cc_set_params(cc_ctx* c, const uint8_t* g_tilde) {
         !memcmp(c->gtilde_bytes.data(), g_tilde, c->gtilde_bytes.size()))
         return CC_OK;
     HIPCK(hipSetDevice(c->device));
+    drain_slots(c);  // concurrent verify batches read g~ and the tables rebuilt below
     c->have_params = false;  // until the decode below has succeeded
     c->gtilde_bytes.clear();
     int og = oth_group(c->mode);
@@ -545,10 +589,11 @@ cc_status cc_set_verkey(cc_ctx* c, const uint8_t* X, const uint8_t* Y, size_t q)
     if (c->have_vk && c->q == q && c->vk_built_force == c->force_vk_bits && c->vk_bytes == all) return CC_OK;
     // no verkey until every step below has succeeded: a failed call leaves the context refusing
     // verify / RLC / PoK calls with CC_ERR_STATE instead of running on a half-built table
+    HIPCK(hipSetDevice(c->device));
+    drain_slots(c);  // concurrent verify batches read the verkey and its tables
     c->have_vk = false;
     c->q = 0;
     c->vk_bytes.clear();
-    HIPCK(hipSetDevice(c->device));
     if (c->vk_aff.ensure((q + 3) * aw * 4) || c->vk_inf.ensure((q + 3) * 4)) return CC_ERR_HIP;
     cc_status s = decode_points_host(c, og, q + 1, all.data(), c->vk_aff.as<uint32_t>(), c->vk_inf.as<uint32_t>());
     if (s) return s;
@@ -595,6 +640,9 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
 
 static cc_status ensure_work(cc_ctx* c, size_t n) {
     size_t words = n * 12;  // one Fp slot
+    if (c->prep.bytes < words * 4 * PREP_SLOTS || c->flags.bytes < n * 4 || c->fbuf.bytes < words * 4 * 12 ||
+        c->scratch.bytes < (n * 15 * 84 + 72 * 12) * 4 || c->verdicts.bytes < n)
+        drain_slots(c);  // a concurrent batch may still read the buffers about to be reallocated
     // scratch: the PoK prep's per-proof table of d J (15 Jacobian points, <= 15 x 84 words: SigG1's lazy
     // G2 points), and the one-element fexp's (fexp_pl.hip k_fexp1: 72 slots of 12 words); the batched
     // fexp (fexp_q.hip) keeps its chain in registers
@@ -607,22 +655,27 @@ static cc_status ensure_work(cc_ctx* c, size_t n) {
 // the three verify launches on device buffers; timing per phase when enabled.  d_vkX == NULL: the
 // shared verkey's tables; else one verkey per credential (d_vkX n x OtherGroup, d_vkY n x q x
 // OtherGroup; the Straus MSM of pervk.hip, its scratch in c->vkb, sized by the caller)
-static cc_status launch_verify(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s1, const uint8_t* d_s2,
-                               const uint8_t* d_msgs, const uint8_t* d_vkX, const uint8_t* d_vkY, uint8_t* d_verdicts,
-                               uint8_t* d_gt, hipStream_t st) {
+struct VerifyWork {
+    DevBuf *prep, *flags, *fbuf, *vkb;
+};
+static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, const uint8_t* d_s1,
+                               const uint8_t* d_s2, const uint8_t* d_msgs, const uint8_t* d_vkX, const uint8_t* d_vkY,
+                               uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     if (d_vkX)
-        KCK(cck_prep_var(c->mode, n, (int)q, d_s1, d_s2, d_vkX, d_vkY, d_msgs, c->vkb.as<uint32_t>(),
-                         c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), st));
+        KCK(cck_prep_var(c->mode, n, (int)q, d_s1, d_s2, d_vkX, d_vkY, d_msgs, w.vkb->as<uint32_t>(),
+                         w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), st));
     else
         KCK(cck_prep(c->mode, n, (int)q, d_s1, d_s2, d_msgs, c->vk_aff.as<uint32_t>(), c->X_inf,
-                     c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
-                     c->flags.as<uint32_t>(), st));
+                     c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(),
+                     w.flags->as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_lz.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
-    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
+    KCK(cck_miller(c->mode, n, w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), cst, w.fbuf->as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
-    KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(), d_verdicts, d_gt, st));
+    // n = 1 takes the one-element fexp (k_fexp1), whose scratch is the context's: only slot 0 (the
+    // serialized path) uses it, see verify_device
+    KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), c->scratch.as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }
@@ -631,6 +684,88 @@ static void collect_timing(cc_ctx* c) {
     if (!c->timing) return;
     (void)hipEventSynchronize(c->ev[3]);
     for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
+}
+
+// the *_device verify calls: with one slot, ordered against everything on the context (StreamOrder);
+// with K > 1 (cc_set_concurrency), on the next slot round-robin, ordered only after the context
+// stream's queued work (tables, params) and that slot's previous batch.  n = 1 always takes the
+// serialized path (its one-element final exponentiation uses the context's scratch).
+static cc_status verify_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s1, const uint8_t* d_s2,
+                               const uint8_t* d_msgs, const uint8_t* d_vkX, const uint8_t* d_vkY, uint8_t* d_verdicts,
+                               uint8_t* d_gt, hipStream_t st) {
+    const size_t vkw = d_vkX ? cck_prep_var_words(c->mode, n, q) * 4 : 0;
+    if (c->concurrency <= 1 || n == 1) {
+        if (d_vkX && c->vkb.bytes < vkw) drain_slots(c);  // slot 0's batch may still read it
+        StreamOrder order(c, st);
+        if (d_vkX && c->vkb.ensure(vkw)) return CC_ERR_HIP;
+        return launch_verify(c, VerifyWork{&c->prep, &c->flags, &c->fbuf, &c->vkb}, n, q, d_s1, d_s2, d_msgs, d_vkX,
+                             d_vkY, d_verdicts, d_gt, st);
+    }
+    const int k = c->vslot_next;
+    c->vslot_next = (k + 1) % c->concurrency;
+    VerifySlot& sl = k ? *c->vslots[k - 1] : c->slot0;
+    VerifyWork w = k ? VerifyWork{&sl.prep, &sl.flags, &sl.fbuf, &sl.vkb}
+                     : VerifyWork{&c->prep, &c->flags, &c->fbuf, &c->vkb};
+    const size_t words = n * 12;
+    if (w.prep->bytes < words * 4 * PREP_SLOTS || w.flags->bytes < n * 4 || w.fbuf->bytes < words * 4 * 12 ||
+        w.vkb->bytes < vkw) {
+        if (sl.recorded) HIPCK(hipEventSynchronize(sl.done));  // the slot's last batch still reads them
+        if (w.prep->ensure(words * 4 * PREP_SLOTS) || w.flags->ensure(n * 4) || w.fbuf->ensure(words * 4 * 12) ||
+            (vkw && w.vkb->ensure(vkw)))
+            return CC_ERR_HIP;
+    }
+    if (st != c->stream) {  // the context's queued work: tables, params, other entry points
+        HIPCK(hipEventRecord(c->ev_order, c->stream));
+        HIPCK(hipStreamWaitEvent(st, c->ev_order, 0));
+    }
+    if (sl.recorded) HIPCK(hipStreamWaitEvent(st, sl.done, 0));
+    cc_status s = launch_verify(c, w, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
+    if (s) return s;
+    HIPCK(hipEventRecord(sl.done, st));
+    sl.recorded = true;
+    return CC_OK;
+}
+
+cc_status cc_set_concurrency(cc_ctx* c, int slots) {
+    if (!c || slots < 1 || slots > 8) return CC_ERR_DECODE;
+    for (cc_ctx* p : c->peers) {
+        cc_status s = cc_set_concurrency(p, slots);
+        if (s) return s;
+    }
+    if (!c->peers.empty()) {
+        c->concurrency = slots;
+        return CC_OK;
+    }
+    HIPCK(hipSetDevice(c->device));
+    drain_slots(c);
+    if (!c->slot0.done) HIPCK(hipEventCreateWithFlags(&c->slot0.done, hipEventDisableTiming));
+    while ((int)c->vslots.size() > slots - 1) {
+        VerifySlot* v = c->vslots.back();
+        c->vslots.pop_back();
+        v->prep.release();
+        v->flags.release();
+        v->fbuf.release();
+        v->vkb.release();
+        if (v->done) (void)hipEventDestroy(v->done);
+        delete v;
+    }
+    while ((int)c->vslots.size() < slots - 1) {
+        VerifySlot* v = new VerifySlot;
+        if (hipEventCreateWithFlags(&v->done, hipEventDisableTiming) != hipSuccess) {
+            delete v;
+            return CC_ERR_HIP;
+        }
+        c->vslots.push_back(v);
+    }
+    c->concurrency = slots;
+    c->vslot_next = 0;
+    return CC_OK;
+}
+
+cc_status cc_concurrency(const cc_ctx* c, int* slots) {
+    if (!c || !slots) return CC_ERR_DECODE;
+    *slots = c->concurrency;
+    return CC_OK;
 }
 
 cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s1, const uint8_t* d_s2,
@@ -644,10 +779,7 @@ cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d
     cc_status s = ensure_work(c, n);
     if (s) return s;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    {
-        StreamOrder order(c, st);
-        s = launch_verify(c, n, q, d_s1, d_s2, d_msgs, nullptr, nullptr, d_verdicts, d_gt, st);
-    }
+    s = verify_device(c, n, q, d_s1, d_s2, d_msgs, nullptr, nullptr, d_verdicts, d_gt, st);
     if (s) return s;
     if (c->timing) collect_timing(c);
     return CC_OK;
@@ -665,11 +797,7 @@ cc_status cc_verify_batch_pervk_device(cc_ctx* c, size_t n, size_t q, const uint
     cc_status s = ensure_work(c, n);
     if (s) return s;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    {
-        StreamOrder order(c, st);
-        if (c->vkb.ensure(cck_prep_var_words(c->mode, n, q) * 4)) return CC_ERR_HIP;
-        s = launch_verify(c, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
-    }
+    s = verify_device(c, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
     if (s) return s;
     if (c->timing) collect_timing(c);
     return CC_OK;
@@ -693,6 +821,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
     if (q != c->q) return CC_ERR_LEN;
     HIPCK(hipSetDevice(c->device));
+    drain_slots(c);  // concurrent verify batches (cc_set_concurrency) use buffers rebuilt here
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     StreamOrder order(c, st);
     if (!n) {
@@ -837,6 +966,7 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
     if (!n) return CC_OK;
     if (!c->peers.empty()) return multi_verify(c, n, q, s1, s2, msgs, vkX, vkY, verdicts, gt, rlc);
     HIPCK(hipSetDevice(c->device));
+    drain_slots(c);  // concurrent device batches still using slot 0's workspaces (cc_set_concurrency)
     size_t sb = (size_t)sig_bytes(c->mode), ob = (size_t)oth_bytes(c->mode);
     if (c->in_s1.ensure(n * sb) || c->in_s2.ensure(n * sb) || c->in_msgs.ensure(n * q * 48 + 16) ||
         c->verdicts.ensure(n) || (gt && c->gt.ensure(n * 576)))
@@ -866,9 +996,10 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
         HIPCK(hipMemcpyAsync(c->in_vkX.p, vkX, n * ob, hipMemcpyHostToDevice, st));
         if (q) HIPCK(hipMemcpyAsync(c->in_vkY.p, vkY, n * q * ob, hipMemcpyHostToDevice, st));
     }
-    s = launch_verify(c, n, q, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), d_msgs,
-                      per_vk ? c->in_vkX.as<uint8_t>() : nullptr, per_vk ? c->in_vkY.as<uint8_t>() : nullptr,
-                      c->verdicts.as<uint8_t>(), gt ? c->gt.as<uint8_t>() : nullptr, st);
+    s = launch_verify(c, VerifyWork{&c->prep, &c->flags, &c->fbuf, &c->vkb}, n, q, c->in_s1.as<uint8_t>(),
+                      c->in_s2.as<uint8_t>(), d_msgs, per_vk ? c->in_vkX.as<uint8_t>() : nullptr,
+                      per_vk ? c->in_vkY.as<uint8_t>() : nullptr, c->verdicts.as<uint8_t>(),
+                      gt ? c->gt.as<uint8_t>() : nullptr, st);
     if (s) return s;
     HIPCK(hipMemcpyAsync(verdicts, c->verdicts.p, n, hipMemcpyDeviceToHost, st));
     if (gt) HIPCK(hipMemcpyAsync(gt, c->gt.p, n * 576, hipMemcpyDeviceToHost, st));
@@ -1222,6 +1353,7 @@ cc_status cc_set_issuers(cc_ctx* c, size_t n_iss, size_t q, const uint64_t* ids,
     c->iss_q = 0;
     c->iss_ids_host.clear();
     HIPCK(hipSetDevice(c->device));
+    drain_slots(c);  // concurrent verify batches (cc_set_concurrency) use buffers rebuilt here
     const int og = oth_group(c->mode);
     const size_t ob = (size_t)oth_bytes(c->mode), aw = aff_words(og);
     // rows sorted by id; ids must be unique (they are the signers' Shamir x-coordinates)

@@ -118,6 +118,17 @@ cc_status cc_verify_batch_pervk_device(cc_ctx* ctx, size_t n, size_t q, const ui
                                        const uint8_t* d_vk_Y, uint8_t* d_verdicts, uint8_t* d_gt_or_null,
                                        void* stream);
 
+/* Concurrent verify batches on one context: with `slots` = K > 1, cc_verify_batch_device and
+ * cc_verify_batch_pervk_device calls take K workspace slots round-robin (each slot its own prep SoA,
+ * flags and Miller values; the verkey tables are shared) and are ordered only after the context's
+ * earlier work (tables, params) and the same slot's previous batch — so K batches issued on K caller
+ * streams overlap on the device (one batch's kernel tails with the next batch's kernels).  Every other
+ * entry point, and cc_set_params / cc_set_verkey, first waits for the slots' batches.  The per-phase
+ * timing (cc_last_timing) is meaningful with one slot only.  slots: 1 (default, every call ordered
+ * against every other) .. 8.  cc_concurrency reports the current value. */
+cc_status cc_set_concurrency(cc_ctx* ctx, int slots);
+cc_status cc_concurrency(const cc_ctx* ctx, int* slots);
+
 /* RLC batch mode, multi-GPU form.  Each GPU reduces its shard to one partial of
  * CC_RLC_PARTIAL_WORDS u32 (= cc_rlc_partial_words(): the Fp12 Miller product in the library's
  * Montgomery words, a fall-back flag, and the shard's 16 fold window sums, affine with identity

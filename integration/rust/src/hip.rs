@@ -33,6 +33,9 @@ extern "C" {
     pub fn cc_set_table_bits(ctx: *mut CcCtx, verkey_bits: c_int, issuer_bits: c_int) -> c_int;
     pub fn cc_table_bits(ctx: *const CcCtx, verkey_bits: *mut c_int, issuer_bits: *mut c_int) -> c_int;
     pub fn cc_device_error(ctx: *mut CcCtx, stream: *mut c_void, out: *mut u32) -> c_int;
+    // concurrent verify batches on one context (K workspace slots, round-robin; K caller streams)
+    pub fn cc_set_concurrency(ctx: *mut CcCtx, slots: c_int) -> c_int;
+    pub fn cc_concurrency(ctx: *const CcCtx, slots: *mut c_int) -> c_int;
     // RLC partial: CC_RLC_PARTIAL_WORDS (929) u32 = Fp12 product, flag, 16 window sums
     pub fn cc_rlc_partial_words() -> c_int;
     pub fn cc_rlc_partial_device(ctx: *mut CcCtx, n: usize, q: usize, base_index: u64, seed32: *const u8,

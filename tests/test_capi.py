@@ -54,6 +54,8 @@ def test_null_and_bad_arguments_rejected_without_gpu():
     assert lib.cc_ctx_create(0, 7, None) == -4        # bad mode / null out
     assert lib.cc_verify_batch(None, 1, 6, None, None, None, None, None, None, None, 0) == -4
     assert lib.cc_set_params(None, None) == -4
+    assert lib.cc_set_concurrency(None, 2) == -4
+    assert lib.cc_concurrency(None, None) == -4
 
 
 def test_ctx_create_without_gpu_fails_loudly():

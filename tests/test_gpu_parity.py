@@ -418,3 +418,81 @@ def test_rlc_partials_gathered_across_shards(ctxs, mode):
     i = 3 * n // 4 + 5  # inside shard 3: swap in another credential's sigma_2
     bad[i * sb:(i + 1) * sb] = s2[(i + 1) * sb:(i + 2) * sb]
     assert not run(bad)
+
+
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_concurrent_verify_slots(ctxs, mode):
+    """cc_set_concurrency(3): six cc_verify_batch_device calls on three caller streams with no host
+    synchronisation in between (each slot reused twice, batches of different sizes so a slot's buffers
+    grow while the other slots' batches run), an n = 1 call (the serialized path) in the middle, then a
+    host-buffer call and a set_verkey rebind that must wait for the slots; every verdict equals
+    construction.  Then the per-credential-verkey fixture through cc_verify_batch_pervk_device on two
+    streams.  The context is returned to one slot."""
+    import torch
+    from coconut import _lib, verify_batch
+    m = MODES[mode]
+    q = 6
+    ctx = ctxs[mode]
+    b = _gen_batch(m, 1024, q, seed=2024 + m, bad_every=7)
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    sb = 192 if m == 0 else 97
+    dev = torch.device("cuda", 0)
+    to = lambda x: torch.frombuffer(bytearray(x), dtype=torch.uint8).to(dev)  # noqa: E731
+    P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    d1, d2, dm = to(b["s1"]), to(b["s2"]), to(b["msgs"])
+    ctx.set_concurrency(3)
+    try:
+        assert ctx.concurrency() == 3
+        streams = [torch.cuda.Stream(dev) for _ in range(3)]
+        torch.cuda.synchronize()
+        sizes = [256, 512, 1024, 1024, 1, 768, 1024]
+        outs = []
+        for k, n in enumerate(sizes):
+            v = torch.zeros(n, dtype=torch.uint8, device=dev)
+            st = streams[k % 3]
+            st.wait_stream(torch.cuda.current_stream(dev))  # v's zero fill
+            assert _lib.lib.cc_verify_batch_device(ctx.h, n, q, P(d1), P(d2), P(dm), P(v), None,
+                                                   ctypes.c_void_p(st.cuda_stream)) == 0
+            v.record_stream(st)
+            outs.append((n, v))
+        vh = verify_batch(ctx, 1024, q, b["s1"], b["s2"], b["msgs"])  # host path: waits for the slots
+        assert np.array_equal(vh, b["expect"])
+        torch.cuda.synchronize()
+        for n, v in outs:
+            assert np.array_equal(v.cpu().numpy(), b["expect"][:n]), n
+        # a verkey rebind while batches are in flight: the rebuild waits for them, later batches see it
+        v0 = torch.zeros(1024, dtype=torch.uint8, device=dev)
+        assert _lib.lib.cc_verify_batch_device(ctx.h, 1024, q, P(d1), P(d2), P(dm), P(v0), None,
+                                               ctypes.c_void_p(streams[0].cuda_stream)) == 0
+        b2 = _gen_batch(m, 512, q, seed=4048 + m, bad_every=5)
+        ctx.set_verkey(b2["X"], b2["Y"])
+        ctx.set_params(b2["g_tilde"])
+        e1, e2, em = to(b2["s1"]), to(b2["s2"]), to(b2["msgs"])
+        v1 = torch.zeros(512, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        assert _lib.lib.cc_verify_batch_device(ctx.h, 512, q, P(e1), P(e2), P(em), P(v1), None,
+                                               ctypes.c_void_p(streams[1].cuda_stream)) == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(v0.cpu().numpy(), b["expect"])
+        assert np.array_equal(v1.cpu().numpy(), b2["expect"])
+        # per-credential verkeys on two streams
+        d = golden(f"verify_{mode.lower()}_q6_pervk.json")
+        ctx.set_params(bytes.fromhex(d["g_tilde"]))
+        cr = d["creds"]
+        n = len(cr)
+        D = [to(_cat(c[k] for c in cr)) for k in ("sigma1", "sigma2")]
+        D.append(to(_cat(mm for c in cr for mm in c["msgs"])))
+        D.append(to(_cat(c["vk"]["X"] for c in cr)))
+        D.append(to(_cat(y for c in cr for y in c["vk"]["Y"])))
+        vs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+        torch.cuda.synchronize()
+        for k in range(2):
+            assert _lib.lib.cc_verify_batch_pervk_device(ctx.h, n, q, *[P(x) for x in D], P(vs[k]), None,
+                                                         ctypes.c_void_p(streams[k].cuda_stream)) == 0
+        torch.cuda.synchronize()
+        for v in vs:
+            assert list(v.cpu().numpy()) == [c["verdict"] for c in cr]
+    finally:
+        ctx.set_concurrency(1)
+    assert ctx.concurrency() == 1
