@@ -219,12 +219,14 @@ def _max_over_ranks(x, dist, dev):
     return float(t.item())
 
 
-def default_tables_leg(args, ctx, rebind, step, check, n, dev, dist, unit="credentials/s", table_kind="verkey"):
+def default_tables_leg(args, ctx, rebind, step, check, n, dev, dist, unit="credentials/s", table_kind="verkey",
+                       run_k=None):
     """The rate a drop-in caller gets with the library's DEFAULT table widths (cc_set_table_bits(0, 0):
     verkey tables <= 4 GiB, issuer tables <= 16 GiB), measured in the same run after the headline's
     timed region: rebind the tables at the default width, one warmup step, then min(args.steps, 10) timed
     steps bracketed like the headline's (synchronize + barrier, max over ranks); the outputs are checked
-    again (check() must return True)."""
+    again (check() must return True).  run_k(k), when given, runs k steps itself (the RLC's pipelined
+    loop) in place of k calls of step()."""
     import torch
     world = dist.get_world_size() if dist else 1
     ctx.set_table_bits(0, 0)
@@ -232,13 +234,16 @@ def default_tables_leg(args, ctx, rebind, step, check, n, dev, dist, unit="crede
     rebind()
     build_ms = (time.perf_counter() - t) * 1e3
     k = max(1, min(args.steps, 10))
-    step()
+    if run_k is None:
+        def run_k(kk):
+            for _ in range(kk):
+                step()
+    run_k(1)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(k):
-        step()
+    run_k(k)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -680,14 +685,14 @@ def bench_rlc(args):
         lat.append(time.perf_counter() - t1)
     single_ms = _max_over_ranks(min(lat), dist, dev) * 1e3 if lat else None
 
-    def rlc_step():
-        allp, k = gather_partials(eng.partial())
-        rlc_step.ok &= eng.finish(allp, k)
-    rlc_step.ok = True
-    dflt = default_tables_leg(args, ctx, lambda: ctx.set_verkey(batch["X"], batch["Y"]), rlc_step,
-                              lambda: rlc_step.ok, n, dev, dist)
+    ok_dflt = [True]
+
+    def run_dflt(k_steps):
+        ok_dflt[0] &= run(k_steps)
+    dflt = default_tables_leg(args, ctx, lambda: ctx.set_verkey(batch["X"], batch["Y"]), None,
+                              lambda: ok_dflt[0], n, dev, dist, run_k=run_dflt)
     dflt.update(table_config(ctx, q))
-    dflt["note"] += "; non-pipelined decisions (partial -> all-gather -> finish each step)"
+    dflt["note"] += "; pipelined as the headline (finish of batch i under the partial of batch i + 1)"
     if rank == 0:
         phase_ms = phase / max(args.steps, 1)
         out = {
