@@ -784,8 +784,9 @@ def main():
     ap.add_argument("--vk-bits", type=int, default=None,
                     help="verkey table window width (cc_set_table_bits; 0 = the library's <= 4 GiB default; "
                          "unset = the mode's opt-in width, BENCH_VK_BITS)")
-    ap.add_argument("--inflight", type=int, default=1,
-                    help="verify modes: batches in flight (one context + stream each, issued round-robin)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="verify modes: batches in flight on one context (cc_set_concurrency slots) and as many "
+                         "streams, issued round-robin; 1 = each batch ordered after the previous one")
     ap.add_argument("--mode", choices=["verify", "verify-g1", "verify-pervk", "verify-pervk-g1", "rlc", "aggregate",
                                        "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
     args = ap.parse_args()
