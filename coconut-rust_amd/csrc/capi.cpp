@@ -137,7 +137,7 @@ struct DevBuf {
 // One in-flight verify batch's workspaces (cc_set_concurrency): the prep SoA, flags, Miller values and
 // the per-credential-verkey MSM scratch; `done` marks the end of the slot's last batch on its stream.
 struct VerifySlot {
-    DevBuf prep, flags, fbuf, vkb;
+    DevBuf prep, flags, fbuf, vkb, scratch, idx;  // scratch, idx: PoK (the d J tables, the revealed indices)
     hipEvent_t done = nullptr;
     bool recorded = false;
 };
@@ -363,6 +363,8 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
         v->flags.release();
         v->fbuf.release();
         v->vkb.release();
+        v->scratch.release();
+        v->idx.release();
         if (v->done) (void)hipEventDestroy(v->done);
         delete v;
     }
@@ -656,8 +658,9 @@ static cc_status ensure_work(cc_ctx* c, size_t n) {
 // shared verkey's tables; else one verkey per credential (d_vkX n x OtherGroup, d_vkY n x q x
 // OtherGroup; the Straus MSM of pervk.hip, its scratch in c->vkb, sized by the caller)
 struct VerifyWork {
-    DevBuf *prep, *flags, *fbuf, *vkb;
+    DevBuf *prep, *flags, *fbuf, *vkb, *scratch, *idx;
 };
+static VerifyWork ctx_work(cc_ctx* c) { return {&c->prep, &c->flags, &c->fbuf, &c->vkb, &c->scratch, &c->pok_idx}; }
 static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, const uint8_t* d_s1,
                                const uint8_t* d_s2, const uint8_t* d_msgs, const uint8_t* d_vkX, const uint8_t* d_vkY,
                                uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
@@ -673,9 +676,9 @@ static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t 
     const uint32_t* cst = c->mode == 0 ? c->gtilde_lz.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
     KCK(cck_miller(c->mode, n, w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), cst, w.fbuf->as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
-    // n = 1 takes the one-element fexp (k_fexp1), whose scratch is the context's: only slot 0 (the
-    // serialized path) uses it, see verify_device
-    KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), c->scratch.as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt, st));
+    // n = 1 takes the one-element fexp (k_fexp1), whose scratch is the context's: only the serialized
+    // path uses it (verify_device)
+    KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }
@@ -684,6 +687,38 @@ static void collect_timing(cc_ctx* c) {
     if (!c->timing) return;
     (void)hipEventSynchronize(c->ev[3]);
     for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
+}
+
+// The next concurrent slot (round-robin): its workspaces grown to n credentials (vkw bytes of per-verkey
+// MSM scratch, scratch_bytes of PoK tables, idx_bytes of revealed indices) once its last batch is done,
+// and stream st ordered after the context stream's queued work (tables, params, other entry points) and
+// after that last batch.  slot_end records the slot's completion on st.
+static cc_status slot_begin(cc_ctx* c, hipStream_t st, size_t n, size_t vkw, size_t scratch_bytes, size_t idx_bytes,
+                            VerifySlot*& sl, VerifyWork& w) {
+    const int k = c->vslot_next;
+    c->vslot_next = (k + 1) % c->concurrency;
+    sl = k ? c->vslots[k - 1] : &c->slot0;
+    w = k ? VerifyWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->vkb, &sl->scratch, &sl->idx} : ctx_work(c);
+    const size_t words = n * 12;
+    if (w.prep->bytes < words * 4 * PREP_SLOTS || w.flags->bytes < n * 4 || w.fbuf->bytes < words * 4 * 12 ||
+        w.vkb->bytes < vkw || w.scratch->bytes < scratch_bytes || w.idx->bytes < idx_bytes) {
+        if (sl->recorded) HIPCK(hipEventSynchronize(sl->done));  // the slot's last batch still reads them
+        if (w.prep->ensure(words * 4 * PREP_SLOTS) || w.flags->ensure(n * 4) || w.fbuf->ensure(words * 4 * 12) ||
+            (vkw && w.vkb->ensure(vkw)) || (scratch_bytes && w.scratch->ensure(scratch_bytes)) ||
+            (idx_bytes && w.idx->ensure(idx_bytes)))
+            return CC_ERR_HIP;
+    }
+    if (st != c->stream) {
+        HIPCK(hipEventRecord(c->ev_order, c->stream));
+        HIPCK(hipStreamWaitEvent(st, c->ev_order, 0));
+    }
+    if (sl->recorded) HIPCK(hipStreamWaitEvent(st, sl->done, 0));
+    return CC_OK;
+}
+static cc_status slot_end(hipStream_t st, VerifySlot* sl) {
+    HIPCK(hipEventRecord(sl->done, st));
+    sl->recorded = true;
+    return CC_OK;
 }
 
 // the *_device verify calls: with one slot, ordered against everything on the context (StreamOrder);
@@ -698,32 +733,15 @@ static cc_status verify_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s
         if (d_vkX && c->vkb.bytes < vkw) drain_slots(c);  // slot 0's batch may still read it
         StreamOrder order(c, st);
         if (d_vkX && c->vkb.ensure(vkw)) return CC_ERR_HIP;
-        return launch_verify(c, VerifyWork{&c->prep, &c->flags, &c->fbuf, &c->vkb}, n, q, d_s1, d_s2, d_msgs, d_vkX,
-                             d_vkY, d_verdicts, d_gt, st);
+        return launch_verify(c, ctx_work(c), n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
     }
-    const int k = c->vslot_next;
-    c->vslot_next = (k + 1) % c->concurrency;
-    VerifySlot& sl = k ? *c->vslots[k - 1] : c->slot0;
-    VerifyWork w = k ? VerifyWork{&sl.prep, &sl.flags, &sl.fbuf, &sl.vkb}
-                     : VerifyWork{&c->prep, &c->flags, &c->fbuf, &c->vkb};
-    const size_t words = n * 12;
-    if (w.prep->bytes < words * 4 * PREP_SLOTS || w.flags->bytes < n * 4 || w.fbuf->bytes < words * 4 * 12 ||
-        w.vkb->bytes < vkw) {
-        if (sl.recorded) HIPCK(hipEventSynchronize(sl.done));  // the slot's last batch still reads them
-        if (w.prep->ensure(words * 4 * PREP_SLOTS) || w.flags->ensure(n * 4) || w.fbuf->ensure(words * 4 * 12) ||
-            (vkw && w.vkb->ensure(vkw)))
-            return CC_ERR_HIP;
-    }
-    if (st != c->stream) {  // the context's queued work: tables, params, other entry points
-        HIPCK(hipEventRecord(c->ev_order, c->stream));
-        HIPCK(hipStreamWaitEvent(st, c->ev_order, 0));
-    }
-    if (sl.recorded) HIPCK(hipStreamWaitEvent(st, sl.done, 0));
-    cc_status s = launch_verify(c, w, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
+    VerifySlot* sl = nullptr;
+    VerifyWork w;
+    cc_status s = slot_begin(c, st, n, vkw, 0, 0, sl, w);
     if (s) return s;
-    HIPCK(hipEventRecord(sl.done, st));
-    sl.recorded = true;
-    return CC_OK;
+    s = launch_verify(c, w, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
+    if (s) return s;
+    return slot_end(st, sl);
 }
 
 cc_status cc_set_concurrency(cc_ctx* c, int slots) {
@@ -746,6 +764,8 @@ cc_status cc_set_concurrency(cc_ctx* c, int slots) {
         v->flags.release();
         v->fbuf.release();
         v->vkb.release();
+        v->scratch.release();
+        v->idx.release();
         if (v->done) (void)hipEventDestroy(v->done);
         delete v;
     }
@@ -1559,20 +1579,20 @@ static cc_status check_revealed(size_t q, size_t r, const uint64_t* rev_idx, std
     return CC_OK;
 }
 
-static cc_status launch_pok(cc_ctx* c, size_t n, size_t q, size_t r, const uint8_t* d_s1, const uint8_t* d_s2,
-                            const uint8_t* d_J, const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal,
-                            const uint32_t* d_idx, const uint8_t* d_rev_msgs, uint8_t* d_verdicts, uint8_t* d_gt,
-                            hipStream_t st) {
+static cc_status launch_pok(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, size_t r, const uint8_t* d_s1,
+                            const uint8_t* d_s2, const uint8_t* d_J, const uint8_t* d_T, const uint8_t* d_resp,
+                            const uint8_t* d_chal, const uint32_t* d_idx, const uint8_t* d_rev_msgs, uint8_t* d_verdicts,
+                            uint8_t* d_gt, hipStream_t st) {
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     KCK(cck_prep_pok(c->mode, n, (int)q, (int)r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_idx,
                      c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(), c->wbits,
-                     c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(), c->flags.as<uint32_t>(),
-                     c->scratch.as<uint32_t>(), st));  // J*chal window table: the fexp scratch, free until fexp
+                     c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(), w.flags->as<uint32_t>(),
+                     w.scratch->as<uint32_t>(), st));  // J*chal window table: the fexp scratch, free until fexp
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     const uint32_t* cst = c->mode == 0 ? c->gtilde_lz.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
-    KCK(cck_miller(c->mode, n, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), cst, c->fbuf.as<uint32_t>(), st));
+    KCK(cck_miller(c->mode, n, w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), cst, w.fbuf->as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
-    KCK(cck_fexp(n, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->flags.as<uint32_t>(), d_verdicts, d_gt, st));
+    KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }
@@ -1593,14 +1613,26 @@ cc_status cc_pok_verify_batch_device(cc_ctx* c, size_t n, size_t q, size_t r, si
     if (nresp != q - r + 1) return CC_ERR_BASES_EXPS;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (c->concurrency > 1) {  // the next concurrency slot (cc_set_concurrency): its own tables of d J
+        VerifySlot* sl = nullptr;
+        VerifyWork w;
+        s = slot_begin(c, st, n, 0, (n * 15 * 84 + 72 * 12) * 4, idx.size() * 4 + 4, sl, w);
+        if (s) return s;
+        // pageable host memory: the copy is staged before the call returns, so idx may go out of scope
+        if (r) HIPCK(hipMemcpyAsync(w.idx->p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, st));
+        s = launch_pok(c, w, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, w.idx->as<uint32_t>(), d_rev_msgs,
+                       d_verdicts, d_gt, st);
+        if (s) return s;
+        return slot_end(st, sl);
+    }
     s = ensure_work(c, n);
     if (s) return s;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     StreamOrder order(c, st);
     if (c->pok_idx.ensure(idx.size() * 4)) return CC_ERR_HIP;
     HIPCK(hipMemcpyAsync(c->pok_idx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, st));
-    s = launch_pok(c, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, c->pok_idx.as<uint32_t>(), d_rev_msgs, d_verdicts,
-                   d_gt, st);
+    s = launch_pok(c, ctx_work(c), n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, c->pok_idx.as<uint32_t>(), d_rev_msgs,
+                   d_verdicts, d_gt, st);
     if (s) return s;
     if (c->timing) collect_timing(c);
     return CC_OK;
@@ -1621,6 +1653,7 @@ cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nr
     if (nresp != q - r + 1) return CC_ERR_BASES_EXPS;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
+    drain_slots(c);  // concurrent device batches still using slot 0's workspaces (cc_set_concurrency)
     size_t sb = (size_t)sig_bytes(c->mode), ob = (size_t)oth_bytes(c->mode);
     hipStream_t st = c->stream;
     DevBuf& dJ = c->in_aux[0];
@@ -1645,7 +1678,7 @@ cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nr
         HIPCK(hipMemcpyAsync(dM.p, rev_msgs, n * r * 48, hipMemcpyHostToDevice, st));
         HIPCK(hipMemcpyAsync(dI.p, idx.data(), r * 4, hipMemcpyHostToDevice, st));
     }
-    s = launch_pok(c, n, q, r, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), dJ.as<uint8_t>(), dT.as<uint8_t>(),
+    s = launch_pok(c, ctx_work(c), n, q, r, c->in_s1.as<uint8_t>(), c->in_s2.as<uint8_t>(), dJ.as<uint8_t>(), dT.as<uint8_t>(),
                    dR.as<uint8_t>(), dC.as<uint8_t>(), dI.as<uint32_t>(), dM.as<uint8_t>(), c->verdicts.as<uint8_t>(),
                    gt ? c->gt.as<uint8_t>() : nullptr, st);
     if (s) return s;

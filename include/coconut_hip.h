@@ -118,11 +118,12 @@ cc_status cc_verify_batch_pervk_device(cc_ctx* ctx, size_t n, size_t q, const ui
                                        const uint8_t* d_vk_Y, uint8_t* d_verdicts, uint8_t* d_gt_or_null,
                                        void* stream);
 
-/* Concurrent verify batches on one context: with `slots` = K > 1, cc_verify_batch_device and
- * cc_verify_batch_pervk_device calls take K workspace slots round-robin (each slot its own prep SoA,
- * flags and Miller values; the verkey tables are shared) and are ordered only after the context's
- * earlier work (tables, params) and the same slot's previous batch — so K batches issued on K caller
- * streams overlap on the device (one batch's kernel tails with the next batch's kernels).  Every other
+/* Concurrent verify batches on one context: with `slots` = K > 1, cc_verify_batch_device,
+ * cc_verify_batch_pervk_device and cc_pok_verify_batch_device calls take K workspace slots round-robin
+ * (each slot its own prep SoA, flags, Miller values and PoK d J tables; the verkey tables are shared)
+ * and are ordered only after the context's earlier work (tables, params) and the same slot's previous
+ * batch — so K batches issued on K caller streams overlap on the device (one batch's kernel tails with
+ * the next batch's kernels).  An n = 1 verify call takes the serialized path.  Every other
  * entry point, and cc_set_params / cc_set_verkey, first waits for the slots' batches.  The per-phase
  * timing (cc_last_timing) is meaningful with one slot only.  slots: 1 (default, every call ordered
  * against every other) .. 8.  cc_concurrency reports the current value. */

@@ -496,3 +496,56 @@ def test_concurrent_verify_slots(ctxs, mode):
     finally:
         ctx.set_concurrency(1)
     assert ctx.concurrency() == 1
+
+
+@pytest.mark.parametrize("name", ["pok_g2_q32.json", "pok_g1_q6.json"])
+def test_concurrent_pok_slots(ctxs, name):
+    """cc_pok_verify_batch_device under cc_set_concurrency(2): four calls on two streams (each slot its
+    own d J tables and revealed-index buffer), alternating the fixture with a copy whose responses are
+    all corrupted, no synchronisation in between; every verdict and GT equals the fixture's."""
+    import torch
+    from coconut import _lib
+    d = golden(name)
+    ctx = ctxs[d["mode"]]
+    ctx.set_params(bytes.fromhex(d["g_tilde"]))
+    ctx.set_verkey(bytes.fromhex(d["vk"]["X"]), [bytes.fromhex(y) for y in d["vk"]["Y"]])
+    pr = d["proofs"]
+    n, q, r = len(pr), d["q"], len(d["revealed"])
+    nresp = len(pr[0]["responses"])
+    dev = torch.device("cuda", 0)
+    to = lambda x: torch.frombuffer(bytearray(x), dtype=torch.uint8).to(dev)  # noqa: E731
+    P = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    resp = _cat(x for p in pr for x in p["responses"])
+    bad_resp = bytearray(resp)
+    for i in range(n):  # the last response's low byte of every proof
+        bad_resp[(i * nresp + nresp) * 48 - 1] ^= 1
+    D = {k: to(_cat(p[k] for p in pr)) for k in ("sigma1", "sigma2", "J", "T", "chal")}
+    D["rev"] = to(_cat(m for p in pr for m in p["revealed_msgs"]))
+    R = [to(resp), to(bytes(bad_resp))]
+    ridx = (ctypes.c_uint64 * max(r, 1))(*d["revealed"])
+    ctx.set_concurrency(2)
+    try:
+        streams = [torch.cuda.Stream(dev) for _ in range(2)]
+        outs = []
+        torch.cuda.synchronize()
+        for k in range(4):
+            v = torch.zeros(n, dtype=torch.uint8, device=dev)
+            gt = torch.zeros(n * 576, dtype=torch.uint8, device=dev)
+            st = streams[k % 2]
+            st.wait_stream(torch.cuda.current_stream(dev))
+            assert _lib.lib.cc_pok_verify_batch_device(ctx.h, n, q, r, nresp, P(D["sigma1"]), P(D["sigma2"]), P(D["J"]),
+                                                       P(D["T"]), P(R[k % 2]), P(D["chal"]), ridx, P(D["rev"]), P(v),
+                                                       P(gt), ctypes.c_void_p(st.cuda_stream)) == 0
+            outs.append((k % 2, v, gt))
+        torch.cuda.synchronize()
+        for bad, v, gt in outs:
+            v, gt = v.cpu().numpy(), bytes(gt.cpu().numpy())
+            for i, p in enumerate(pr):
+                if bad:
+                    assert v[i] == 0, (i, p["kind"])
+                    continue
+                assert v[i] == p["verdict"], (i, p["kind"])
+                if p["gt"] is not None:
+                    assert gt[576 * i:576 * (i + 1)].hex() == p["gt"], (i, p["kind"])
+    finally:
+        ctx.set_concurrency(1)
