@@ -5,9 +5,11 @@ set -o pipefail
 OUT=gpurun_out/${1:-r05d}
 mkdir -p $OUT
 run() {  # name, args
-  timeout -k 10 400 python bench.py $2 > $OUT/$1.json 2> $OUT/$1.err || { tail -5 $OUT/$1.err; exit 1; }
+  timeout -k 10 400 python -X faulthandler bench.py $2 > $OUT/$1.json 2> $OUT/$1.err || { tail -5 $OUT/$1.err; exit 1; }
   python3 -c "import json; d=json.loads(open('$OUT/$1.json').read().strip().splitlines()[-1]); print('$1', d['value'], d['ms_per_step'], d['config'].get('batches_in_flight'), (d.get('default_tables') or {}).get('value'), d.get('single_call_ms'))"
 }
+timeout -k 10 300 python -u -X faulthandler -m pytest tests/test_gpu_parity.py -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider -k "concurrent" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
 run verify "--steps 20 --warmup 5"
 run verify_if1 "--steps 20 --warmup 5 --inflight 1"
 run verify_b "--steps 20 --warmup 5"
