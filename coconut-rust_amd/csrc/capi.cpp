@@ -658,7 +658,11 @@ static cc_status ensure_work(cc_ctx* c, size_t n) {
 // shared verkey's tables; else one verkey per credential (d_vkX n x OtherGroup, d_vkY n x q x
 // OtherGroup; the Straus MSM of pervk.hip, its scratch in c->vkb, sized by the caller)
 struct VerifyWork {
-    DevBuf *prep, *flags, *fbuf, *vkb, *scratch, *idx;
+    DevBuf *prep = nullptr, *flags = nullptr, *fbuf = nullptr, *vkb = nullptr, *scratch = nullptr, *idx = nullptr;
+    VerifyWork() = default;
+    // every workspace named: a partial list does not compile (a missing one would be a null pointer)
+    VerifyWork(DevBuf* p, DevBuf* f, DevBuf* fb, DevBuf* v, DevBuf* s, DevBuf* i)
+        : prep(p), flags(f), fbuf(fb), vkb(v), scratch(s), idx(i) {}
 };
 static VerifyWork ctx_work(cc_ctx* c) { return {&c->prep, &c->flags, &c->fbuf, &c->vkb, &c->scratch, &c->pok_idx}; }
 static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, const uint8_t* d_s1,
@@ -1016,7 +1020,7 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
         HIPCK(hipMemcpyAsync(c->in_vkX.p, vkX, n * ob, hipMemcpyHostToDevice, st));
         if (q) HIPCK(hipMemcpyAsync(c->in_vkY.p, vkY, n * q * ob, hipMemcpyHostToDevice, st));
     }
-    s = launch_verify(c, VerifyWork{&c->prep, &c->flags, &c->fbuf, &c->vkb}, n, q, c->in_s1.as<uint8_t>(),
+    s = launch_verify(c, ctx_work(c), n, q, c->in_s1.as<uint8_t>(),
                       c->in_s2.as<uint8_t>(), d_msgs, per_vk ? c->in_vkX.as<uint8_t>() : nullptr,
                       per_vk ? c->in_vkY.as<uint8_t>() : nullptr, c->verdicts.as<uint8_t>(),
                       gt ? c->gt.as<uint8_t>() : nullptr, st);
