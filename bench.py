@@ -625,40 +625,54 @@ def bench_rlc(args):
     ctx.set_table_bits(vk_bits_for(args), 0)
     ctx.set_verkey(batch["X"], batch["Y"])
     d_s1, d_s2, d_m = to_dev(batch["s1"], dev), to_dev(batch["s2"], dev), to_dev(batch["msgs"], dev)
-    eng = DeviceEngine(ctx, n, q, d_s1, d_s2, d_m, base_index=rank * n)
+    # --inflight K: K engines (own streams and partial buffers) take turns on ONE context whose
+    # cc_set_concurrency(K) gives successive partials their own workspace slots, so batch i + 1's partial
+    # can start while batch i's is still draining (its last waves) and batch i's finish runs
+    K = max(1, args.rlc_inflight if args.rlc_inflight is not None else args.inflight)
+    engs = [DeviceEngine(ctx, n, q, d_s1, d_s2, d_m, base_index=rank * n) for _ in range(K)]
+    eng = engs[0]
 
     # batches are pipelined: batch i's single final exponentiation (one wave, latency-bound) runs on the
     # engine's finish stream while batch i+1's partial runs (DeviceEngine.finish_async)
-    def run(k_steps, phase=None):
+    def run(k_steps, phase=None, k_eng=1):
         ok = True
-        part = eng.partial()
+        cur = engs[0]
+        part = cur.partial()
         if phase is not None:
             phase += np.array(ctx.last_timing())
         for s in range(k_steps):
             allp, k = gather_partials(part)
-            decision = eng.finish_async(allp, k)
+            decision = cur.finish_async(allp, k)
             if s + 1 < k_steps:
-                part = eng.partial()
+                cur = engs[(s + 1) % k_eng]
+                part = cur.partial()
                 if phase is not None:
                     phase += np.array(ctx.last_timing())
             ok &= decision()
         return ok
 
+    # per-phase times come from a single-slot pass (the phase events of overlapping batches would overlap)
+    phase = np.zeros(3)
+    if args.steps:
+        ctx.timing(True)
+        assert run(min(args.steps, 5), phase)
+        torch.cuda.synchronize(dev)
+        ctx.timing(False)
+        phase *= args.steps / min(args.steps, 5)
+    ctx.set_concurrency(K)
     if args.warmup:
-        assert run(args.warmup)
+        assert run(args.warmup, k_eng=K)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ctx.timing(True)
-    phase = np.zeros(3)
     t0 = time.perf_counter()
-    ok = run(args.steps, phase)
+    ok = run(args.steps, k_eng=K)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ctx.timing(False)
+    ctx.set_concurrency(1)
     if not ok:
         raise SystemExit("RLC rejected an all-valid batch — refusing to report a number")
     bad = d_s2.clone()
@@ -688,7 +702,9 @@ def bench_rlc(args):
     ok_dflt = [True]
 
     def run_dflt(k_steps):
-        ok_dflt[0] &= run(k_steps)
+        ctx.set_concurrency(K)
+        ok_dflt[0] &= run(k_steps, k_eng=K)
+        ctx.set_concurrency(1)
     dflt = default_tables_leg(args, ctx, lambda: ctx.set_verkey(batch["X"], batch["Y"]), None,
                               lambda: ok_dflt[0], n, dev, dist, run_k=run_dflt)
     dflt.update(table_config(ctx, q))
@@ -704,6 +720,7 @@ def bench_rlc(args):
             "config": {"workload": "config3: RLC batch verify, msg_count=16, shared verkey, SigG2",
                        "credentials_per_gpu": n, "msg_count": q,
                        "parallelism": f"shard-by-credential x{world} + RCCL all-gather of Fp12 partials",
+                       "batches_in_flight": K,
                        **opt_in, "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
             **lib_info(),
             "single_call_ms": round(single_ms, 3) if single_ms else None,
@@ -787,6 +804,8 @@ def main():
     ap.add_argument("--inflight", type=int, default=2,
                     help="verify modes: batches in flight on one context (cc_set_concurrency slots) and as many "
                          "streams, issued round-robin; 1 = each batch ordered after the previous one")
+    ap.add_argument("--rlc-inflight", type=int, default=None,
+                    help="RLC mode: engines/slots in flight (default: --inflight)")
     ap.add_argument("--mode", choices=["verify", "verify-g1", "verify-pervk", "verify-pervk-g1", "rlc", "aggregate",
                                        "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
     args = ap.parse_args()

@@ -138,8 +138,12 @@ struct DevBuf {
 // the per-credential-verkey MSM scratch; `done` marks the end of the slot's last batch on its stream.
 struct VerifySlot {
     DevBuf prep, flags, fbuf, vkb, scratch, idx;  // scratch, idx: PoK (the d J tables, the revealed indices)
+    DevBuf rkey, rany, rpts, rdig, rwork;         // RLC partial: delta key, flag, fold points, digits, fold
     hipEvent_t done = nullptr;
     bool recorded = false;
+    void release() {
+        for (DevBuf* b : {&prep, &flags, &fbuf, &vkb, &scratch, &idx, &rkey, &rany, &rpts, &rdig, &rwork}) b->release();
+    }
 };
 
 }  // namespace
@@ -359,12 +363,7 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     drain_slots(c);
     (void)hipStreamSynchronize(c->stream);
     for (VerifySlot* v : c->vslots) {
-        v->prep.release();
-        v->flags.release();
-        v->fbuf.release();
-        v->vkb.release();
-        v->scratch.release();
-        v->idx.release();
+        v->release();
         if (v->done) (void)hipEventDestroy(v->done);
         delete v;
     }
@@ -764,12 +763,7 @@ cc_status cc_set_concurrency(cc_ctx* c, int slots) {
     while ((int)c->vslots.size() > slots - 1) {
         VerifySlot* v = c->vslots.back();
         c->vslots.pop_back();
-        v->prep.release();
-        v->flags.release();
-        v->fbuf.release();
-        v->vkb.release();
-        v->scratch.release();
-        v->idx.release();
+        v->release();
         if (v->done) (void)hipEventDestroy(v->done);
         delete v;
     }
@@ -837,6 +831,84 @@ static int fresh_seed(uint8_t seed[32]) {
     return got == 32 ? 0 : -1;
 }
 
+// The RLC partial's workspaces: prep SoA (twin layout), flags, Miller values, the product tree's scratch,
+// the delta key, the fall-back flag word, the fold points, delta digits and fold workspace.
+struct RlcWork {
+    DevBuf *prep, *flags, *fbuf, *scratch, *key, *any, *pts, *dig, *work;
+};
+static RlcWork ctx_rlc_work(cc_ctx* c) {
+    return {&c->prep, &c->flags, &c->fbuf, &c->scratch, &c->rlc_key, &c->rlc_any, &c->rlc_pts, &c->rlc_dig, &c->rlc_work};
+}
+// sizes for n credentials; a concurrency slot whose buffers must grow waits for its last batch first
+static int rlc_ensure(cc_ctx* c, const RlcWork& r, size_t n, bool slot, VerifySlot* sl) {
+    const size_t PS = (n + 1) / 2, N = (n + 3) / 4;
+    const size_t prep_b = (size_t)PREP_SLOTS * 12 * 4 * std::max(PS, n), flags_b = n * 4, fbuf_b = N * 144 * 4,
+                 scr_b = ((N + 1) / 2) * 144 * 4 + n * 12 * 4 * 72, pts_b = n * 48 * 4, dig_b = 16 * n,
+                 work_b = cck_fold_words(c->mode, n) * 4;
+    const bool grow = r.prep->bytes < prep_b || r.flags->bytes < flags_b || r.fbuf->bytes < fbuf_b ||
+                      r.scratch->bytes < scr_b || r.key->bytes < 32 || r.any->bytes < 4 || r.pts->bytes < pts_b ||
+                      r.dig->bytes < dig_b || r.work->bytes < work_b;
+    if (!grow) return 0;
+    if (slot && sl && sl->recorded && hipEventSynchronize(sl->done) != hipSuccess) return -1;
+    return r.prep->ensure(prep_b) || r.flags->ensure(flags_b) || r.fbuf->ensure(fbuf_b) || r.scratch->ensure(scr_b) ||
+           r.key->ensure(32) || r.any->ensure(4) || r.pts->ensure(pts_b) || r.dig->ensure(dig_b) ||
+           r.work->ensure(work_b);
+}
+
+static cc_status launch_rlc_partial(cc_ctx* c, const RlcWork& w, size_t n, size_t q, uint64_t base_index,
+                                    const uint8_t* seed32, const uint8_t* d_s1, const uint8_t* d_s2,
+                                    const uint8_t* d_msgs, uint32_t* d_partial, hipStream_t st) {
+    const size_t PS = (n + 1) / 2;  // prep SoA stride (the twin layout: credentials 2 t, 2 t + 1 at element t)
+    const size_t N = (n + 3) / 4;   // Miller values (four credentials' pairs each, k_miller4)
+    // pageable source: the copy is staged before the call returns
+    HIPCK(hipMemcpyAsync(w.key->p, seed32, 32, hipMemcpyHostToDevice, st));
+    HIPCK(hipMemsetAsync(w.any->p, 0, 4, st));
+    if (c->timing) (void)hipEventRecord(c->ev[0], st);
+    auto prep_part = [&](int part) {
+        return cck_prep_rlc(c->mode, part, n, PS, (int)q, base_index, w.key->as<uint32_t>(), d_s1, d_s2, d_msgs,
+                            c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(),
+                            w.flags->as<uint32_t>(), w.any->as<uint32_t>(), w.pts->as<uint32_t>(),
+                            w.dig->as<int8_t>(), st);
+    };
+    KCK(prep_part(0));  // decode, subgroup checks, the fold's inputs
+    if (!c->vk_subgroup) {
+        // a verkey / g~ point outside the subgroup: the linear-combination argument does not hold,
+        // so the batch is never accepted here and the caller verifies per credential (exact)
+        static const uint32_t one = 1;
+        HIPCK(hipMemcpyAsync(w.any->p, &one, 4, hipMemcpyHostToDevice, st));
+    }
+    // The second pairs fold into 16 window sums S_w (fold.hip).  The fold's short kernels run alone
+    // (behind a full launch each would wait milliseconds for a free slot); the window sums (16 waves)
+    // then run on the high-priority side stream beside the delta MSM and land in the partial's window
+    // section; their pairs e(S_w, P_w) are evaluated in the finish, once per batch over every shard
+    // (rlc_part.h), so the credentials' two-per-loop Miller launch stays at (n + 1) / 2 loops (2,048
+    // waves at 131,072 credentials: the chip's wave slots).
+    KCK(cck_fold(c->mode, n, w.dig->as<int8_t>(), w.pts->as<uint32_t>(), w.work->as<uint32_t>(), st));
+    hipStream_t side = c->side ? c->side : st;
+    if (side != st) {
+        HIPCK(hipEventRecord(c->ev_fork, st));
+        HIPCK(hipStreamWaitEvent(side, c->ev_fork, 0));
+    }
+    KCK(cck_fold_window(c->mode, n, w.work->as<uint32_t>(), d_partial, side));
+    KCK(prep_part(1));  // delta X~ + sum (delta m_j) Y~_j
+    if (c->timing) (void)hipEventRecord(c->ev[1], st);
+    // SigG2: sigma_1's subgroup test comes from this loop's T (a failure raises rlc_any: fallback)
+    KCK(cck_miller_quad(c->mode, n, PS, w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), w.fbuf->as<uint32_t>(), N,
+                        c->mode == 0 ? w.any->as<uint32_t>() : nullptr, st));
+    if (c->timing) (void)hipEventRecord(c->ev[2], st);
+    KCK(cck_rlc_reduce(N, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.any->as<uint32_t>(), d_partial,
+                       st));
+    if (side != st) {  // the window section is part of the partial: the call ends when both are written
+        HIPCK(hipEventRecord(c->ev_join, side));
+        HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));
+    }
+    if (c->timing) {
+        (void)hipEventRecord(c->ev[3], st);
+        collect_timing(c);
+    }
+    return CC_OK;
+}
+
 cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_index, const uint8_t* seed32,
                                 const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs, uint32_t* d_partial,
                                 void* stream) {
@@ -845,9 +917,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
     if (q != c->q) return CC_ERR_LEN;
     HIPCK(hipSetDevice(c->device));
-    drain_slots(c);  // concurrent verify batches (cc_set_concurrency) use buffers rebuilt here
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    StreamOrder order(c, st);
     if (!n) {
         // empty shard (a batch smaller than the rank count): the neutral partial — Fp12 one (Montgomery
         // one in slot 0, zeros elsewhere), a clear fall-back flag and 16 identity window sums — so every
@@ -863,61 +933,26 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
         HIPCK(hipMemcpyAsync(d_partial, kNeutral.data(), RLC_PART_WORDS * 4, hipMemcpyHostToDevice, st));
         return CC_OK;
     }
-    const size_t PS = (n + 1) / 2;  // prep SoA stride (the twin layout: credentials 2 t, 2 t + 1 at element t)
-    const size_t N = (n + 3) / 4;   // Miller values (four credentials' pairs each, k_miller4)
+    if (c->concurrency > 1) {  // the next concurrency slot (cc_set_concurrency): its own workspaces
+        VerifySlot* sl = nullptr;
+        VerifyWork w;
+        cc_status s = slot_begin(c, st, n, 0, 0, 0, sl, w);
+        if (s) return s;
+        RlcWork r = sl == &c->slot0 ? ctx_rlc_work(c)
+                                    : RlcWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->scratch, &sl->rkey, &sl->rany,
+                                              &sl->rpts, &sl->rdig, &sl->rwork};
+        if (rlc_ensure(c, r, n, true, sl)) return CC_ERR_HIP;
+        s = launch_rlc_partial(c, r, n, q, base_index, seed32, d_s1, d_s2, d_msgs, d_partial, st);
+        if (s) return s;
+        return slot_end(st, sl);
+    }
+    drain_slots(c);  // concurrent batches (cc_set_concurrency) may still use the buffers sized below
     cc_status s = ensure_work(c, n);
     if (s) return s;
-    if (c->rlc_key.ensure(32) || c->rlc_any.ensure(4) || c->fbuf.ensure(N * 144 * 4) ||
-        c->scratch.ensure(((N + 1) / 2) * 144 * 4 + n * 12 * 4 * 72) || c->rlc_pts.ensure(n * 48 * 4) ||
-        c->rlc_dig.ensure(16 * n) || c->rlc_work.ensure(cck_fold_words(c->mode, n) * 4))
-        return CC_ERR_HIP;
-    memcpy(c->rlc_key_host, seed32, 32);
-    HIPCK(hipMemcpyAsync(c->rlc_key.p, c->rlc_key_host, 32, hipMemcpyHostToDevice, st));
-    HIPCK(hipMemsetAsync(c->rlc_any.p, 0, 4, st));
-    if (c->timing) (void)hipEventRecord(c->ev[0], st);
-    auto prep_part = [&](int part) {
-        return cck_prep_rlc(c->mode, part, n, PS, (int)q, base_index, c->rlc_key.as<uint32_t>(), d_s1, d_s2, d_msgs,
-                            c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), c->prep.as<uint32_t>(),
-                            c->flags.as<uint32_t>(), c->rlc_any.as<uint32_t>(), c->rlc_pts.as<uint32_t>(),
-                            c->rlc_dig.as<int8_t>(), st);
-    };
-    KCK(prep_part(0));  // decode, subgroup checks, the fold's inputs
-    if (!c->vk_subgroup) {
-        // a verkey / g~ point outside the subgroup: the linear-combination argument does not hold,
-        // so the batch is never accepted here and the caller verifies per credential (exact)
-        static const uint32_t one = 1;
-        HIPCK(hipMemcpyAsync(c->rlc_any.p, &one, 4, hipMemcpyHostToDevice, st));
-    }
-    // The second pairs fold into 16 window sums S_w (fold.hip).  The fold's short kernels run alone
-    // (behind a full launch each would wait milliseconds for a free slot); the window sums (16 waves)
-    // then run on the high-priority side stream beside the delta MSM and land in the partial's window
-    // section; their pairs e(S_w, P_w) are evaluated in the finish, once per batch over every shard
-    // (rlc_part.h), so the credentials' two-per-loop Miller launch stays at (n + 1) / 2 loops (2,048
-    // waves at 131,072 credentials: the chip's wave slots).
-    KCK(cck_fold(c->mode, n, c->rlc_dig.as<int8_t>(), c->rlc_pts.as<uint32_t>(), c->rlc_work.as<uint32_t>(), st));
-    hipStream_t side = c->side ? c->side : st;
-    if (side != st) {
-        HIPCK(hipEventRecord(c->ev_fork, st));
-        HIPCK(hipStreamWaitEvent(side, c->ev_fork, 0));
-    }
-    KCK(cck_fold_window(c->mode, n, c->rlc_work.as<uint32_t>(), d_partial, side));
-    KCK(prep_part(1));  // delta X~ + sum (delta m_j) Y~_j
-    if (c->timing) (void)hipEventRecord(c->ev[1], st);
-    // SigG2: sigma_1's subgroup test comes from this loop's T (a failure raises rlc_any: fallback)
-    KCK(cck_miller_quad(c->mode, n, PS, c->prep.as<uint32_t>(), c->flags.as<uint32_t>(), c->fbuf.as<uint32_t>(), N,
-                        c->mode == 0 ? c->rlc_any.as<uint32_t>() : nullptr, st));
-    if (c->timing) (void)hipEventRecord(c->ev[2], st);
-    KCK(cck_rlc_reduce(N, c->fbuf.as<uint32_t>(), c->scratch.as<uint32_t>(), c->rlc_any.as<uint32_t>(), d_partial,
-                       st));
-    if (side != st) {  // the window section is part of the partial: the call ends when both are written
-        HIPCK(hipEventRecord(c->ev_join, side));
-        HIPCK(hipStreamWaitEvent(st, c->ev_join, 0));
-    }
-    if (c->timing) {
-        (void)hipEventRecord(c->ev[3], st);
-        collect_timing(c);
-    }
-    return CC_OK;
+    RlcWork r = ctx_rlc_work(c);
+    if (rlc_ensure(c, r, n, false, nullptr)) return CC_ERR_HIP;
+    StreamOrder order(c, st);
+    return launch_rlc_partial(c, r, n, q, base_index, seed32, d_s1, d_s2, d_msgs, d_partial, st);
 }
 
 cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_partials, uint8_t* d_accept,

@@ -119,8 +119,9 @@ cc_status cc_verify_batch_pervk_device(cc_ctx* ctx, size_t n, size_t q, const ui
                                        void* stream);
 
 /* Concurrent verify batches on one context: with `slots` = K > 1, cc_verify_batch_device,
- * cc_verify_batch_pervk_device and cc_pok_verify_batch_device calls take K workspace slots round-robin
- * (each slot its own prep SoA, flags, Miller values and PoK d J tables; the verkey tables are shared)
+ * cc_verify_batch_pervk_device, cc_pok_verify_batch_device and cc_rlc_partial_device calls take K
+ * workspace slots round-robin (each slot its own prep SoA, flags, Miller values, PoK d J tables and RLC
+ * delta/fold buffers; the verkey tables are shared)
  * and are ordered only after the context's earlier work (tables, params) and the same slot's previous
  * batch — so K batches issued on K caller streams overlap on the device (one batch's kernel tails with
  * the next batch's kernels).  An n = 1 verify call takes the serialized path.  Every other
@@ -148,7 +149,7 @@ cc_status cc_concurrency(const cc_ctx* ctx, int* slots);
  * Both are asynchronous on `stream` (NULL: the context stream).  The partial is ordered against the
  * context's other work; the finish owns its buffers and is NOT, so on a second stream it may overlap
  * the next batch's partial (the caller orders d_partials before it, and two finishes of one context
- * one after the other).  cc_verify_batch(..., rlc = 1) runs the single-GPU form with a fresh seed
+ * one after the other); with cc_set_concurrency(K) successive partials take K slots and overlap too.  cc_verify_batch(..., rlc = 1) runs the single-GPU form with a fresh seed
  * from /dev/urandom and falls back by itself. */
 #define CC_RLC_PARTIAL_WORDS 929
 int cc_rlc_partial_words(void);
