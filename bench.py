@@ -628,7 +628,7 @@ def bench_rlc(args):
     # --inflight K: K engines (own streams and partial buffers) take turns on ONE context whose
     # cc_set_concurrency(K) gives successive partials their own workspace slots, so batch i + 1's partial
     # can start while batch i's is still draining (its last waves) and batch i's finish runs
-    K = max(1, args.rlc_inflight if args.rlc_inflight is not None else args.inflight)
+    K = max(1, args.rlc_inflight)
     engs = [DeviceEngine(ctx, n, q, d_s1, d_s2, d_m, base_index=rank * n) for _ in range(K)]
     eng = engs[0]
 
@@ -804,8 +804,10 @@ def main():
     ap.add_argument("--inflight", type=int, default=2,
                     help="verify modes: batches in flight on one context (cc_set_concurrency slots) and as many "
                          "streams, issued round-robin; 1 = each batch ordered after the previous one")
-    ap.add_argument("--rlc-inflight", type=int, default=None,
-                    help="RLC mode: engines/slots in flight (default: --inflight)")
+    ap.add_argument("--rlc-inflight", type=int, default=1,
+                    help="RLC mode: engines (own streams, partial buffers) taking cc_set_concurrency slots in "
+                         "turn; 1 = the pipelined single engine (measured the same as 2 and 3: "
+                         "profiles/r05/modes2)")
     ap.add_argument("--mode", choices=["verify", "verify-g1", "verify-pervk", "verify-pervk-g1", "rlc", "aggregate",
                                        "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
     args = ap.parse_args()
