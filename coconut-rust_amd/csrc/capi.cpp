@@ -62,6 +62,9 @@ int cck_fold_fixed(int mode, int q, const uint32_t* d_table, int wbits, const ui
                    uint8_t* d_finf, hipStream_t st);
 int cck_miller_wide(size_t n, const uint32_t* d_prep, const uint32_t* d_flags, uint32_t* d_f, size_t fstride,
                     size_t foff, hipStream_t st);
+int cck_f12_reduce_wide(size_t n, const uint32_t* d_in, uint32_t* d_out, hipStream_t st);
+int cck_wide_pairs(int mode, size_t n, size_t ps, const uint32_t* d_prep, const uint32_t* d_flags,
+                   const uint32_t* d_gaff, uint32_t* d_wprep, uint32_t* d_wflags, hipStream_t st);
 int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
              uint8_t* d_gt, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
@@ -138,11 +141,13 @@ struct DevBuf {
 // the per-credential-verkey MSM scratch; `done` marks the end of the slot's last batch on its stream.
 struct VerifySlot {
     DevBuf prep, flags, fbuf, vkb, scratch, idx;  // scratch, idx: PoK (the d J tables, the revealed indices)
+    DevBuf wprep, wflags, wf;                     // small batches' one-wave-per-pair Miller path
     DevBuf rkey, rany, rpts, rdig, rwork;         // RLC partial: delta key, flag, fold points, digits, fold
     hipEvent_t done = nullptr;
     bool recorded = false;
     void release() {
-        for (DevBuf* b : {&prep, &flags, &fbuf, &vkb, &scratch, &idx, &rkey, &rany, &rpts, &rdig, &rwork}) b->release();
+        for (DevBuf* b : {&prep, &flags, &fbuf, &vkb, &scratch, &idx, &wprep, &wflags, &wf, &rkey, &rany, &rpts, &rdig, &rwork})
+            b->release();
     }
 };
 
@@ -175,6 +180,7 @@ struct cc_ctx {
     // workspaces
     DevBuf in_s1, in_s2, in_msgs, in_vkX, in_vkY, in_aux[6];
     DevBuf prep, flags, fbuf, scratch, verdicts, gt, vkb, lag;  // vkb: per-credential-verkey MSM scratch
+    DevBuf wide_prep, wide_flags, wide_f;  // batches of <= kWideMax: the one-wave-per-pair Miller path
     // RLC batch mode: ChaCha20 key, identity flag word, partial / gathered partials, verdict
     DevBuf rlc_key, rlc_any, rlc_part, rlc_flag, rlc_accept;
     // cc_rlc_finish_device's own buffers: Fp12 values (partial products, window pairs' Miller values),
@@ -371,7 +377,7 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     if (c->slot0.done) (void)hipEventDestroy(c->slot0.done);
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->gtilde_lz, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
-                      &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->lag,
+                      &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->lag, &c->wide_prep, &c->wide_flags, &c->wide_f,
                       &c->rlc_key, &c->rlc_any, &c->rlc_part, &c->rlc_flag, &c->rlc_accept, &c->fin_f, &c->fin_scratch, &c->fin_prep, &c->fin_flags2, &c->fin_part, &c->pok_idx, &c->rlc_gath,
                       &c->rlc_pts, &c->rlc_dig, &c->rlc_work, &c->rlc_pw, &c->rlc_finf,
                       &c->iss_ids, &c->iss_aff, &c->iss_inf, &c->iss_table, &c->agg_scratch, &c->dev_err};
@@ -639,11 +645,29 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
     return CC_OK;
 }
 
+// Batches of up to kWideMax credentials run their Miller loops one wave per pair (fexp_pl.hip
+// k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide: ~1.8 ms however small the batch) instead of one
+// lane pair per credential (k_miller: ~7.5 ms for any batch up to a few thousand, one loop's latency on
+// a lone wave).  k_miller_wide holds one wave a SIMD, so 2 x 512 pairs are one round of the chip's
+// 1,024 SIMDs (measured crossover: profiles/r05/).
+constexpr size_t kWideMax = 512;
+static bool wide_short(DevBuf& p, DevBuf& f, DevBuf& v, size_t n) {
+    const size_t m = 2 * n, words = m * 12;
+    return n <= kWideMax && (p.bytes < words * 4 * PREP_SLOTS || f.bytes < m * 4 || v.bytes < words * 4 * 12);
+}
+static int wide_ensure(DevBuf& p, DevBuf& f, DevBuf& v, size_t n) {
+    if (n > kWideMax) return 0;
+    const size_t m = 2 * n, words = m * 12;
+    return p.ensure(words * 4 * PREP_SLOTS) || f.ensure(m * 4) || v.ensure(words * 4 * 12) ? -1 : 0;
+}
+
 static cc_status ensure_work(cc_ctx* c, size_t n) {
     size_t words = n * 12;  // one Fp slot
     if (c->prep.bytes < words * 4 * PREP_SLOTS || c->flags.bytes < n * 4 || c->fbuf.bytes < words * 4 * 12 ||
-        c->scratch.bytes < (n * 15 * 84 + 72 * 12) * 4 || c->verdicts.bytes < n)
+        c->scratch.bytes < (n * 15 * 84 + 72 * 12) * 4 || c->verdicts.bytes < n ||
+        wide_short(c->wide_prep, c->wide_flags, c->wide_f, n))
         drain_slots(c);  // a concurrent batch may still read the buffers about to be reallocated
+    if (wide_ensure(c->wide_prep, c->wide_flags, c->wide_f, n)) return CC_ERR_HIP;
     // scratch: the PoK prep's per-proof table of d J (15 Jacobian points, <= 15 x 84 words: SigG1's lazy
     // G2 points), and the one-element fexp's (fexp_pl.hip k_fexp1: 72 slots of 12 words); the batched
     // fexp (fexp_q.hip) keeps its chain in registers
@@ -658,12 +682,30 @@ static cc_status ensure_work(cc_ctx* c, size_t n) {
 // OtherGroup; the Straus MSM of pervk.hip, its scratch in c->vkb, sized by the caller)
 struct VerifyWork {
     DevBuf *prep = nullptr, *flags = nullptr, *fbuf = nullptr, *vkb = nullptr, *scratch = nullptr, *idx = nullptr;
+    DevBuf *wprep = nullptr, *wflags = nullptr, *wf = nullptr;  // the small-batch Miller path's
     VerifyWork() = default;
     // every workspace named: a partial list does not compile (a missing one would be a null pointer)
-    VerifyWork(DevBuf* p, DevBuf* f, DevBuf* fb, DevBuf* v, DevBuf* s, DevBuf* i)
-        : prep(p), flags(f), fbuf(fb), vkb(v), scratch(s), idx(i) {}
+    VerifyWork(DevBuf* p, DevBuf* f, DevBuf* fb, DevBuf* v, DevBuf* s, DevBuf* i, DevBuf* wp, DevBuf* wfl, DevBuf* wv)
+        : prep(p), flags(f), fbuf(fb), vkb(v), scratch(s), idx(i), wprep(wp), wflags(wfl), wf(wv) {}
 };
-static VerifyWork ctx_work(cc_ctx* c) { return {&c->prep, &c->flags, &c->fbuf, &c->vkb, &c->scratch, &c->pok_idx}; }
+static VerifyWork ctx_work(cc_ctx* c) {
+    return {&c->prep, &c->flags, &c->fbuf, &c->vkb, &c->scratch, &c->pok_idx, &c->wide_prep, &c->wide_flags, &c->wide_f};
+}
+// the batch's Miller values into w.fbuf (SoA stride n): n <= kWideMax one wave per pair, else the
+// pair-lane loop (one lane pair per credential, both pairs with a shared squaring)
+static cc_status launch_miller(cc_ctx* c, const VerifyWork& w, size_t n, hipStream_t st) {
+    if (n <= kWideMax) {
+        const size_t m = 2 * n;
+        KCK(cck_wide_pairs(c->mode, n, n, w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), c->gtilde_aff.as<uint32_t>(),
+                           w.wprep->as<uint32_t>(), w.wflags->as<uint32_t>(), st));
+        KCK(cck_miller_wide(m, w.wprep->as<uint32_t>(), w.wflags->as<uint32_t>(), w.wf->as<uint32_t>(), m, 0, st));
+        KCK(cck_f12_reduce_wide(m, w.wf->as<uint32_t>(), w.fbuf->as<uint32_t>(), st));
+        return CC_OK;
+    }
+    const uint32_t* cst = c->mode == 0 ? c->gtilde_lz.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
+    KCK(cck_miller(c->mode, n, w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), cst, w.fbuf->as<uint32_t>(), st));
+    return CC_OK;
+}
 static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, const uint8_t* d_s1,
                                const uint8_t* d_s2, const uint8_t* d_msgs, const uint8_t* d_vkX, const uint8_t* d_vkY,
                                uint8_t* d_verdicts, uint8_t* d_gt, hipStream_t st) {
@@ -676,8 +718,8 @@ static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t 
                      c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(),
                      w.flags->as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
-    const uint32_t* cst = c->mode == 0 ? c->gtilde_lz.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
-    KCK(cck_miller(c->mode, n, w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), cst, w.fbuf->as<uint32_t>(), st));
+    cc_status ms = launch_miller(c, w, n, st);
+    if (ms) return ms;
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     // n = 1 takes the one-element fexp (k_fexp1), whose scratch is the context's: only the serialized
     // path uses it (verify_device)
@@ -701,14 +743,16 @@ static cc_status slot_begin(cc_ctx* c, hipStream_t st, size_t n, size_t vkw, siz
     const int k = c->vslot_next;
     c->vslot_next = (k + 1) % c->concurrency;
     sl = k ? c->vslots[k - 1] : &c->slot0;
-    w = k ? VerifyWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->vkb, &sl->scratch, &sl->idx} : ctx_work(c);
+    w = k ? VerifyWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->vkb, &sl->scratch, &sl->idx, &sl->wprep, &sl->wflags, &sl->wf}
+          : ctx_work(c);
     const size_t words = n * 12;
     if (w.prep->bytes < words * 4 * PREP_SLOTS || w.flags->bytes < n * 4 || w.fbuf->bytes < words * 4 * 12 ||
-        w.vkb->bytes < vkw || w.scratch->bytes < scratch_bytes || w.idx->bytes < idx_bytes) {
+        w.vkb->bytes < vkw || w.scratch->bytes < scratch_bytes || w.idx->bytes < idx_bytes ||
+        wide_short(*w.wprep, *w.wflags, *w.wf, n)) {
         if (sl->recorded) HIPCK(hipEventSynchronize(sl->done));  // the slot's last batch still reads them
         if (w.prep->ensure(words * 4 * PREP_SLOTS) || w.flags->ensure(n * 4) || w.fbuf->ensure(words * 4 * 12) ||
             (vkw && w.vkb->ensure(vkw)) || (scratch_bytes && w.scratch->ensure(scratch_bytes)) ||
-            (idx_bytes && w.idx->ensure(idx_bytes)))
+            (idx_bytes && w.idx->ensure(idx_bytes)) || wide_ensure(*w.wprep, *w.wflags, *w.wf, n))
             return CC_ERR_HIP;
     }
     if (st != c->stream) {
@@ -1628,8 +1672,8 @@ static cc_status launch_pok(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, 
                      c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(), w.flags->as<uint32_t>(),
                      w.scratch->as<uint32_t>(), st));  // J*chal window table: the fexp scratch, free until fexp
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
-    const uint32_t* cst = c->mode == 0 ? c->gtilde_lz.as<uint32_t>() : c->gtilde_lines.as<uint32_t>();
-    KCK(cck_miller(c->mode, n, w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), cst, w.fbuf->as<uint32_t>(), st));
+    cc_status ms = launch_miller(c, w, n, st);
+    if (ms) return ms;
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);

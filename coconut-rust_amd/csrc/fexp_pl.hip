@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include "codec.h"
+#include "lazy.h"  // LZ_ONE_LIMBS (k_wide_pairs)
 #include "tower_pl.h"
 
 namespace cc {
@@ -668,6 +669,77 @@ __global__ __launch_bounds__(64, 1) void k_miller_wide(size_t n, const uint32_t*
     if (threadIdx.x < 2) st_f12(Soa{fout, fstride}, foff + i, f);
 }
 
+// ================================================================ small batches: one wave per pair
+// A batch of n credentials fills 2n lanes of the pair-lane Miller kernel (k_miller): for small n that is
+// a handful of waves, each the latency of a 2-pair loop on one lane pair (~7.5 ms alone on its SIMD,
+// whatever n up to ~4k).  For n <= kWideMax (capi.cpp) each credential's two pairs run instead as two
+// waves of k_miller_wide (one pair a wave, the independent products of a step spread over the lane
+// pairs: ~1.8 ms), and k_f12_reduce_wide multiplies each credential's two Miller values.  k_wide_pairs
+// lays the pairs out for it: pair 2i = credential i's pair 0, 2i + 1 its pair 1, Q affine (storage R
+// form) in slots S_Q1.., P in evaluation form (X Z, Y, Z^3) in S_P1..; wide flag bit 0 = skip.
+//   SigG2: pair 0 (sigma_1, pr), pair 1 (-sigma_2, g~);  SigG1: pair 0 (pr, sigma_1), pair 1 (g~, -sigma_2)
+// The prep's P are affine in the lazy R' form (kAffRp): words x R' mod p, read by the storage-form tower
+// as x 2^-14, so P = (x, y) goes in as (x R', y R', R' mod p) = 2^-14 (x, y, 1), a scaling of the
+// evaluation form by an Fp constant (the final exponentiation removes it).  g~ (ctx gtilde_aff, AoS,
+// R form) goes in as (x, y, 1) in R form.  Verdict flags stay per credential (the prep's).
+DEV Fp one_rprime_words() {  // R' mod p (lazy.h LZ_ONE_LIMBS, 14 x 28 bits) as 12 x 32-bit words
+    constexpr uint32_t L[14] = {LZ_ONE_LIMBS};
+    Fp r;
+#pragma unroll
+    for (int j = 0; j < NL; j++) {
+        uint64_t w = 0;
+#pragma unroll
+        for (int k = 0; k < 14; k++) {
+            const int sh = 28 * k - 32 * j;
+            if (sh >= 32 || sh <= -28) continue;
+            w |= sh >= 0 ? (uint64_t)L[k] << sh : (uint64_t)L[k] >> -sh;
+        }
+        r.v[j] = (uint32_t)w;
+    }
+    return r;
+}
+template <int MODE>
+__global__ __launch_bounds__(64) void k_wide_pairs(size_t n, size_t ps, const uint32_t* __restrict__ prep,
+                                                   const uint32_t* __restrict__ flags,
+                                                   const uint32_t* __restrict__ gaff, uint32_t* __restrict__ wprep,
+                                                   uint32_t* __restrict__ wflags) {
+    const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (e >= 2 * n) return;
+    const size_t i = e >> 1;
+    const int k = (int)(e & 1);
+    const Soa S{const_cast<uint32_t*>(prep), ps}, W{wprep, 2 * n};
+    Fp v;
+    const bool q_is_g = MODE == 1 && k == 1, p_is_g = MODE == 0 && k == 1;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {  // Q: x.a, x.b, y.a, y.b
+        if (q_is_g) {
+#pragma unroll
+            for (int l = 0; l < NL; l++) v.v[l] = gaff[NL * j + l];
+        } else {
+            ld_fp(v, S, (k ? S_Q2 : S_Q1) + j, i);
+        }
+        st_fp(W, S_Q1 + j, e, v);
+    }
+    if (p_is_g) {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+#pragma unroll
+            for (int l = 0; l < NL; l++) v.v[l] = gaff[NL * j + l];
+            st_fp(W, S_P1 + j, e, v);
+        }
+        fp_one(v);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            ld_fp(v, S, (k ? S_P2 : S_P1) + j, i);
+            st_fp(W, S_P1 + j, e, v);
+        }
+        v = one_rprime_words();
+    }
+    st_fp(W, S_P1 + 2, e, v);
+    wflags[e] = (flags[i] & (k ? 18u : 5u)) ? 1u : 0u;
+}
+
 // one level of the RLC product tree in the wide form: out[t] = in[2t] in[2t+1] (in[2t] alone for an odd
 // tail), one wave per product, the 18 Fp2 products on the wave's lane pairs at once.  The tree's short
 // levels are latency-bound (k_f12_reduce: one product on one lane pair, ~45 us a level whatever its
@@ -710,6 +782,22 @@ extern "C" int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint
     if (n > 1) return cck_fexp_q(n, d_f, d_flags, d_verdicts, d_gt, st);
     // one element (the RLC batch's combined product): latency-bound, the wide one-wave form
     hipLaunchKernelGGL(cc::pl::k_fexp1, dim3(1), dim3(64), 0, st, d_f, d_scratch, d_flags, d_verdicts, d_gt);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// credential i's two Miller pairs as wide pairs 2i, 2i + 1 (k_wide_pairs above); gaff: g~ affine (AoS,
+// R form) of the context
+extern "C" int cck_wide_pairs(int mode, size_t n, size_t ps, const uint32_t* d_prep, const uint32_t* d_flags,
+                              const uint32_t* d_gaff, uint32_t* d_wprep, uint32_t* d_wflags, hipStream_t st) {
+    if (!n) return 0;
+    if (ps < n) return -1;
+    const unsigned g = nblocks(2 * n, 64);
+    if (mode == 0)
+        hipLaunchKernelGGL(cc::pl::k_wide_pairs<0>, dim3(g), dim3(64), 0, st, n, ps, d_prep, d_flags, d_gaff, d_wprep,
+                           d_wflags);
+    else
+        hipLaunchKernelGGL(cc::pl::k_wide_pairs<1>, dim3(g), dim3(64), 0, st, n, ps, d_prep, d_flags, d_gaff, d_wprep,
+                           d_wflags);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
