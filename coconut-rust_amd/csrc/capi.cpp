@@ -646,11 +646,12 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
 }
 
 // Batches of up to kWideMax credentials run their Miller loops one wave per pair (fexp_pl.hip
-// k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide: ~1.8 ms however small the batch) instead of one
-// lane pair per credential (k_miller: ~7.5 ms for any batch up to a few thousand, one loop's latency on
-// a lone wave).  k_miller_wide holds one wave a SIMD, so 2 x 512 pairs are one round of the chip's
-// 1,024 SIMDs (measured crossover: profiles/r05/).
-constexpr size_t kWideMax = 512;
+// k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide) instead of one lane pair per credential (k_miller:
+// one 2-pair loop's latency on a lone wave, ~7.5 ms for any batch up to a few thousand).  k_miller_wide
+// holds one wave a SIMD, so 2 x 512 pairs are one round of the chip's 1,024 SIMDs.  Measured Miller phase
+// (profiles/r05/latency): 1.6 ms at n = 1, 1.9 ms at 512, 3.7 ms at 1,024 against 7.5 ms; at 2,048 the
+// wide path still leads (7.0 ms) but by 7 %, with 32x the lane-work, so the threshold stays at 1,024.
+constexpr size_t kWideMax = 1024;
 static bool wide_short(DevBuf& p, DevBuf& f, DevBuf& v, size_t n) {
     const size_t m = 2 * n, words = m * 12;
     return n <= kWideMax && (p.bytes < words * 4 * PREP_SLOTS || f.bytes < m * 4 || v.bytes < words * 4 * 12);

@@ -26,6 +26,7 @@ template <bool W>
 DEV void m12(Fp12& r, const Fp12& x, const Fp12& y);  // f12_mul, wide when W (below)
 template <bool W>
 DEV void cs12(Fp12& r, const Fp12& x);  // f12_cyc_sqr, wide when W (below)
+DEV void f12_inv_wide(Fp12& r, const Fp12& x);  // f12_inv, wide (below)
 
 DEV void fx_apply(Fp12& x, int op) {
     if (op == OP_CONJ) {
@@ -45,7 +46,8 @@ template <bool W>
 static __device__ __noinline__ void fx_inv(Soa src, Soa dst, size_t i) {
     Fp12 f, t;
     ld_f12(f, src, i);
-    f12_inv(t, f);
+    if (W) f12_inv_wide(t, f);
+    else f12_inv(t, f);
     st_f12(dst, i, t);
 }
 
@@ -339,6 +341,78 @@ DEV void f12_cyc_sqr_wide(Fp12& r, const Fp12& x) {
     r.b = rb;
 }
 
+// k Fp4 products x_m y_m (m < k <= 10) as 3k Fp2 products on pairs 0..3k-1 (f4_mul's Karatsuba: pair
+// 3m + p forms x.a y.a, x.b y.b, (x.a + x.b)(y.a + y.b) for p = 0, 1, 2); every pair gets all k results
+DEV void f4w_mul(Fp4* r, const Fp4* x, const Fp4* y, int k) {
+    const int j = pair_idx() % (3 * k), m = j / 3, p = j % 3;
+    Fp2 xa[10], xb[10], ya[10], yb[10];
+    for (int t = 0; t < k; t++) {
+        xa[t] = x[t].a; xb[t] = x[t].b; ya[t] = y[t].a; yb[t] = y[t].b;
+    }
+    const Fp2 Xa = f2_pick(m, xa, k), Xb = f2_pick(m, xb, k), Ya = f2_pick(m, ya, k), Yb = f2_pick(m, yb, k);
+    Fp2 o1 = Xa, o2 = Ya, s1, s2, pr;
+    f2_add_lz(s1, Xa, Xb);
+    f2_add_lz(s2, Ya, Yb);
+    o1.c = fp_sel(p == 1, Xb.c, o1.c);
+    o2.c = fp_sel(p == 1, Yb.c, o2.c);
+    o1.c = fp_sel(p == 2, s1.c, o1.c);
+    o2.c = fp_sel(p == 2, s2.c, o2.c);
+    f2_mul(pr, o1, o2);
+    for (int t = 0; t < k; t++) f4_from_products(r[t], bcast_f2(pr, 3 * t), bcast_f2(pr, 3 * t + 1), bcast_f2(pr, 3 * t + 2));
+}
+
+// = f12_inv (tower.inc) for the one-element kernel: its 40 Fp2 products as five spread calls and the
+// one inversion (a^2, bc, c^2, ab, b^2, ac | c B0, b C0, a A0 | F.a^2, F.b^2 | inverse | A0, B0, C0 by 1/F)
+DEV void f12_inv_wide(Fp12& r, const Fp12& x) {
+    Fp4 P[6];
+    {
+        const Fp4 X[6] = {x.a, x.b, x.c, x.a, x.b, x.a}, Y[6] = {x.a, x.c, x.c, x.b, x.b, x.c};
+        f4w_mul(P, X, Y, 6);
+    }
+    Fp4 A0, B0, C0, t;
+    f4_mul_s(t, P[1]);
+    f4_sub(A0, P[0], t);  // a^2 - s bc
+    f4_mul_s(t, P[2]);
+    f4_sub(B0, t, P[3]);  // s c^2 - ab
+    f4_sub(C0, P[4], P[5]);  // b^2 - ac
+    Fp4 F;
+    {
+        const Fp4 X[3] = {x.c, x.b, x.a}, Y[3] = {B0, C0, A0};
+        f4w_mul(P, X, Y, 3);
+        f4_add(F, P[0], P[1]);
+        f4_mul_s(F, F);
+        f4_add(F, F, P[2]);
+    }
+    Fp2 n, pr, u, v;
+    {  // f4_inv: pairs 0, 1 square F.a, F.b
+        const int j = pair_idx() & 1;
+        Fp2 in = F.a;
+        in.c = fp_sel(j == 1, F.b.c, in.c);
+        f2_sqr(pr, in);
+        f2_mul_xi(u, bcast_f2(pr, 1));
+        f2_sub(n, bcast_f2(pr, 0), u);  // a^2 - xi b^2
+    }
+    f2_inv(n, n);
+    {
+        const int j = pair_idx() & 1;
+        Fp2 in = F.a;
+        in.c = fp_sel(j == 1, F.b.c, in.c);
+        f2_mul(pr, in, n);
+        u = bcast_f2(pr, 0);
+        v = bcast_f2(pr, 1);
+    }
+    Fp4 Fi;
+    Fi.a = u;
+    f2_neg(Fi.b, v);
+    {
+        const Fp4 X[3] = {A0, B0, C0}, Y[3] = {Fi, Fi, Fi};
+        f4w_mul(P, X, Y, 3);
+    }
+    r.a = P[0];
+    r.b = P[1];
+    r.c = P[2];
+}
+
 template <bool W>
 DEV void m12(Fp12& r, const Fp12& x, const Fp12& y) {
     if (W) f12_mul_wide(r, x, y);
@@ -375,13 +449,118 @@ DEV void ld_cyc4(Cyc4& x, const Soa& K, int base, size_t i) {
 // Granger-Scott squarings of g^(2^57) (cheaper than three more decompressions).  Five Fp12
 // multiplications as before.  A zero denominator (b = c = 0 pattern; never reached by honest inputs,
 // e.g. src = 1) sends the lane pair to the Granger-Scott ladder.
+// The wide (one-element) form of the decompression: the three snapshots' 12 squarings, then their 18
+// products, as two spread calls (pair j loads its operands from the scratch by index), the three
+// denominators' pairwise products, ONE inversion, the three inverses and the six a-coefficients —
+// six product latencies and the inversion, against the 42 products one after another of the
+// per-lane form.  Snapshots (Cyc4, 8 slots each) at K slots 0 (g^(2^16)), 8 (g^(2^48)), 16 (g^(2^57));
+// N_b, N_c and then the numerators in the scratch region X (12 slots; the chain's S, free during a
+// pow-by-x).  Returns false on a zero denominator (the Granger-Scott fallback).
+DEV bool decompress3_wide(Fp12& a16, Fp12& a48, Fp12& a57, const Soa& K, const Soa& X) {
+    const int j = pair_idx();
+    {  // squarings of b0, b1, c0, c1 of each snapshot (pairs 0..11)
+        const int jj = j % 12;
+        Fp2 in, sq;
+        ld_f2(in, K, 8 * (jj >> 2) + 2 * (jj & 3), 0);
+        f2_sqr(sq, in);
+        for (int s = 0; s < 3; s++) {
+            Fp2 t, u;
+            f2_mul_xi(t, bcast_f2(sq, 4 * s + 1));
+            f2_sub(u, bcast_f2(sq, 4 * s), t);  // N_b = b0^2 - xi b1^2
+            st_f2(X, 4 * s, 0, u);
+            f2_mul_xi(t, bcast_f2(sq, 4 * s + 3));
+            f2_sub(u, bcast_f2(sq, 4 * s + 2), t);  // N_c = c0^2 - xi c1^2
+            st_f2(X, 4 * s + 2, 0, u);
+        }
+    }
+    Fp2 d[3];
+    {  // per snapshot: b0 N_b, c1 N_c, c0 N_c, b1 N_b, b0 c0, b1 c1 (pairs 0..17)
+        const int jj = j % 18, s = jj / 6, t = jj % 6;
+        const int c1 = (0x101230 >> (4 * t)) & 15;  // first factor's component: b0 c1 c0 b1 b0 b1
+        Fp2 o1, o2, pr;
+        ld_f2(o1, K, 8 * s + 2 * c1, 0);
+        if (t < 4) ld_f2(o2, X, 4 * s + (t == 1 || t == 2 ? 2 : 0), 0);
+        else ld_f2(o2, K, 8 * s + (t == 4 ? 4 : 6), 0);
+        f2_mul(pr, o1, o2);
+        for (int s2 = 0; s2 < 3; s2++) {
+            Fp2 u, v;
+            f2_mul_xi(u, bcast_f2(pr, 6 * s2 + 1));
+            f2_add(v, bcast_f2(pr, 6 * s2), u);  // a0 numerator: b0 N_b + xi c1 N_c
+            st_f2(X, 4 * s2, 0, v);
+            f2_add(v, bcast_f2(pr, 6 * s2 + 2), bcast_f2(pr, 6 * s2 + 3));  // a1 numerator: c0 N_c + b1 N_b
+            st_f2(X, 4 * s2 + 2, 0, v);
+            f2_mul_xi(u, bcast_f2(pr, 6 * s2 + 5));
+            f2_sub(v, bcast_f2(pr, 6 * s2 + 4), u);
+            f2_dbl(d[s2], v);  // D = 2 (b0 c0 - xi b1 c1)
+        }
+    }
+    Fp2 e[3], p2, inv;
+    {  // pairs 0..2: d16 d48, d48 d57, d16 d57
+        const int jj = j % 3;
+        Fp2 pr;
+        f2_mul(pr, f2_pick(jj == 1 ? 1 : 0, d, 3), f2_pick(jj == 0 ? 1 : 2, d, 3));
+        for (int k = 0; k < 3; k++) e[k] = bcast_f2(pr, k);
+    }
+    f2_mul(p2, e[0], d[2]);
+    if (f2_is_zero(p2)) return false;  // wave-uniform: every pair holds the same values
+    f2_inv(inv, p2);
+    Fp2 iv[3];
+    {  // pairs 0..2: 1/d16 = inv d48 d57, 1/d48 = inv d16 d57, 1/d57 = inv d16 d48
+        const int jj = j % 3;
+        Fp2 pr;
+        f2_mul(pr, inv, f2_pick(jj == 0 ? 1 : jj == 1 ? 2 : 0, e, 3));
+        for (int k = 0; k < 3; k++) iv[k] = bcast_f2(pr, k);
+    }
+    {  // pairs 0..5: the a-coefficients, numerator (s, h) times 1/d_s
+        const int jj = j % 6, s = jj >> 1;
+        Fp2 nm, pr;
+        ld_f2(nm, X, 4 * s + 2 * (jj & 1), 0);
+        f2_mul(pr, nm, f2_pick(s, iv, 3));
+        Fp12* outs[3] = {&a16, &a48, &a57};
+        for (int s2 = 0; s2 < 3; s2++) {
+            Fp12& r = *outs[s2];
+            r.a.a = bcast_f2(pr, 2 * s2);
+            r.a.b = bcast_f2(pr, 2 * s2 + 1);
+            ld_f2(r.b.a, K, 8 * s2, 0);
+            ld_f2(r.b.b, K, 8 * s2 + 2, 0);
+            ld_f2(r.c.a, K, 8 * s2 + 4, 0);
+            ld_f2(r.c.b, K, 8 * s2 + 6, 0);
+        }
+    }
+    return true;
+}
+
 template <bool W>
-static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i) {
+static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i, Soa X) {
     Cyc4 c;
     ld_f2(c.b0, src, 4, i);
     ld_f2(c.b1, src, 6, i);
     ld_f2(c.c0, src, 8, i);
     ld_f2(c.c1, src, 10, i);
+    if (W) {  // one element (k_fexp1): the decompression spread over the lane pairs
+        for (int k = 1; k <= 57; k++) {
+            c4s<W>(c);
+            if (k == 16) st_cyc4(K, 0, i, c);
+            if (k == 48) st_cyc4(K, 8, i, c);
+        }
+        st_cyc4(K, 16, i, c);
+        Fp12 acc, t, y;
+        if (!decompress3_wide(acc, t, y, K, X)) {
+            fx_pow_x_gs<W>(src, dst, i);
+            return;
+        }
+        m12<W>(acc, acc, t);
+        m12<W>(acc, acc, y);
+        for (int k = 0; k < 3; k++) cs12<W>(y, y);
+        m12<W>(acc, acc, y);  // 2^60
+        for (int k = 0; k < 2; k++) cs12<W>(y, y);
+        m12<W>(acc, acc, y);  // 2^62
+        cs12<W>(y, y);
+        m12<W>(acc, acc, y);  // 2^63
+        f12_conj(acc, acc);
+        st_f12(dst, i, acc);
+        return;
+    }
     for (int k = 1; k <= 57; k++) {
         c4s<W>(c);
         if (k == 16) st_cyc4(K, 0, i, c);
@@ -462,18 +641,18 @@ DEV void fexp_chain(size_t n, size_t i, uint32_t* fbuf, uint32_t* scratch) {
     fx_mul<W>(F, OP_CONJ, T, OP_ID, F, i);   // f^(p^6 - 1)
     fx_mul<W>(F, OP_FROB2, F, OP_ID, F, i);  // ^(p^2 + 1)
     fx_cube<W>(F, R, i);                     // res = f^3
-    fx_pow_x<W>(F, T, K, i);
+    fx_pow_x<W>(F, T, K, i, S);
     fx_mul<W>(T, OP_ID, F, OP_CONJ, T, i);   // t = f^(x-1)
-    fx_pow_x<W>(T, A, K, i);
+    fx_pow_x<W>(T, A, K, i, S);
     fx_mul<W>(A, OP_ID, T, OP_CONJ, A, i);   // a = f^((x-1)^2)
     fx_mul<W>(A, OP_FROB2, A, OP_CONJ, S, i);
     fx_mul<W>(S, OP_FROB, R, OP_ID, R, i);   // res *= (a^(p^2) a^-1)^p
-    fx_pow_x<W>(A, T, K, i);                 // b = a^x
+    fx_pow_x<W>(A, T, K, i, S);                 // b = a^x
     fx_mul<W>(T, OP_FROB2, T, OP_CONJ, S, i);
     fx_mul<W>(S, OP_ID, R, OP_ID, R, i);     // res *= b^(p^2) b^-1
-    fx_pow_x<W>(T, A, K, i);                 // c = b^x
+    fx_pow_x<W>(T, A, K, i, S);                 // c = b^x
     fx_mul<W>(A, OP_FROB, R, OP_ID, R, i);   // res *= c^p
-    fx_pow_x<W>(A, T, K, i);                 // d = c^x
+    fx_pow_x<W>(A, T, K, i, S);                 // d = c^x
     fx_mul<W>(T, OP_ID, R, OP_ID, R, i);     // res *= d
 }
 

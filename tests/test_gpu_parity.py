@@ -302,16 +302,20 @@ def test_ragged_batch_sizes_pair_lanes(ctxs, n):
     assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v)
 
 
+WIDE_MAX = 1024  # capi.cpp kWideMax
+
+
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
-    """Batches of <= 512 credentials take the one-wave-per-pair Miller path (capi.cpp kWideMax:
+    """Batches of <= 1,024 credentials take the one-wave-per-pair Miller path (capi.cpp kWideMax:
     k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide), larger ones the pair-lane loop: the same
-    credentials through both (the first 512 of a 520 batch, then alone; then one at a time) give the
-    same verdicts and GT bytes, with every corruption kind (identity sigmas included) in the batch."""
+    credentials through both (a 1,032 batch on the pair-lane path; its first 1,024, then a ragged 37,
+    then single credentials on the wide path) give the same verdicts and GT bytes, with every
+    corruption kind (identity sigmas included) in the batch."""
     import bench
     from coconut import verify_batch
     m = MODES[mode]
-    q, n = 6, 520
+    q, n = 6, WIDE_MAX + 8
     ctx = ctxs[mode]
     b = bench.make_verify_batch(ctx, m, n, q, seed=4242 + m, bad_every=4)
     ctx.set_params(b["g_tilde"])
@@ -319,11 +323,11 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
     sb = 192 if m == 0 else 97
     v_big, gt_big = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], want_gt=True)
     assert np.array_equal(v_big, b["expect"])
-    k = 512
-    v_w, gt_w = verify_batch(ctx, k, q, b["s1"][:k * sb], b["s2"][:k * sb], b["msgs"][:k * q * 48], want_gt=True)
-    assert np.array_equal(v_w, b["expect"][:k])
-    assert gt_w == gt_big[:576 * k]
-    for i in (0, 3, 7, 11, 15, 19, 23, 511):  # valid ones and every corruption kind (bad_every = 4)
+    for k in (WIDE_MAX, 37):
+        v_w, gt_w = verify_batch(ctx, k, q, b["s1"][:k * sb], b["s2"][:k * sb], b["msgs"][:k * q * 48], want_gt=True)
+        assert np.array_equal(v_w, b["expect"][:k])
+        assert gt_w == gt_big[:576 * k]
+    for i in (0, 3, 7, 11, 15, 19, 23, WIDE_MAX - 1, n - 1):  # valid ones and every corruption kind
         v1, g1 = verify_batch(ctx, 1, q, b["s1"][i * sb:(i + 1) * sb], b["s2"][i * sb:(i + 1) * sb],
                               b["msgs"][i * q * 48:(i + 1) * q * 48], want_gt=True)
         assert v1[0] == b["expect"][i], (i, b["kind"][i])
