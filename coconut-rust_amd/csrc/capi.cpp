@@ -66,7 +66,7 @@ int cck_f12_reduce_wide(size_t n, const uint32_t* d_in, uint32_t* d_out, hipStre
 int cck_wide_pairs(int mode, size_t n, size_t ps, const uint32_t* d_prep, const uint32_t* d_flags,
                    const uint32_t* d_gaff, uint32_t* d_wprep, uint32_t* d_wflags, hipStream_t st);
 int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
-             uint8_t* d_gt, hipStream_t st);
+             uint8_t* d_gt, size_t wide_max, hipStream_t st);
 int cck_lagrange(size_t n, size_t len, size_t t, const uint64_t* d_ids, uint32_t* d_l, hipStream_t st);
 int cck_h_input_canon(int group, size_t n, size_t len, int kn, uint8_t* d_data, hipStream_t st);
 
@@ -722,9 +722,9 @@ static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t 
     cc_status ms = launch_miller(c, w, n, st);
     if (ms) return ms;
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
-    // n = 1 takes the one-element fexp (k_fexp1), whose scratch is the context's: only the serialized
-    // path uses it (verify_device)
-    KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt, st));
+    // n <= kWideMax: one wave per credential (k_fexp1, its chain in w.scratch: 72 x 12 x n words)
+    KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt,
+                 kWideMax, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }
@@ -747,6 +747,7 @@ static cc_status slot_begin(cc_ctx* c, hipStream_t st, size_t n, size_t vkw, siz
     w = k ? VerifyWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->vkb, &sl->scratch, &sl->idx, &sl->wprep, &sl->wflags, &sl->wf}
           : ctx_work(c);
     const size_t words = n * 12;
+    if (n <= kWideMax && scratch_bytes < 72 * 12 * n * 4) scratch_bytes = 72 * 12 * n * 4;  // k_fexp1's chain
     if (w.prep->bytes < words * 4 * PREP_SLOTS || w.flags->bytes < n * 4 || w.fbuf->bytes < words * 4 * 12 ||
         w.vkb->bytes < vkw || w.scratch->bytes < scratch_bytes || w.idx->bytes < idx_bytes ||
         wide_short(*w.wprep, *w.wflags, *w.wf, n)) {
@@ -771,13 +772,12 @@ static cc_status slot_end(hipStream_t st, VerifySlot* sl) {
 
 // the *_device verify calls: with one slot, ordered against everything on the context (StreamOrder);
 // with K > 1 (cc_set_concurrency), on the next slot round-robin, ordered only after the context
-// stream's queued work (tables, params) and that slot's previous batch.  n = 1 always takes the
-// serialized path (its one-element final exponentiation uses the context's scratch).
+// stream's queued work (tables, params) and that slot's previous batch.
 static cc_status verify_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s1, const uint8_t* d_s2,
                                const uint8_t* d_msgs, const uint8_t* d_vkX, const uint8_t* d_vkY, uint8_t* d_verdicts,
                                uint8_t* d_gt, hipStream_t st) {
     const size_t vkw = d_vkX ? cck_prep_var_words(c->mode, n, q) * 4 : 0;
-    if (c->concurrency <= 1 || n == 1) {
+    if (c->concurrency <= 1) {
         if (d_vkX && c->vkb.bytes < vkw) drain_slots(c);  // slot 0's batch may still read it
         StreamOrder order(c, st);
         if (d_vkX && c->vkb.ensure(vkw)) return CC_ERR_HIP;
@@ -1032,7 +1032,7 @@ cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_parti
     KCK(cck_rlc_reduce(NF, c->fin_f.as<uint32_t>(), c->fin_scratch.as<uint32_t>(), c->rlc_flag.as<uint32_t>(),
                        c->fin_part.as<uint32_t>(), st));
     KCK(cck_fexp(1, c->fin_part.as<uint32_t>(), c->fin_scratch.as<uint32_t>(), c->fin_part.as<uint32_t>() + RLC_FLAG,
-                 d_accept, d_gt, st));
+                 d_accept, d_gt, 1, st));
     HIPCK(hipEventRecord(c->ev_fin, st));
     c->fin_recorded = true;
     return CC_OK;
@@ -1676,7 +1676,8 @@ static cc_status launch_pok(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, 
     cc_status ms = launch_miller(c, w, n, st);
     if (ms) return ms;
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
-    KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt, st));
+    KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt,
+                 kWideMax, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }

@@ -456,21 +456,21 @@ DEV void ld_cyc4(Cyc4& x, const Soa& K, int base, size_t i) {
 // per-lane form.  Snapshots (Cyc4, 8 slots each) at K slots 0 (g^(2^16)), 8 (g^(2^48)), 16 (g^(2^57));
 // N_b, N_c and then the numerators in the scratch region X (12 slots; the chain's S, free during a
 // pow-by-x).  Returns false on a zero denominator (the Granger-Scott fallback).
-DEV bool decompress3_wide(Fp12& a16, Fp12& a48, Fp12& a57, const Soa& K, const Soa& X) {
+DEV bool decompress3_wide(Fp12& a16, Fp12& a48, Fp12& a57, const Soa& K, const Soa& X, size_t i) {
     const int j = pair_idx();
     {  // squarings of b0, b1, c0, c1 of each snapshot (pairs 0..11)
         const int jj = j % 12;
         Fp2 in, sq;
-        ld_f2(in, K, 8 * (jj >> 2) + 2 * (jj & 3), 0);
+        ld_f2(in, K, 8 * (jj >> 2) + 2 * (jj & 3), i);
         f2_sqr(sq, in);
         for (int s = 0; s < 3; s++) {
             Fp2 t, u;
             f2_mul_xi(t, bcast_f2(sq, 4 * s + 1));
             f2_sub(u, bcast_f2(sq, 4 * s), t);  // N_b = b0^2 - xi b1^2
-            st_f2(X, 4 * s, 0, u);
+            st_f2(X, 4 * s, i, u);
             f2_mul_xi(t, bcast_f2(sq, 4 * s + 3));
             f2_sub(u, bcast_f2(sq, 4 * s + 2), t);  // N_c = c0^2 - xi c1^2
-            st_f2(X, 4 * s + 2, 0, u);
+            st_f2(X, 4 * s + 2, i, u);
         }
     }
     Fp2 d[3];
@@ -478,17 +478,17 @@ DEV bool decompress3_wide(Fp12& a16, Fp12& a48, Fp12& a57, const Soa& K, const S
         const int jj = j % 18, s = jj / 6, t = jj % 6;
         const int c1 = (0x101230 >> (4 * t)) & 15;  // first factor's component: b0 c1 c0 b1 b0 b1
         Fp2 o1, o2, pr;
-        ld_f2(o1, K, 8 * s + 2 * c1, 0);
-        if (t < 4) ld_f2(o2, X, 4 * s + (t == 1 || t == 2 ? 2 : 0), 0);
-        else ld_f2(o2, K, 8 * s + (t == 4 ? 4 : 6), 0);
+        ld_f2(o1, K, 8 * s + 2 * c1, i);
+        if (t < 4) ld_f2(o2, X, 4 * s + (t == 1 || t == 2 ? 2 : 0), i);
+        else ld_f2(o2, K, 8 * s + (t == 4 ? 4 : 6), i);
         f2_mul(pr, o1, o2);
         for (int s2 = 0; s2 < 3; s2++) {
             Fp2 u, v;
             f2_mul_xi(u, bcast_f2(pr, 6 * s2 + 1));
             f2_add(v, bcast_f2(pr, 6 * s2), u);  // a0 numerator: b0 N_b + xi c1 N_c
-            st_f2(X, 4 * s2, 0, v);
+            st_f2(X, 4 * s2, i, v);
             f2_add(v, bcast_f2(pr, 6 * s2 + 2), bcast_f2(pr, 6 * s2 + 3));  // a1 numerator: c0 N_c + b1 N_b
-            st_f2(X, 4 * s2 + 2, 0, v);
+            st_f2(X, 4 * s2 + 2, i, v);
             f2_mul_xi(u, bcast_f2(pr, 6 * s2 + 5));
             f2_sub(v, bcast_f2(pr, 6 * s2 + 4), u);
             f2_dbl(d[s2], v);  // D = 2 (b0 c0 - xi b1 c1)
@@ -514,17 +514,17 @@ DEV bool decompress3_wide(Fp12& a16, Fp12& a48, Fp12& a57, const Soa& K, const S
     {  // pairs 0..5: the a-coefficients, numerator (s, h) times 1/d_s
         const int jj = j % 6, s = jj >> 1;
         Fp2 nm, pr;
-        ld_f2(nm, X, 4 * s + 2 * (jj & 1), 0);
+        ld_f2(nm, X, 4 * s + 2 * (jj & 1), i);
         f2_mul(pr, nm, f2_pick(s, iv, 3));
         Fp12* outs[3] = {&a16, &a48, &a57};
         for (int s2 = 0; s2 < 3; s2++) {
             Fp12& r = *outs[s2];
             r.a.a = bcast_f2(pr, 2 * s2);
             r.a.b = bcast_f2(pr, 2 * s2 + 1);
-            ld_f2(r.b.a, K, 8 * s2, 0);
-            ld_f2(r.b.b, K, 8 * s2 + 2, 0);
-            ld_f2(r.c.a, K, 8 * s2 + 4, 0);
-            ld_f2(r.c.b, K, 8 * s2 + 6, 0);
+            ld_f2(r.b.a, K, 8 * s2, i);
+            ld_f2(r.b.b, K, 8 * s2 + 2, i);
+            ld_f2(r.c.a, K, 8 * s2 + 4, i);
+            ld_f2(r.c.b, K, 8 * s2 + 6, i);
         }
     }
     return true;
@@ -545,7 +545,7 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i, 
         }
         st_cyc4(K, 16, i, c);
         Fp12 acc, t, y;
-        if (!decompress3_wide(acc, t, y, K, X)) {
+        if (!decompress3_wide(acc, t, y, K, X, i)) {
             fx_pow_x_gs<W>(src, dst, i);
             return;
         }
@@ -675,14 +675,18 @@ DEV void fexp_out(size_t n, size_t i, const uint32_t* scratch, const uint32_t* f
     }
 }
 
-// one element on one wave (64 lanes, all pairs holding the same values; pair 0 writes the outputs).
-// One wave per SIMD (HIP's second bound): the whole register file (every step function is a W = true
-// instantiation).  Batches (n > 1) run the quad-lane lazy-field kernel of fexp_q.hip.
-__global__ __launch_bounds__(64, 1) void k_fexp1(uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
+// one element per wave (64 lanes, all pairs holding the same values; pair 0 writes the outputs):
+// element blockIdx.x of n, its chain through SoA scratch of stride n.  One wave per SIMD (HIP's second
+// bound): the whole register file (every step function is a W = true instantiation).  Latency-bound
+// small batches (cck_fexp: n <= kFexpWideMax) and the RLC batch's one product; larger batches run the
+// quad-lane lazy-field kernel of fexp_q.hip.
+__global__ __launch_bounds__(64, 1) void k_fexp1(size_t n, uint32_t* __restrict__ fbuf, uint32_t* __restrict__ scratch,
                                               const uint32_t* __restrict__ flags, uint8_t* __restrict__ verdicts,
                                               uint8_t* __restrict__ gt_out) {
-    fexp_chain<true>(1, 0, fbuf, scratch);
-    fexp_out(1, 0, scratch, flags, verdicts, gt_out, threadIdx.x < 2);
+    const size_t i = blockIdx.x;
+    if (i >= n) return;  // wave-uniform
+    fexp_chain<true>(n, i, fbuf, scratch);
+    fexp_out(n, i, scratch, flags, verdicts, gt_out, threadIdx.x < 2);
 }
 
 // ================================================================ wide Miller loop
@@ -955,12 +959,13 @@ static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + b
 extern "C" int cck_fexp_q(size_t n, const uint32_t* d_f, const uint32_t* d_flags, uint8_t* d_verdicts, uint8_t* d_gt,
                           hipStream_t st);
 
+// n <= wide_max (the caller's threshold; d_scratch >= 72 x 12 x n words): one wave per element, the
+// latency-bound form (k_fexp1); otherwise the quad-lane batch kernel
 extern "C" int cck_fexp(size_t n, uint32_t* d_f, uint32_t* d_scratch, const uint32_t* d_flags, uint8_t* d_verdicts,
-                        uint8_t* d_gt, hipStream_t st) {
+                        uint8_t* d_gt, size_t wide_max, hipStream_t st) {
     if (!n) return 0;
-    if (n > 1) return cck_fexp_q(n, d_f, d_flags, d_verdicts, d_gt, st);
-    // one element (the RLC batch's combined product): latency-bound, the wide one-wave form
-    hipLaunchKernelGGL(cc::pl::k_fexp1, dim3(1), dim3(64), 0, st, d_f, d_scratch, d_flags, d_verdicts, d_gt);
+    if (n > wide_max) return cck_fexp_q(n, d_f, d_flags, d_verdicts, d_gt, st);
+    hipLaunchKernelGGL(cc::pl::k_fexp1, dim3((unsigned)n), dim3(64), 0, st, n, d_f, d_scratch, d_flags, d_verdicts, d_gt);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
