@@ -257,6 +257,46 @@ def default_tables_leg(args, ctx, rebind, step, check, n, dev, dist, unit="crede
             "note": "library default widths (cc_set_table_bits(0, 0)): what a drop-in caller gets without opting in"}
 
 
+def latency_leg(ctx, d_s1, d_s2, d_m, q, expect, dev, ns=(1, 256), reps=5):
+    """Single-call latency of the device verify path (what a drop-in caller waiting on ONE
+    Signature::verify, or a small batch, sees): the first n credentials of the bench batch, inputs
+    resident, one call + synchronize, median of `reps` after a warmup; per-phase times from
+    cc_last_timing.  Batches of <= 1,024 take the one-wave-per-pair path."""
+    import numpy as np
+    import torch
+    import coconut
+    lib = coconut._lib.lib
+    sh = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    out = {}
+    for nn in ns:
+        d_v = torch.zeros(nn, dtype=torch.uint8, device=dev)
+
+        def call():
+            st = lib.cc_verify_batch_device(ctx.h, nn, q, ctypes.c_void_p(d_s1.data_ptr()),
+                                            ctypes.c_void_p(d_s2.data_ptr()), ctypes.c_void_p(d_m.data_ptr()),
+                                            ctypes.c_void_p(d_v.data_ptr()), None, sh)
+            if st != 0:
+                raise RuntimeError(f"cc_verify_batch_device: {lib.cc_status_str(st).decode()}")
+        call()
+        torch.cuda.synchronize(dev)
+        ms = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            call()
+            torch.cuda.synchronize(dev)
+            ms.append((time.perf_counter() - t0) * 1e3)
+        if not np.array_equal(d_v.cpu().numpy(), expect[:nn]):
+            raise SystemExit("latency-leg verdicts disagree with construction — refusing to report a number")
+        ctx.timing(True)
+        call()
+        ph = ctx.last_timing()
+        ctx.timing(False)
+        out[str(nn)] = {"ms": round(float(np.median(ms)), 3), "phase_ms": {"prep": round(ph[0], 3),
+                        "miller": round(ph[1], 3), "fexp": round(ph[2], 3)}}
+    return {"credentials": out, "note": "one cc_verify_batch_device call + synchronize on resident inputs, "
+                                        "median of %d; n <= 1,024 runs one wave per pair" % reps}
+
+
 # ---------------------------------------------------------------- synthetic data (on the GPU)
 def rand_fr(rng):
     return int.from_bytes(rng.bytes(32), "big") % R_ORDER
@@ -476,6 +516,7 @@ def bench_verify(args, mode):
     # verkey tables) and K streams, steps issued round-robin, so one batch's kernel tails overlap the
     # next batch's kernels
     K = max(1, args.inflight)
+    KK = [K]  # slots the steps rotate over (the per-kernel pass below uses one)
     ctx.set_concurrency(K)
     setup_s = time.perf_counter() - t_setup
     d_s1, d_s2, d_m = to_dev(batch["s1"], dev), to_dev(batch["s2"], dev), to_dev(batch["msgs"], dev)
@@ -490,7 +531,7 @@ def bench_verify(args, mode):
     rr = [0]
 
     def step():
-        k = rr[0] % K
+        k = rr[0] % KK[0]
         rr[0] += 1
         st = lib.cc_verify_batch_device(ctx.h, n, q, ctypes.c_void_p(d_s1.data_ptr()),
                                         ctypes.c_void_p(d_s2.data_ptr()), ctypes.c_void_p(d_m.data_ptr()),
@@ -526,7 +567,7 @@ def bench_verify(args, mode):
         if rr[0] > k and not np.array_equal(d_vs[k].cpu().numpy(), batch["expect"]):
             raise SystemExit("verdicts disagree with construction — refusing to report a number")
     ctx.set_concurrency(1)
-    K = 1
+    KK[0] = 1
     rr[0] = 0
     if not timed_phases:  # the per-kernel table from a separate single-batch pass
         ctx.timing(True)
@@ -548,9 +589,21 @@ def bench_verify(args, mode):
             v = coconut.verify_batch(ctx, n, q, batch["s1"], batch["s2"], batch["msgs"])
         pcie_rate = n * reps / (time.perf_counter() - t)
         assert np.array_equal(v, batch["expect"])
-    dflt = default_tables_leg(args, ctx, lambda: ctx.set_verkey(batch["X"], batch["Y"]), step,
-                              lambda: np.array_equal(d_v.cpu().numpy(), batch["expect"]), n, dev, dist)
+    # the library-default tables at the headline's batches in flight
+    def rebind_dflt():
+        ctx.set_verkey(batch["X"], batch["Y"])
+        ctx.set_concurrency(K)
+        KK[0] = K
+        rr[0] = 0
+
+    def check_dflt():
+        ok = all(np.array_equal(d_vs[k].cpu().numpy(), batch["expect"]) for k in range(min(K, rr[0])))
+        ctx.set_concurrency(1)
+        return ok
+    dflt = default_tables_leg(args, ctx, rebind_dflt, step, check_dflt, n, dev, dist)
+    dflt["batches_in_flight"] = K
     dflt.update(table_config(ctx, q))
+    latency = latency_leg(ctx, d_s1, d_s2, d_m, q, batch["expect"], dev)
     if rank == 0:
         key = "verify_sigg2_q6_shared_vk" if mode == 0 else "verify_sigg1_q6_shared_vk"
         counts = opcounts(key)
@@ -581,6 +634,7 @@ def bench_verify(args, mode):
             **lib_info(),
             "pairings_per_s": round(2 * value, 1),
             "default_tables": dflt,
+            "latency": latency,
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),
