@@ -234,30 +234,31 @@ DEV void f4_from_products(Fp4& r, const Fp2& p0, const Fp2& p1, const Fp2& p2) {
 
 // = f12_mul (tower.inc): the six f4 products (t0, t1, t2 and the three cross terms) as 18 Fp2
 // products on pairs 0..17 — f12w_operands picks pair j's two factors, f12w_assemble combines the
-// products (so a caller can run other independent products on pairs 18..31 in the same call)
+// products (so a caller can run other independent products on pairs 18..31 in the same call).
+// Operand m of the six (a, b, c, b + c, a + b, a + c) is formed by each pair for its own m only: one
+// pick of its first term, one of its second (zero for m < 3), one f4 addition.
+DEV Fp4 f4_pick3(int k, const Fp4& a, const Fp4& b, const Fp4& c) {  // k in {0, 1, 2}
+    Fp4 r = a;
+    r.a.c = fp_sel(k == 1, b.a.c, r.a.c);
+    r.b.c = fp_sel(k == 1, b.b.c, r.b.c);
+    r.a.c = fp_sel(k == 2, c.a.c, r.a.c);
+    r.b.c = fp_sel(k == 2, c.b.c, r.b.c);
+    return r;
+}
+DEV Fp4 f12w_term(int m, const Fp12& x) {
+    // first term a b c b a a, second - - - c b c (m = 0..5)
+    Fp4 u = f4_pick3((0x001210 >> (4 * m)) & 15, x.a, x.b, x.c);
+    Fp4 v = f4_pick3((0x212000 >> (4 * m)) & 15, x.a, x.b, x.c);
+    Fp4 r;
+    f4_add(r, u, v);
+    r.a.c = fp_sel(m < 3, u.a.c, r.a.c);
+    r.b.c = fp_sel(m < 3, u.b.c, r.b.c);
+    return r;
+}
 DEV void f12w_operands(Fp2& o1, Fp2& o2, int j, const Fp12& x, const Fp12& y) {
     j %= 18;
     const int m = j / 3, p = j % 3;
-    Fp4 U, V;
-    {
-        Fp4 u[6], v[6];
-        u[0] = x.a; u[1] = x.b; u[2] = x.c;
-        f4_add(u[3], x.b, x.c);
-        f4_add(u[4], x.a, x.b);
-        f4_add(u[5], x.a, x.c);
-        v[0] = y.a; v[1] = y.b; v[2] = y.c;
-        f4_add(v[3], y.b, y.c);
-        f4_add(v[4], y.a, y.b);
-        f4_add(v[5], y.a, y.c);
-        Fp2 ua[6], ub[6], va[6], vb[6];
-        for (int k = 0; k < 6; k++) {
-            ua[k] = u[k].a; ub[k] = u[k].b; va[k] = v[k].a; vb[k] = v[k].b;
-        }
-        U.a = f2_pick(m, ua, 6);
-        U.b = f2_pick(m, ub, 6);
-        V.a = f2_pick(m, va, 6);
-        V.b = f2_pick(m, vb, 6);
-    }
+    const Fp4 U = f12w_term(m, x), V = f12w_term(m, y);
     Fp2 s1, s2;
     o1 = U.a;
     o2 = V.a;
@@ -268,31 +269,49 @@ DEV void f12w_operands(Fp2& o1, Fp2& o2, int j, const Fp12& x, const Fp12& y) {
     o1.c = fp_sel(p == 2, s1.c, o1.c);
     o2.c = fp_sel(p == 2, s2.c, o2.c);
 }
+// The combination, spread: (1) pair k < 12 forms component k & 1 of Fp4 result k / 2 (t0, t1, t2 and
+// the three cross products, f4_mul's (p0 + xi p1, p2 - p0 - p1)) from its three products, gathered
+// with one shuffle each; (2) pair q < 6 forms Fp12 coefficient q (a.a, a.b, b.a, b.b, c.a, c.b) as
+// xi^[q = 0] (G1 - G2 - G3) + xi^[q = 2] G4 from four components of step 1:
+//     a.a = xi (s_bc.b - t1.b - t2.b) + t0.a     a.b = s_bc.a - t1.a - t2.a + t0.b
+//     b.a = s_ab.a - t0.a - t1.a + xi t2.b       b.b = s_ab.b - t0.b - t1.b + t2.a
+//     c.a = s_ac.a - t0.a - t2.a + t1.a          c.b = s_ac.b - t0.b - t2.b + t1.b
+// (3) the six coefficients broadcast to every pair.  Same field values as the sequential assembly.
 DEV void f12w_assemble(Fp12& r, const Fp2& prod, int base = 0) {
-    Fp4 t0, t1, t2, s, w, ra, rb, rc;
-    f4_from_products(t0, bcast_f2(prod, base + 0), bcast_f2(prod, base + 1), bcast_f2(prod, base + 2));
-    f4_from_products(t1, bcast_f2(prod, base + 3), bcast_f2(prod, base + 4), bcast_f2(prod, base + 5));
-    f4_from_products(t2, bcast_f2(prod, base + 6), bcast_f2(prod, base + 7), bcast_f2(prod, base + 8));
-    // (b + c)(b' + c')
-    f4_from_products(s, bcast_f2(prod, base + 9), bcast_f2(prod, base + 10), bcast_f2(prod, base + 11));
-    f4_sub(s, s, t1);
-    f4_sub(s, s, t2);
-    f4_mul_s(s, s);
-    f4_add(ra, s, t0);
-    // (a + b)(a' + b')
-    f4_from_products(s, bcast_f2(prod, base + 12), bcast_f2(prod, base + 13), bcast_f2(prod, base + 14));
-    f4_sub(s, s, t0);
-    f4_sub(s, s, t1);
-    f4_mul_s(w, t2);
-    f4_add(rb, s, w);
-    // (a + c)(a' + c')
-    f4_from_products(s, bcast_f2(prod, base + 15), bcast_f2(prod, base + 16), bcast_f2(prod, base + 17));
-    f4_sub(s, s, t0);
-    f4_sub(s, s, t2);
-    f4_add(rc, s, t1);
-    r.a = ra;
-    r.b = rb;
-    r.c = rc;
+    const int j = pair_idx();
+    Fp2 C;
+    {
+        const int k = j % 12, m = k >> 1;
+        const Fp2 p0 = bcast_f2(prod, base + 3 * m), p1 = bcast_f2(prod, base + 3 * m + 1),
+                  p2 = bcast_f2(prod, base + 3 * m + 2);
+        Fp2 t, ca, cb;
+        f2_mul_xi(t, p1);
+        f2_add(ca, p0, t);
+        f2_sub(t, p2, p0);
+        f2_sub(cb, t, p1);
+        C = ca;
+        C.c = fp_sel(k & 1, cb.c, ca.c);
+    }
+    Fp2 O;
+    {
+        const int q = j % 6;
+        const Fp2 G1 = bcast_f2(C, (0xBA9867 >> (4 * q)) & 15), G2 = bcast_f2(C, (0x101023 >> (4 * q)) & 15),
+                  G3 = bcast_f2(C, (0x543245 >> (4 * q)) & 15);
+        Fp2 G4 = bcast_f2(C, (0x324510 >> (4 * q)) & 15), u, v;
+        f2_sub(u, G1, G2);
+        f2_sub(u, u, G3);
+        f2_mul_xi(v, u);
+        u.c = fp_sel(q == 0, v.c, u.c);
+        f2_mul_xi(v, G4);
+        G4.c = fp_sel(q == 2, v.c, G4.c);
+        f2_add(O, u, G4);
+    }
+    r.a.a = bcast_f2(O, 0);
+    r.a.b = bcast_f2(O, 1);
+    r.b.a = bcast_f2(O, 2);
+    r.b.b = bcast_f2(O, 3);
+    r.c.a = bcast_f2(O, 4);
+    r.c.b = bcast_f2(O, 5);
 }
 DEV void f12_mul_wide(Fp12& r, const Fp12& x, const Fp12& y) {
     Fp2 o1, o2, prod;
