@@ -645,13 +645,16 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
     return CC_OK;
 }
 
-// Batches of up to kWideMax credentials run their Miller loops one wave per pair (fexp_pl.hip
+// Small batches run latency-bound: their Miller loops one wave per pair (n <= kWideMax: fexp_pl.hip
 // k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide) instead of one lane pair per credential (k_miller:
-// one 2-pair loop's latency on a lone wave, ~7.5 ms for any batch up to a few thousand).  k_miller_wide
-// holds one wave a SIMD, so 2 x 512 pairs are one round of the chip's 1,024 SIMDs.  Measured Miller phase
-// (profiles/r05/latency): 1.6 ms at n = 1, 1.9 ms at 512, 3.7 ms at 1,024 against 7.5 ms; at 2,048 the
-// wide path still leads (7.0 ms) but by 7 %, with 32x the lane-work, so the threshold stays at 1,024.
-constexpr size_t kWideMax = 1024;
+// one 2-pair loop's latency on a lone wave, ~7.5 ms for any batch up to a few thousand), and their
+// final exponentiation one wave per credential (n <= kFexpWideMax: k_fexp1, ~1.9 ms) instead of a lane
+// quad (k_fexp_q: ~2.8 ms floor).  Both wide kernels hold one wave a SIMD: 1,024 waves a round of the
+// chip, i.e. 512 credentials a round of the Miller path, 1,024 of the fexp.  Measured
+// (profiles/r05/wide_spread): Miller 0.89 ms at n = 1 .. 512, 1.86 ms at 1,024 against 7.5 ms; fexp
+// 1.9 - 2.0 ms up to 1,024 (a second round would double it against the quad kernel's 2.8).
+constexpr size_t kWideMax = 2048;
+constexpr size_t kFexpWideMax = 1024;
 static bool wide_short(DevBuf& p, DevBuf& f, DevBuf& v, size_t n) {
     const size_t m = 2 * n, words = m * 12;
     return n <= kWideMax && (p.bytes < words * 4 * PREP_SLOTS || f.bytes < m * 4 || v.bytes < words * 4 * 12);
@@ -722,9 +725,9 @@ static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t 
     cc_status ms = launch_miller(c, w, n, st);
     if (ms) return ms;
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
-    // n <= kWideMax: one wave per credential (k_fexp1, its chain in w.scratch: 72 x 12 x n words)
+    // n <= kFexpWideMax: one wave per credential (k_fexp1, its chain in w.scratch: 72 x 12 x n words)
     KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt,
-                 kWideMax, st));
+                 kFexpWideMax, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }
@@ -747,7 +750,7 @@ static cc_status slot_begin(cc_ctx* c, hipStream_t st, size_t n, size_t vkw, siz
     w = k ? VerifyWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->vkb, &sl->scratch, &sl->idx, &sl->wprep, &sl->wflags, &sl->wf}
           : ctx_work(c);
     const size_t words = n * 12;
-    if (n <= kWideMax && scratch_bytes < 72 * 12 * n * 4) scratch_bytes = 72 * 12 * n * 4;  // k_fexp1's chain
+    if (n <= kFexpWideMax && scratch_bytes < 72 * 12 * n * 4) scratch_bytes = 72 * 12 * n * 4;  // k_fexp1's chain
     if (w.prep->bytes < words * 4 * PREP_SLOTS || w.flags->bytes < n * 4 || w.fbuf->bytes < words * 4 * 12 ||
         w.vkb->bytes < vkw || w.scratch->bytes < scratch_bytes || w.idx->bytes < idx_bytes ||
         wide_short(*w.wprep, *w.wflags, *w.wf, n)) {
@@ -1677,7 +1680,7 @@ static cc_status launch_pok(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, 
     if (ms) return ms;
     if (c->timing) (void)hipEventRecord(c->ev[2], st);
     KCK(cck_fexp(n, w.fbuf->as<uint32_t>(), w.scratch->as<uint32_t>(), w.flags->as<uint32_t>(), d_verdicts, d_gt,
-                 kWideMax, st));
+                 kFexpWideMax, st));
     if (c->timing) (void)hipEventRecord(c->ev[3], st);
     return CC_OK;
 }

@@ -302,15 +302,16 @@ def test_ragged_batch_sizes_pair_lanes(ctxs, n):
     assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v)
 
 
-WIDE_MAX = 1024  # capi.cpp kWideMax
+WIDE_MAX, FEXP_WIDE_MAX = 2048, 1024  # capi.cpp kWideMax, kFexpWideMax
 
 
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
-    """Batches of <= 1,024 credentials take the one-wave-per-pair Miller path (capi.cpp kWideMax:
-    k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide), larger ones the pair-lane loop: the same
-    credentials through both (a 1,032 batch on the pair-lane path; its first 1,024, then a ragged 37,
-    then single credentials on the wide path) give the same verdicts and GT bytes, with every
+    """Batches of <= 2,048 credentials take the one-wave-per-pair Miller path (capi.cpp kWideMax:
+    k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide) and those of <= 1,024 also the one-wave-per-
+    credential final exponentiation (kFexpWideMax: k_fexp1); larger ones the pair-lane loop and the
+    quad-lane fexp.  The same credentials through every combination (a 2,056 batch; its first 2,048,
+    1,024 and a ragged 37; then single credentials) give the same verdicts and GT bytes, with every
     corruption kind (identity sigmas included) in the batch."""
     import bench
     from coconut import verify_batch
@@ -323,11 +324,11 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
     sb = 192 if m == 0 else 97
     v_big, gt_big = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], want_gt=True)
     assert np.array_equal(v_big, b["expect"])
-    for k in (WIDE_MAX, 37):
+    for k in (WIDE_MAX, FEXP_WIDE_MAX + 1, FEXP_WIDE_MAX, 37):
         v_w, gt_w = verify_batch(ctx, k, q, b["s1"][:k * sb], b["s2"][:k * sb], b["msgs"][:k * q * 48], want_gt=True)
-        assert np.array_equal(v_w, b["expect"][:k])
-        assert gt_w == gt_big[:576 * k]
-    for i in (0, 3, 7, 11, 15, 19, 23, WIDE_MAX - 1, n - 1):  # valid ones and every corruption kind
+        assert np.array_equal(v_w, b["expect"][:k]), k
+        assert gt_w == gt_big[:576 * k], k
+    for i in (0, 3, 7, 11, 15, 19, 23, FEXP_WIDE_MAX - 1, WIDE_MAX - 1, n - 1):  # every corruption kind
         v1, g1 = verify_batch(ctx, 1, q, b["s1"][i * sb:(i + 1) * sb], b["s2"][i * sb:(i + 1) * sb],
                               b["msgs"][i * q * 48:(i + 1) * q * 48], want_gt=True)
         assert v1[0] == b["expect"][i], (i, b["kind"][i])
