@@ -223,6 +223,44 @@ DEV void cyc4_sqr_wide(Cyc4& x) {
     f2_3u_p2v(x.c1, Xb, x.c1);
 }
 
+// cyc4_sqr with the state spread: pair q (mod 4) holds component q of (b0, b1, c0, c1).  Pair t (mod 6)
+// squares b0, b1, b0 + b1, c0, c1, c0 + c1 (its inputs gathered from pairs 0..3), then pair q forms its
+// new component from three gathered squares S_t:
+//     b0' = 3 xi (S5 - S3 - S4) + 2 b0     b1' = 3 (S3 + xi S4) - 2 b1
+//     c0' = 3 (S0 + xi S1) - 2 c0          c1' = 3 (S2 - S0 - S1) + 2 c1
+// — the same values as cyc4_sqr_wide without every pair redoing all four.
+DEV void cyc4_sqr_dist(Fp2& V) {
+    const int j = pair_idx(), t = j % 6, q = j & 3;
+    Fp2 a = bcast_f2(V, (0x232010 >> (4 * t)) & 15), b = bcast_f2(V, (0x300100 >> (4 * t)) & 15), s, sq;
+    f2_add_lz(s, a, b);
+    a.c = fp_sel(t == 2 || t == 5, s.c, a.c);
+    f2_sqr(sq, a);
+    const Fp2 G1 = bcast_f2(sq, (0x2035 >> (4 * q)) & 15), G2 = bcast_f2(sq, (0x0143 >> (4 * q)) & 15),
+              G3 = bcast_f2(sq, (0x1004 >> (4 * q)) & 15);
+    const bool xf = q == 0 || q == 3;  // X family: G1 - G2 - G3 (times xi for b0'); else T: G1 + xi G2
+    Fp2 x, u, w;
+    f2_sub(x, G1, G2);
+    f2_sub(x, x, G3);
+    f2_mul_xi(u, x);
+    x.c = fp_sel(q == 0, u.c, x.c);
+    f2_mul_xi(u, G2);
+    f2_add(w, G1, u);
+    u = w;
+    u.c = fp_sel(xf, x.c, w.c);
+    f2_neg(w, V);  // 3u + 2V = u + 2 (u + V) (X family), 3u - 2V = u + 2 (u - V) (T family)
+    w.c = fp_sel(xf, V.c, w.c);
+    f2_add(w, u, w);
+    f2_dbl(w, w);
+    f2_add(V, w, u);
+}
+DEV void st_cyc4_dist(const Soa& K, int base, size_t i, const Fp2& V) {
+    Cyc4 c{bcast_f2(V, 0), bcast_f2(V, 1), bcast_f2(V, 2), bcast_f2(V, 3)};
+    st_f2(K, base + 0, i, c.b0);
+    st_f2(K, base + 2, i, c.b1);
+    st_f2(K, base + 4, i, c.c0);
+    st_f2(K, base + 6, i, c.c1);
+}
+
 // f4_mul's three products of operand set m, spread: pair 3m + p computes product p
 DEV void f4_from_products(Fp4& r, const Fp2& p0, const Fp2& p1, const Fp2& p2) {
     Fp2 t;
@@ -556,13 +594,15 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i, 
     ld_f2(c.b1, src, 6, i);
     ld_f2(c.c0, src, 8, i);
     ld_f2(c.c1, src, 10, i);
-    if (W) {  // one element (k_fexp1): the decompression spread over the lane pairs
+    if (W) {  // one element (k_fexp1): the squarings' state and the decompression spread over the pairs
+        Fp2 V;
+        ld_f2(V, src, 4 + 2 * (pair_idx() & 3), i);
         for (int k = 1; k <= 57; k++) {
-            c4s<W>(c);
-            if (k == 16) st_cyc4(K, 0, i, c);
-            if (k == 48) st_cyc4(K, 8, i, c);
+            cyc4_sqr_dist(V);
+            if (k == 16) st_cyc4_dist(K, 0, i, V);
+            if (k == 48) st_cyc4_dist(K, 8, i, V);
         }
-        st_cyc4(K, 16, i, c);
+        st_cyc4_dist(K, 16, i, V);
         Fp12 acc, t, y;
         if (!decompress3_wide(acc, t, y, K, X, i)) {
             fx_pow_x_gs<W>(src, dst, i);
