@@ -40,6 +40,9 @@ int cck_sigreq_verify(int group, size_t n, int k, const uint8_t* d_g, const uint
 int cck_prep(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
              const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
              uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
+int cck_prep_wide(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
+                  const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits, const uint32_t* d_binf_fixed,
+                  uint32_t* d_prep, uint32_t* d_flags, hipStream_t st);
 size_t cck_prep_var_words(int mode, size_t n, size_t q);
 int cck_prep_var(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_vkX,
                  const uint8_t* d_vkY, const uint8_t* d_msgs, uint32_t* d_scratch, uint32_t* d_prep,
@@ -717,10 +720,11 @@ static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t 
     if (d_vkX)
         KCK(cck_prep_var(c->mode, n, (int)q, d_s1, d_s2, d_vkX, d_vkY, d_msgs, w.vkb->as<uint32_t>(),
                          w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), st));
-    else
-        KCK(cck_prep(c->mode, n, (int)q, d_s1, d_s2, d_msgs, c->vk_aff.as<uint32_t>(), c->X_inf,
-                     c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(),
-                     w.flags->as<uint32_t>(), st));
+    else  // small batches: one wave per credential, the MSM's window terms over its lanes
+        KCK((n <= kWideMax ? cck_prep_wide : cck_prep)(c->mode, n, (int)q, d_s1, d_s2, d_msgs,
+                                                       c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(),
+                                                       c->wbits, c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(),
+                                                       w.flags->as<uint32_t>(), st));
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     cc_status ms = launch_miller(c, w, n, st);
     if (ms) return ms;

@@ -380,6 +380,124 @@ __global__ __launch_bounds__(256, 2) void k_prep_sigg1_pair(size_t n, int q, con
     if (!h) flags[i] = fl;
 }
 
+// Small batches (capi.cpp: n <= kWideMax): ONE WAVE per credential, its verkey MSM's window terms
+// spread over the lanes.  The pair kernels above walk all q x nwin terms on one lane (pair) — the whole
+// launch then lasts one such chain, however few credentials there are.  Here term t = (j, w) goes to
+// lane (pair) t mod 64 (32), lane (pair) 0 also takes X~, and a butterfly sums the partial sums
+// (curve.h lane_group_sum / curve_pl.h pair_group_sum).  Same outputs as the pair kernels: sigma_1 /
+// -sigma_2 decoded by lanes 0 / 1, pr affine as the Miller loop's operand, flags.
+__global__ __launch_bounds__(64) void k_prep_sigg2_wide(size_t n, int q, const uint8_t* __restrict__ s1b,
+                                                        const uint8_t* __restrict__ s2b,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                        const uint32_t* __restrict__ table, int wbits,
+                                                        const uint32_t* __restrict__ binf_fixed,
+                                                        uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
+    const size_t i = blockIdx.x;
+    if (i >= n) return;  // wave-uniform
+    const int l = (int)threadIdx.x, h = l & 1;
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp2> a;
+        if (!g2_decode(a, (h ? s2b : s1b) + i * 192)) fl |= h ? 2u : 1u;
+        if (h) f2_neg(a.y, a.y);  // -sigma_2
+        if (l < 2) {
+            st_f2(S, h ? S_Q2 : S_Q1, i, a.x);
+            st_f2(S, (h ? S_Q2 : S_Q1) + 2, i, a.y);
+        }
+    }
+    fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
+    const int nwin = ft_nwin(wbits), nt = q * nwin;
+    Jac<Fp> acc;
+    if (l == 0 && !Xinf) {
+        Aff<Fp> x;
+        ld_aff_aos<Fp>(x, Xaff);
+        jac_from_aff(acc, x);
+    } else {
+        jac_set_inf(acc);
+    }
+    {
+        lz::JG a = lz::jg_from(acc);
+#pragma unroll 1
+        for (int t = l; t < nt; t += 64) {
+            const int j = t / nwin, w = t - j * nwin;
+            if (binf_fixed[j]) continue;
+            Fr m;
+            fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
+            ft_add_lz(a, m.v, table, wbits, j, w, w + 1);
+        }
+        acc = lz::jg_to(a);
+    }
+    lane_group_sum<Fp, 64>(acc);  // every lane the same sum
+    if (jac_is_inf(acc)) {
+        fl |= 4u;
+    } else {
+        Fp x, y;
+        lz::jg_to_aff_rp(x, y, lz::jg_from(acc));
+        if (l < 2) st_fp(S, S_P1 + h, i, h ? y : x);
+    }
+    if (l == 0) flags[i] = fl;
+}
+
+__global__ __launch_bounds__(64) void k_prep_sigg1_wide(size_t n, int q, const uint8_t* __restrict__ s1b,
+                                                        const uint8_t* __restrict__ s2b,
+                                                        const uint8_t* __restrict__ msgs,
+                                                        const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                        const uint32_t* __restrict__ table, int wbits,
+                                                        const uint32_t* __restrict__ binf_fixed,
+                                                        uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
+    const size_t i = blockIdx.x;
+    if (i >= n) return;  // wave-uniform
+    const int l = (int)threadIdx.x, h = l & 1, p = l >> 1;
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp> a;
+        if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
+        if (h) fp_neg(a.y, a.y);  // -sigma_2
+        fp_to_lazy_form(a.x);     // the Miller loop's affine P in the lazy R' form (kAffRp)
+        fp_to_lazy_form(a.y);
+        if (l < 2) {
+            st_fp(S, h ? S_P2 : S_P1, i, a.x);
+            st_fp(S, (h ? S_P2 : S_P1) + 1, i, a.y);
+        }
+    }
+    fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
+    Jac<pl::Fp2> acc;
+    if (p == 0 && !Xinf) {
+        Aff<pl::Fp2> x;
+        for (int c = 0; c < NL; c++) {
+            x.x.c.v[c] = Xaff[NL * h + c];
+            x.y.c.v[c] = Xaff[2 * NL + NL * h + c];
+        }
+        jac_from_aff(acc, x);
+    } else {
+        jac_set_inf(acc);
+    }
+    {
+        const int nwin = ft_nwin(wbits), nt = q * nwin;
+        lz::JL la = pl::jl_from_pl(acc);
+#pragma unroll 1
+        for (int t = p; t < nt; t += 32) {  // pair-uniform
+            const int j = t / nwin, w = t - j * nwin;
+            if (binf_fixed[j]) continue;
+            Fr m;
+            fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
+            pl::ft_add_g2_lz(la, m.v, table, wbits, j, w, w + 1);
+        }
+        acc = pl::jl_to_pl(la);
+    }
+    pl::pair_group_sum<64>(acc);  // every pair the same sum
+    Aff<pl::Fp2> a;
+    if (!jac_to_aff(a, acc)) fl |= 4u;
+    if (p == 0) {
+        pl::st_f2(S, S_Q1, i, a.x);
+        pl::st_f2(S, S_Q1 + 2, i, a.y);
+    }
+    if (l == 0) flags[i] = fl;
+}
+
 // Fixed-argument lines for the constant G2 point g~ (SigG1): per Miller step, (l0, l2c, l3c)
 // — 63 doubling + 5 addition steps, stored in loop order.  One thread computes them at setup.
 __global__ __launch_bounds__(64) void k_gtilde_lines(const uint32_t* __restrict__ gtilde, uint32_t* __restrict__ lines) {
@@ -499,6 +617,21 @@ int cck_prep(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2
     else
         hipLaunchKernelGGL(k_prep_sigg1_pair, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_msgs,
                            d_Xaff, Xinf, d_table, wbits, d_binf_fixed, d_prep, d_flags);
+    CC_CHECK(hipGetLastError());
+    return 0;
+}
+
+// the small-batch form (one wave per credential, k_prep_*_wide): same arguments and outputs as cck_prep
+int cck_prep_wide(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_msgs,
+                  const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
+                  const uint32_t* d_binf_fixed, uint32_t* d_prep, uint32_t* d_flags, hipStream_t st) {
+    if (!n) return 0;
+    if (mode == 0)
+        hipLaunchKernelGGL(k_prep_sigg2_wide, dim3((unsigned)n), dim3(64), 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf,
+                           d_table, wbits, d_binf_fixed, d_prep, d_flags);
+    else
+        hipLaunchKernelGGL(k_prep_sigg1_wide, dim3((unsigned)n), dim3(64), 0, st, n, q, d_s1, d_s2, d_msgs, d_Xaff, Xinf,
+                           d_table, wbits, d_binf_fixed, d_prep, d_flags);
     CC_CHECK(hipGetLastError());
     return 0;
 }
