@@ -372,30 +372,34 @@ DEV void f12_cyc_sqr_wide(Fp12& r, const Fp12& x) {
     o1.c = fp_sel(j & 1, s0.c, o1.c);
     o2.c = fp_sel(j & 1, s1.c, o2.c);
     f2_mul(prod, o1, o2);
-    Fp4 sq[3];
-    for (int k = 0; k < 3; k++) {  // f4_sqr from its two products
-        const Fp2 ab = bcast_f2(prod, 2 * k);
-        Fp2 t = bcast_f2(prod, 2 * k + 1), u;
-        f2_sub(t, t, ab);
-        f2_mul_xi(u, ab);
-        f2_sub(sq[k].a, t, u);
-        f2_dbl(sq[k].b, ab);
-    }
-    // a' = 3A - 2 conj(a), b' = 3 s C + 2 conj(b), c' = 3 B - 2 conj(c)  (A = a^2, B = b^2, C = c^2)
-    Fp4 t;
-    f4_sub_conj(t, sq[0], x.a);
-    f4_dbl(t, t);
-    f4_add(r.a, t, sq[0]);
-    Fp4 Bs;
-    f4_mul_s(Bs, sq[2]);
-    f4_add_conj(t, Bs, x.b);
-    f4_dbl(t, t);
-    Fp4 rb;
-    f4_add(rb, t, Bs);
-    f4_sub_conj(t, sq[1], x.c);
-    f4_dbl(t, t);
-    f4_add(r.c, t, sq[1]);
-    r.b = rb;
+    // the combination, spread: pair q < 6 forms coefficient q (a.a, a.b, b.a, b.b, c.a, c.b) of
+    //   a' = 3A - 2 conj(a), b' = 3 s C + 2 conj(b), c' = 3 B - 2 conj(c)   (A, B, C the f4 squares:
+    //   (t - ab - xi ab, 2ab) from pair 2m's ab and pair 2m + 1's t = (a + b)(a + xi b))
+    // as 3u - 2y with u = t - ab - xi ab (a.a, b.b, c.a) or 3u + 2y with u = 2ab (xi 2ab for b.a)
+    const int q = pair_idx() % 6;
+    const Fp2 Gab = bcast_f2(prod, (0x224400 >> (4 * q)) & 15), Gt = bcast_f2(prod, (0x135111 >> (4 * q)) & 15);
+    const bool fa = q == 0 || q == 3 || q == 4;
+    Fp2 u, v, w, y;
+    f2_sub(u, Gt, Gab);
+    f2_mul_xi(v, Gab);
+    f2_sub(u, u, v);
+    f2_dbl(w, Gab);
+    f2_mul_xi(v, w);
+    w.c = fp_sel(q == 2, v.c, w.c);
+    u.c = fp_sel(fa, u.c, w.c);
+    const Fp2 cs[6] = {x.a.a, x.a.b, x.b.a, x.b.b, x.c.a, x.c.b};
+    y = f2_pick(q, cs, 6);
+    f2_neg(v, y);
+    y.c = fp_sel(fa, v.c, y.c);
+    f2_add(w, u, y);  // u +- y
+    f2_dbl(w, w);
+    f2_add(v, w, u);  // 3u +- 2y
+    r.a.a = bcast_f2(v, 0);
+    r.a.b = bcast_f2(v, 1);
+    r.b.a = bcast_f2(v, 2);
+    r.b.b = bcast_f2(v, 3);
+    r.c.a = bcast_f2(v, 4);
+    r.c.b = bcast_f2(v, 5);
 }
 
 // k Fp4 products x_m y_m (m < k <= 10) as 3k Fp2 products on pairs 0..3k-1 (f4_mul's Karatsuba: pair
