@@ -257,44 +257,48 @@ def default_tables_leg(args, ctx, rebind, step, check, n, dev, dist, unit="crede
             "note": "library default widths (cc_set_table_bits(0, 0)): what a drop-in caller gets without opting in"}
 
 
-def latency_leg(ctx, d_s1, d_s2, d_m, q, expect, dev, ns=(1, 256), reps=5):
-    """Single-call latency of the device verify path (what a drop-in caller waiting on ONE
-    Signature::verify, or a small batch, sees): the first n credentials of the bench batch, inputs
-    resident, one call + synchronize, median of `reps` after a warmup; per-phase times from
-    cc_last_timing.  Batches of <= 1,024 take the one-wave-per-pair path."""
+def latency_of(ctx, launch, expect, dev, ns=(1, 256), reps=5, what="credentials"):
+    """Single-call latency of a device entry point (what a drop-in caller waiting on ONE call sees):
+    launch(nn, d_verdicts, stream_handle) on the first nn items of the bench batch, inputs resident, one
+    call + synchronize, median of `reps` after a warmup; per-phase times from cc_last_timing."""
     import numpy as np
     import torch
-    import coconut
-    lib = coconut._lib.lib
     sh = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     out = {}
     for nn in ns:
         d_v = torch.zeros(nn, dtype=torch.uint8, device=dev)
-
-        def call():
-            st = lib.cc_verify_batch_device(ctx.h, nn, q, ctypes.c_void_p(d_s1.data_ptr()),
-                                            ctypes.c_void_p(d_s2.data_ptr()), ctypes.c_void_p(d_m.data_ptr()),
-                                            ctypes.c_void_p(d_v.data_ptr()), None, sh)
-            if st != 0:
-                raise RuntimeError(f"cc_verify_batch_device: {lib.cc_status_str(st).decode()}")
-        call()
+        launch(nn, d_v, sh)
         torch.cuda.synchronize(dev)
         ms = []
         for _ in range(reps):
             t0 = time.perf_counter()
-            call()
+            launch(nn, d_v, sh)
             torch.cuda.synchronize(dev)
             ms.append((time.perf_counter() - t0) * 1e3)
         if not np.array_equal(d_v.cpu().numpy(), expect[:nn]):
             raise SystemExit("latency-leg verdicts disagree with construction — refusing to report a number")
         ctx.timing(True)
-        call()
+        launch(nn, d_v, sh)
         ph = ctx.last_timing()
         ctx.timing(False)
         out[str(nn)] = {"ms": round(float(np.median(ms)), 3), "phase_ms": {"prep": round(ph[0], 3),
                         "miller": round(ph[1], 3), "fexp": round(ph[2], 3)}}
-    return {"credentials": out, "note": "one cc_verify_batch_device call + synchronize on resident inputs, "
-                                        "median of %d; n <= 1,024 runs one wave per pair" % reps}
+    return {what: out, "note": "one device call + synchronize on resident inputs, median of %d; batches of "
+                               "<= 2,048 run the one-wave-per-pair Miller loop (<= 1,024: one-wave fexp, "
+                               "verify prep)" % reps}
+
+
+def latency_leg(ctx, d_s1, d_s2, d_m, q, expect, dev, ns=(1, 256), reps=5):
+    """latency_of for cc_verify_batch_device (shared verkey): one Signature::verify, a batch of 256."""
+    import coconut
+    lib = coconut._lib.lib
+
+    def launch(nn, d_v, sh):
+        st = lib.cc_verify_batch_device(ctx.h, nn, q, ctypes.c_void_p(d_s1.data_ptr()), ctypes.c_void_p(d_s2.data_ptr()),
+                                        ctypes.c_void_p(d_m.data_ptr()), ctypes.c_void_p(d_v.data_ptr()), None, sh)
+        if st != 0:
+            raise RuntimeError(f"cc_verify_batch_device: {lib.cc_status_str(st).decode()}")
+    return latency_of(ctx, launch, expect, dev, ns, reps)
 
 
 # ---------------------------------------------------------------- synthetic data (on the GPU)

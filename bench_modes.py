@@ -380,6 +380,7 @@ def bench_pok(args):
     for k in range(K):
         if rr[0] > k and not np.array_equal(d_vs[k].cpu().numpy(), b["expect"]):
             raise SystemExit("PoK verdicts disagree with construction — refusing to report a number")
+    K0 = K
     if K > 1:  # the per-kernel table from a separate single-batch pass
         ctx.set_concurrency(1)
         K = 1
@@ -394,9 +395,29 @@ def bench_pok(args):
     value = n * world * args.steps / el
     from bench import default_tables_leg, table_config
     opt_in = table_config(ctx, q)
-    dflt = default_tables_leg(args, ctx, lambda: ctx.set_verkey(b["X"], b["Y"]), step,
-                              lambda: np.array_equal(d_v.cpu().numpy(), b["expect"]), n, dev, dist, unit="proofs/s")
+
+    def rebind_dflt():  # the library-default tables at the headline's batches in flight
+        nonlocal K
+        ctx.set_verkey(b["X"], b["Y"])
+        ctx.set_concurrency(K0)
+        K = K0
+        rr[0] = 0
+
+    def check_dflt():
+        ok = all(np.array_equal(d_vs[k].cpu().numpy(), b["expect"]) for k in range(min(K0, rr[0])))
+        ctx.set_concurrency(1)
+        return ok
+    dflt = default_tables_leg(args, ctx, rebind_dflt, step, check_dflt, n, dev, dist, unit="proofs/s")
+    dflt["batches_in_flight"] = K0
     dflt.update(table_config(ctx, q))
+    from bench import latency_of
+
+    def pok_launch(nn, d_vv, sh):  # the first nn proofs (proof-major inputs)
+        st = lib.cc_pok_verify_batch_device(ctx.h, nn, q, r, nresp, P("s1"), P("s2"), P("J"), P("T"), P("resp"),
+                                            P("chal"), ridx, P("rev"), ctypes.c_void_p(d_vv.data_ptr()), None, sh)
+        if st:
+            raise RuntimeError(f"cc_pok_verify_batch_device: {lib.cc_status_str(st).decode()}")
+    latency = latency_of(ctx, pok_launch, b["expect"], dev, what="proofs")
     if rank == 0:
         from bench import kernel_table, cpu_info, kernel_pmc_report
         peak = peak_mad_per_s()
@@ -417,6 +438,7 @@ def bench_pok(args):
                        "verkey_tables": "opt-in width (bench); library default <= 4 GiB"},
             **__import__("bench").lib_info(),
             "default_tables": dflt,
+            "latency": latency,
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),
@@ -503,6 +525,13 @@ def bench_pervk(args):
         ctx.timing(False)
         phase_ms = ph / max(min(args.steps, 5), 1)
     value = n * world * args.steps / el
+    from bench import latency_of
+
+    def pervk_launch(nn, d_vv, sh):  # the first nn credentials (credential-major inputs)
+        st = lib.cc_verify_batch_pervk_device(ctx.h, nn, q, *P, ctypes.c_void_p(d_vv.data_ptr()), None, sh)
+        if st:
+            raise RuntimeError(f"cc_verify_batch_pervk_device: {lib.cc_status_str(st).decode()}")
+    latency = latency_of(ctx, pervk_launch, b["expect"], dev)
     if rank == 0:
         key = "verify_sigg2_q6_pervk" if mode == 0 else "verify_sigg1_q6_pervk"
         counts = opcounts(key)
@@ -533,6 +562,7 @@ def bench_pervk(args):
                          "whole_step_frac": round(total / (el / args.steps) / peak, 4)},
             "kernels": kt,
             "prep_over_miller": round(kt["prep"]["ms"] / kt["miller"]["ms"], 3) if kt["miller"]["ms"] else None,
+            "latency": latency,
             "rocprof_kernels": __import__("bench").kernel_pmc_report(args.mode),
             "setup": {"synthetic_data_s": round(gen_s, 2)},
         }
