@@ -97,7 +97,11 @@ cc_status cc_table_bits(const cc_ctx* ctx, int* verkey_bits, int* issuer_bits);
  *   verdicts       : n bytes, 1 = verify() returned true
  *   gt_or_null     : n x 576 B, e(.,.)*e(.,.) as amcl_wrapper GT::to_bytes, or NULL
  *   rlc            : 0 = per-credential; 1 = random-linear-combination batch (all-or-fallback)
- * Returns CC_ERR_LEN if q differs from the shared verkey's q (the reference panics there). */
+ * Returns CC_ERR_LEN if q differs from the shared verkey's q (the reference panics there).
+ * Batch size picks the kernels, not the results: a batch of up to 2,048 credentials runs latency-bound
+ * (one wave per Miller pair; up to 1,024 also one wave per final exponentiation and, shared verkey, per
+ * prep), a larger one throughput-bound (one lane pair per credential); verdicts and GT bytes are the
+ * same either way. */
 cc_status cc_verify_batch(cc_ctx* ctx, size_t n, size_t q, const uint8_t* sigma1, const uint8_t* sigma2,
                           const uint8_t* msgs, const uint8_t* vk_X, const uint8_t* vk_Y, uint8_t* verdicts,
                           uint8_t* gt_or_null, int rlc);
@@ -124,7 +128,7 @@ cc_status cc_verify_batch_pervk_device(cc_ctx* ctx, size_t n, size_t q, const ui
  * delta/fold buffers; the verkey tables are shared)
  * and are ordered only after the context's earlier work (tables, params) and the same slot's previous
  * batch — so K batches issued on K caller streams overlap on the device (one batch's kernel tails with
- * the next batch's kernels).  An n = 1 verify call takes the serialized path.  Every other
+ * the next batch's kernels).  Every other
  * entry point, and cc_set_params / cc_set_verkey, first waits for the slots' batches.  The per-phase
  * timing (cc_last_timing) is meaningful with one slot only.  slots: 1 (default, every call ordered
  * against every other) .. 8.  cc_concurrency reports the current value. */
