@@ -760,6 +760,303 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_g1pl(size_t n, int q, int r
     if (!h) flags[i] = fl;
 }
 
+// ---------------------------------------------------------------- small batches: one block per proof
+// The two PoK preps above walk a proof's whole Schnorr MSM (g~ and every hidden Y~ times its response,
+// nwin table windows each), chal J and J' on one lane (pair) or two waves' lanes: for a small batch the
+// launch then lasts that chain (~9 ms at n = 1).  Here one BLOCK of two waves takes one proof: wave 0
+// decodes sigma' and runs chal J (a 256-doubling chain, the part no lane split shortens), wave 1
+// spreads the table terms over its lanes (G1) or lane pairs (G2) — term t = (response or revealed
+// message, window) to lane t mod L — adds -T and X~ + J on two of them, and butterfly-sums the
+// Schnorr part and J'.  The Schnorr parts meet in LDS.  Same outputs as the kernels above.
+DEV bool pok_revealed(int hh, int r, const uint32_t* rev_idx) {
+    bool rv = false;
+    for (int z = 0; z < r; z++) rv |= rev_idx[z] == (uint32_t)hh;
+    return rv;
+}
+DEV int rot_start(int lane, int t0, int L) { return ((lane - t0) % L + L) % L; }
+
+__global__ __launch_bounds__(128) void k_prep_pok_wide_sigg2(size_t n, int q, int r, const uint8_t* __restrict__ s1b,
+                                                            const uint8_t* __restrict__ s2b,
+                                                            const uint8_t* __restrict__ Jb,
+                                                            const uint8_t* __restrict__ Tb,
+                                                            const uint8_t* __restrict__ resp,
+                                                            const uint8_t* __restrict__ chal,
+                                                            const uint8_t* __restrict__ rev_msgs,
+                                                            const uint32_t* __restrict__ rev_idx,
+                                                            const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                            const uint32_t* __restrict__ table, int wbits,
+                                                            const uint32_t* __restrict__ binf,
+                                                            uint32_t* __restrict__ prep, uint32_t* __restrict__ flags,
+                                                            uint32_t* __restrict__ jtab) {
+    using FS_ = Fp2;
+    using FO = Fp;
+    constexpr int JW = sizeof(Jac<FO>) / 4;
+    constexpr int SB = ebytes<FS_>(), OB = ebytes<FO>();
+    __shared__ uint32_t part[JW + 1];  // wave 1's Schnorr part and flag bits
+    const size_t i = blockIdx.x;
+    if (i >= n) return;  // block-uniform
+    const int l = (int)(threadIdx.x & 63);
+    const bool w1 = threadIdx.x >= 64;  // wave-uniform
+    Soa S{prep, n};
+    Aff<FO> Ja;
+    const bool Jok = decode_pt<FO>(Ja, Jb + i * OB);
+    if (!w1) {
+        uint32_t fl = 0;
+        {
+            Aff<FS_> a;
+            const Fp* pa = reinterpret_cast<const Fp*>(&a);
+            if (!decode_pt<FS_>(a, s1b + i * SB)) fl |= 1u;
+            if (l == 0)
+                for (int c = 0; c < 4; c++) st_fp(S, S_Q1 + c, i, pa[c]);
+            if (!decode_pt<FS_>(a, s2b + i * SB)) fl |= 2u;
+            FT<FS_>::neg(a.y, a.y);
+            if (l == 0)
+                for (int c = 0; c < 4; c++) st_fp(S, S_Q2 + c, i, pa[c]);
+        }
+        Jac<FO> acc;
+        jac_set_inf(acc);
+        if (Jok) {  // chal J in fixed 4-bit windows (k_prep_pok_split), every lane the same chain
+            Fr k;
+            fr_from_be48(k, chal + i * 48);
+            constexpr int LW = sizeof(lz::JG) / 4;
+            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * LW + w) * n + i]; };
+            const lz::AG Jl{lz::fit<lz::AN, lz::BC>(lz::reduce(lz::in_r(Ja.x))), lz::fit<lz::AN, lz::BC>(lz::reduce(lz::in_r(Ja.y)))};
+            lz::JG t = lz::jg_add_aff(lz::jg_inf(), Jl);
+#pragma unroll 1
+            for (int d = 1; d <= 15; d++) {
+                if (d > 1) t = lz::jg_add_aff(t, Jl);
+                const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
+                for (int w = 0; w < LW; w++) tab(d, w) = tw[w];
+            }
+            lz::JG sacc = lz::jg_inf();
+#pragma unroll 1
+            for (int win = 63; win >= 0; win--) {
+                for (int b = 0; b < 4; b++) sacc = lz::jg_dbl(sacc);
+                const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
+                if (d) {
+                    uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
+                    for (int w = 0; w < LW; w++) tw[w] = tab((int)d, w);
+                    sacc = lz::jg_add(sacc, t);
+                }
+            }
+            acc = lz::jg_to(sacc);
+        }
+        __syncthreads();
+        Jac<FO> o;
+        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+        for (int c = 0; c < JW; c++) ow[c] = part[c];
+        fl |= part[JW];
+        jac_add(acc, acc, o);
+        if (!jac_is_inf(acc)) fl |= 8u;
+        if (l == 0) flags[i] = fl;
+        return;
+    }
+    const uint8_t* rp = resp + i * (size_t)(q - r + 1) * 48;
+    const int nwin = ft_nwin(wbits), nresp = q - r + 1;
+    lz::JG la = lz::jg_inf(), lj = lz::jg_inf();
+    int hh = -1;
+#pragma unroll 1
+    for (int s = 0; s < nresp; s++) {  // response s: g~ (s = 0, table base q) or the s-th hidden Y~
+        int base = q;
+        if (s) {
+            do hh++;
+            while (pok_revealed(hh, r, rev_idx));
+            base = hh;
+        }
+        if (binf[base]) continue;
+        Fr k;
+        fr_from_be48(k, rp + (size_t)s * 48);
+#pragma unroll 1
+        for (int w = rot_start(l, s * nwin, 64); w < nwin; w += 64) ft_add_lz(la, k.v, table, wbits, base, w, w + 1);
+    }
+#pragma unroll 1
+    for (int z = 0; z < r; z++) {  // J' terms: revealed messages, the lane rotation continued
+        const int base = (int)rev_idx[z];
+        if (binf[base]) continue;
+        Fr m;
+        fr_from_be48(m, rev_msgs + ((size_t)i * r + z) * 48);
+#pragma unroll 1
+        for (int w = rot_start(l, (nresp + z) * nwin, 64); w < nwin; w += 64) ft_add_lz(lj, m.v, table, wbits, base, w, w + 1);
+    }
+    Jac<FO> acc = lz::jg_to(la), jp = lz::jg_to(lj);
+    if (l == 63) {  // -T
+        Aff<FO> Ta;
+        if (decode_pt<FO>(Ta, Tb + i * OB)) {
+            FT<FO>::neg(Ta.y, Ta.y);
+            jac_add_aff(acc, acc, Ta);
+        }
+    }
+    if (l == 62) {  // X~ + J
+        if (!Xinf) {
+            Aff<FO> x;
+            ld_aff_aos<FO>(x, Xaff);
+            jac_add_aff(jp, jp, x);
+        }
+        if (Jok) jac_add_aff(jp, jp, Ja);
+    }
+    lane_group_sum<FO, 64>(acc);
+    lane_group_sum<FO, 64>(jp);
+    uint32_t fl = 0;
+    if (jac_is_inf(jp)) {
+        fl |= 4u;
+    } else {
+        Fp x, y;
+        lz::jg_to_aff_rp(x, y, lz::jg_from(jp));
+        if (l == 0) {
+            st_fp(S, S_P1, i, x);
+            st_fp(S, S_P1 + 1, i, y);
+        }
+    }
+    if (l == 0) {
+        const uint32_t* aw = reinterpret_cast<const uint32_t*>(&acc);
+        for (int c = 0; c < JW; c++) part[c] = aw[c];
+        part[JW] = fl;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(128) void k_prep_pok_wide_sigg1(size_t n, int q, int r, const uint8_t* __restrict__ s1b,
+                                                            const uint8_t* __restrict__ s2b,
+                                                            const uint8_t* __restrict__ Jb,
+                                                            const uint8_t* __restrict__ Tb,
+                                                            const uint8_t* __restrict__ resp,
+                                                            const uint8_t* __restrict__ chal,
+                                                            const uint8_t* __restrict__ rev_msgs,
+                                                            const uint32_t* __restrict__ rev_idx,
+                                                            const uint32_t* __restrict__ Xaff, uint32_t Xinf,
+                                                            const uint32_t* __restrict__ table, int wbits,
+                                                            const uint32_t* __restrict__ binf,
+                                                            uint32_t* __restrict__ prep, uint32_t* __restrict__ flags,
+                                                            uint32_t* __restrict__ jtab) {
+    using G2 = pl::Fp2;
+    constexpr int JW = sizeof(Jac<G2>) / 4;  // one lane's halves
+    __shared__ uint32_t part[2][JW + 1];     // wave 1 pair 0's Schnorr part (each half) and flag bits
+    const size_t i = blockIdx.x;
+    if (i >= n) return;  // block-uniform
+    const int l = (int)(threadIdx.x & 63), h = l & 1, p = l >> 1;
+    const bool w1 = threadIdx.x >= 64;  // wave-uniform
+    Soa S{prep, n};
+    auto own = [&](Aff<G2>& o, const Aff<Fp2>& a) {
+        o.x.c = h ? a.x.b : a.x.a;
+        o.y.c = h ? a.y.b : a.y.a;
+    };
+    Aff<Fp2> Jf;
+    const bool Jok = pl::pair_all(g2_decode(Jf, Jb + i * 192));
+    Aff<G2> Ja;
+    own(Ja, Jf);
+    if (!w1) {
+        uint32_t fl = 0;
+        {  // sigma'_1 on lane 0 (P1), -sigma'_2 on lane 1 (P2)
+            Aff<Fp> a;
+            if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
+            if (h) fp_neg(a.y, a.y);
+            fp_to_lazy_form(a.x);  // the Miller loop's affine P in the lazy R' form (kAffRp)
+            fp_to_lazy_form(a.y);
+            if (l < 2) {
+                st_fp(S, h ? S_P2 : S_P1, i, a.x);
+                st_fp(S, (h ? S_P2 : S_P1) + 1, i, a.y);
+            }
+        }
+        fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
+        lz::JL sacc = lz::jl_inf();
+        if (Jok) {  // chal J in fixed 4-bit windows (k_prep_pok_g1pl), every pair the same chain
+            Fr k;
+            fr_from_be48(k, chal + i * 48);
+            constexpr int LW = sizeof(lz::JL) / 4;
+            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * LW + w) * 2 * n + 2 * i + h]; };
+            const lz::AL Jl{lz::reduce(lz::in_r2(Ja.x)), lz::reduce(lz::in_r2(Ja.y))};
+            lz::JL t = lz::jl_from_aff(Jl);
+#pragma unroll 1
+            for (int d = 1; d <= 15; d++) {
+                if (d > 1) t = lz::jl_add_aff(t, Jl);
+                const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
+                for (int w = 0; w < LW; w++) tab(d, w) = tw[w];
+            }
+#pragma unroll 1
+            for (int win = 63; win >= 0; win--) {
+                for (int b = 0; b < 4; b++) sacc = lz::jl_dbl(sacc);
+                const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
+                if (d) {
+                    uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
+                    for (int w = 0; w < LW; w++) tw[w] = tab((int)d, w);
+                    sacc = lz::jl_add(sacc, t);
+                }
+            }
+        }
+        Jac<G2> acc = pl::jl_to_pl(sacc);
+        __syncthreads();
+        Jac<G2> o;
+        uint32_t* ow = reinterpret_cast<uint32_t*>(&o);
+        for (int c = 0; c < JW; c++) ow[c] = part[h][c];
+        fl |= part[0][JW];
+        jac_add(acc, acc, o);
+        if (!pl::pair_all(jac_is_inf(acc))) fl |= 8u;
+        if (l == 0) flags[i] = fl;
+        return;
+    }
+    const uint8_t* rp = resp + i * (size_t)(q - r + 1) * 48;
+    const int nwin = ft_nwin(wbits), nresp = q - r + 1;
+    lz::JL la = lz::jl_inf(), lj = lz::jl_inf();
+    int hh = -1;
+#pragma unroll 1
+    for (int s = 0; s < nresp; s++) {  // response s: g~ (s = 0, table base q) or the s-th hidden Y~
+        int base = q;
+        if (s) {
+            do hh++;
+            while (pok_revealed(hh, r, rev_idx));
+            base = hh;
+        }
+        if (binf[base]) continue;
+        Fr k;
+        fr_from_be48(k, rp + (size_t)s * 48);
+#pragma unroll 1
+        for (int w = rot_start(p, s * nwin, 32); w < nwin; w += 32) pl::ft_add_g2_lz(la, k.v, table, wbits, base, w, w + 1);
+    }
+#pragma unroll 1
+    for (int z = 0; z < r; z++) {  // J' terms: revealed messages, the pair rotation continued
+        const int base = (int)rev_idx[z];
+        if (binf[base]) continue;
+        Fr m;
+        fr_from_be48(m, rev_msgs + ((size_t)i * r + z) * 48);
+#pragma unroll 1
+        for (int w = rot_start(p, (nresp + z) * nwin, 32); w < nwin; w += 32)
+            pl::ft_add_g2_lz(lj, m.v, table, wbits, base, w, w + 1);
+    }
+    Jac<G2> acc = pl::jl_to_pl(la), jp = pl::jl_to_pl(lj);
+    if (p == 31) {  // -T (both lanes of the pair)
+        Aff<Fp2> Tf;
+        if (pl::pair_all(g2_decode(Tf, Tb + i * 192))) {
+            Aff<G2> Ta;
+            own(Ta, Tf);
+            FT<G2>::neg(Ta.y, Ta.y);
+            jac_add_aff(acc, acc, Ta);
+        }
+    }
+    if (p == 30) {  // X~ + J
+        if (!Xinf) {
+            Aff<G2> x;
+            for (int c = 0; c < NL; c++) {
+                x.x.c.v[c] = Xaff[NL * h + c];
+                x.y.c.v[c] = Xaff[2 * NL + NL * h + c];
+            }
+            jac_add_aff(jp, jp, x);
+        }
+        if (Jok) jac_add_aff(jp, jp, Ja);
+    }
+    pl::pair_group_sum<64>(acc);
+    pl::pair_group_sum<64>(jp);
+    Aff<G2> a;
+    const uint32_t fl = jac_to_aff(a, jp) ? 0u : 4u;
+    if (p == 0) {
+        pl::st_f2(S, S_Q1, i, a.x);
+        pl::st_f2(S, S_Q1 + 2, i, a.y);
+        const uint32_t* aw = reinterpret_cast<const uint32_t*>(&acc);
+        for (int c = 0; c < JW; c++) part[h][c] = aw[c];
+        part[h][JW] = fl;
+    }
+    __syncthreads();
+}
+
 // ================================================================ fixed-base scalar multiplication
 // out_i = k_i * B for one base B with a prebuilt 8-bit window table (keygen-style derivations:
 // reference keygen.rs:27-32 g~ * x_i, and issuer-side h * e).  Scalars are 48-byte BE Fr.
@@ -889,6 +1186,24 @@ int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const ui
     } else
         hipLaunchKernelGGL(k_prep_pok_g1pl, dim3(nblocks(2 * n, 256)), b, 0, st, n, q, r, d_s1, d_s2, d_J, d_T, d_resp,
                            d_chal, d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags, d_jtab);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the small-batch form (one block of two waves per proof, k_prep_pok_wide_*): same arguments and outputs
+int cck_prep_pok_wide(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
+                      const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
+                      const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table,
+                      int wbits, const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_jtab,
+                      hipStream_t st) {
+    if (!n) return 0;
+    if (mode == 0)
+        hipLaunchKernelGGL(k_prep_pok_wide_sigg2, dim3((unsigned)n), dim3(128), 0, st, n, q, r, d_s1, d_s2, d_J, d_T,
+                           d_resp, d_chal, d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags,
+                           d_jtab);
+    else
+        hipLaunchKernelGGL(k_prep_pok_wide_sigg1, dim3((unsigned)n), dim3(128), 0, st, n, q, r, d_s1, d_s2, d_J, d_T,
+                           d_resp, d_chal, d_rev_msgs, d_rev_idx, d_Xaff, Xinf, d_table, wbits, d_binf, d_prep, d_flags,
+                           d_jtab);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -46,7 +46,7 @@ int cck_prep_wide(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t*
 size_t cck_prep_var_words(int mode, size_t n, size_t q);
 int cck_prep_var(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_vkX,
                  const uint8_t* d_vkY, const uint8_t* d_msgs, uint32_t* d_scratch, uint32_t* d_prep,
-                 uint32_t* d_flags, hipStream_t st);
+                 uint32_t* d_flags, int wide, hipStream_t st);
 int cck_miller_lz_g2(int twin, size_t n, size_t pstride, const uint32_t* d_prep, const uint32_t* d_flags,
                      const uint32_t* d_const, uint32_t* d_f, size_t fstride, size_t foff, uint32_t* d_qcheck,
                      hipStream_t st);
@@ -92,6 +92,10 @@ int cck_rlc_reduce(size_t n, uint32_t* d_a, uint32_t* d_b, const uint32_t* d_any
 int cck_rlc_gather(int mode, size_t k, const uint32_t* d_parts, const uint32_t* d_pw, const uint8_t* d_finf,
                    uint32_t* d_fw, size_t fs, uint32_t* d_prep, uint32_t* d_flags2, uint32_t* d_flag, hipStream_t st);
 int cck_prep_pok(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
+                 const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
+                 const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
+                 const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_jtab, hipStream_t st);
+int cck_prep_pok_wide(int mode, size_t n, int q, int r, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_J,
                  const uint8_t* d_T, const uint8_t* d_resp, const uint8_t* d_chal, const uint8_t* d_rev_msgs,
                  const uint32_t* d_rev_idx, const uint32_t* d_Xaff, uint32_t Xinf, const uint32_t* d_table, int wbits,
                  const uint32_t* d_binf, uint32_t* d_prep, uint32_t* d_flags, uint32_t* d_jtab, hipStream_t st);
@@ -719,7 +723,7 @@ static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t 
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     if (d_vkX)
         KCK(cck_prep_var(c->mode, n, (int)q, d_s1, d_s2, d_vkX, d_vkY, d_msgs, w.vkb->as<uint32_t>(),
-                         w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), st));
+                         w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), n <= kFexpWideMax, st));
     else  // small batches: one wave per credential, the MSM's window terms over its lanes
         KCK((n <= kWideMax ? cck_prep_wide : cck_prep)(c->mode, n, (int)q, d_s1, d_s2, d_msgs,
                                                        c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(),
@@ -1675,10 +1679,11 @@ static cc_status launch_pok(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, 
                             const uint8_t* d_chal, const uint32_t* d_idx, const uint8_t* d_rev_msgs, uint8_t* d_verdicts,
                             uint8_t* d_gt, hipStream_t st) {
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
-    KCK(cck_prep_pok(c->mode, n, (int)q, (int)r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_idx,
-                     c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(), c->wbits,
-                     c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(), w.flags->as<uint32_t>(),
-                     w.scratch->as<uint32_t>(), st));  // J*chal window table: the fexp scratch, free until fexp
+    // small batches: one block of two waves per proof (the Schnorr terms over a wave's lanes)
+    KCK((n <= kFexpWideMax ? cck_prep_pok_wide : cck_prep_pok)(
+        c->mode, n, (int)q, (int)r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_idx, c->vk_aff.as<uint32_t>(),
+        c->X_inf, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(),
+        w.flags->as<uint32_t>(), w.scratch->as<uint32_t>(), st));  // J*chal window table: the fexp scratch, free until fexp
     if (c->timing) (void)hipEventRecord(c->ev[1], st);
     cc_status ms = launch_miller(c, w, n, st);
     if (ms) return ms;

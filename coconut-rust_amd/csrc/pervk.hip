@@ -135,6 +135,99 @@ __global__ __launch_bounds__(256, 2) void k_prep_sigg1_var(size_t n, int q, cons
     if (!h) flags[i] = fl;
 }
 
+// Small batches (capi.cpp kWideMax): ONE WAVE per credential, one base per lane (pair).  A Straus
+// chain's 260 doublings are the same for one base as for q, so the pair kernels' lane (pair) walking
+// half (all) of the bases spends most of its time in the additions the other lanes of the wave could
+// take: here lane (pair) k < q takes Y~_k alone, lane (pair) q adds X~, and a butterfly sums the
+// partial results (curve.h lane_group_sum / curve_pl.h pair_group_sum).  Same outputs and scratch
+// layout as the pair kernels.
+__global__ __launch_bounds__(64) void k_prep_sigg2_var_wide(size_t n, int q, const uint8_t* __restrict__ s1b,
+                                                            const uint8_t* __restrict__ s2b,
+                                                            const uint8_t* __restrict__ vkX,
+                                                            const uint8_t* __restrict__ vkY,
+                                                            const uint32_t* __restrict__ scal,
+                                                            uint32_t* __restrict__ scratch,
+                                                            uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
+    const size_t i = blockIdx.x;
+    if (i >= n) return;  // wave-uniform
+    const int l = (int)threadIdx.x, h = l & 1;
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp2> a;
+        if (!g2_decode(a, (h ? s2b : s1b) + i * 192)) fl |= h ? 2u : 1u;
+        if (h) f2_neg(a.y, a.y);  // -sigma_2
+        if (l < 2) {
+            st_f2(S, h ? S_Q2 : S_Q1, i, a.x);
+            st_f2(S, (h ? S_Q2 : S_Q1) + 2, i, a.y);
+        }
+    }
+    fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
+    lz::JG a;
+    straus_g1lz_lane(a, 64, l, (size_t)q, vkY + i * (size_t)q * 97, scal + i * (size_t)q * 8,
+                     scratch + i * straus_g1lz_words((size_t)q));
+    if (l == (q & 63)) {  // X~ with scalar 1 (q < 64 here: cc_verify_batch_pervk_device takes q <= 4096,
+        Aff<Fp> X;        // the lane then also holds the bases k = q mod 64 + 64 j)
+        if (g1_decode(X, vkX + i * 97)) a = lz::jg_add_aff(a, ag_of(lz::reduce(lz::in_r(X.x)), lz::reduce(lz::in_r(X.y))));
+    }
+    Jac<Fp> pr = lz::jg_to(a);
+    lane_group_sum<Fp, 64>(pr);  // every lane the same sum
+    if (jac_is_inf(pr)) {
+        fl |= 4u;
+    } else {
+        Fp x, y;
+        lz::jg_to_aff_rp(x, y, lz::jg_from(pr));
+        if (l < 2) st_fp(S, S_P1 + h, i, h ? y : x);
+    }
+    if (l == 0) flags[i] = fl;
+}
+
+__global__ __launch_bounds__(64) void k_prep_sigg1_var_wide(size_t n, int q, const uint8_t* __restrict__ s1b,
+                                                            const uint8_t* __restrict__ s2b,
+                                                            const uint8_t* __restrict__ vkX,
+                                                            const uint8_t* __restrict__ vkY,
+                                                            const uint32_t* __restrict__ scal,
+                                                            uint32_t* __restrict__ scratch,
+                                                            uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
+    const size_t i = blockIdx.x;
+    if (i >= n) return;  // wave-uniform
+    const int l = (int)threadIdx.x, h = l & 1, p = l >> 1;
+    Soa S{prep, n};
+    uint32_t fl = 0;
+    {
+        Aff<Fp> a;
+        if (!g1_decode(a, (h ? s2b : s1b) + i * 97)) fl |= h ? 2u : 1u;
+        if (h) fp_neg(a.y, a.y);  // -sigma_2
+        fp_to_lazy_form(a.x);     // the Miller loop's affine P in the lazy R' form (kAffRp)
+        fp_to_lazy_form(a.y);
+        if (l < 2) {
+            st_fp(S, h ? S_P2 : S_P1, i, a.x);
+            st_fp(S, (h ? S_P2 : S_P1) + 1, i, a.y);
+        }
+    }
+    fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
+    lz::JL la;
+    straus_g2lz_pair(la, 32, p, h, i, (size_t)q, vkY, (size_t)q * 192, 0, 192, scal, 1, scratch);
+    if (p == (q & 31)) {  // X~ with scalar 1 (both lanes of the pair decode it)
+        Aff<Fp2> X;
+        if (pl::pair_all(g2_decode(X, vkX + i * 192))) {
+            pl::Fp2 hx, hy;
+            hx.c = h ? X.x.b : X.x.a;
+            hy.c = h ? X.y.b : X.y.a;
+            la = lz::jl_add_aff(la, lz::AL{lz::reduce(lz::in_r2(hx)), lz::reduce(lz::in_r2(hy))});
+        }
+    }
+    Jac<pl::Fp2> acc = pl::jl_to_pl(la);
+    pl::pair_group_sum<64>(acc);  // every pair the same sum
+    Aff<pl::Fp2> a;
+    if (!jac_to_aff(a, acc)) fl |= 4u;
+    if (p == 0) {
+        pl::st_f2(S, S_Q1, i, a.x);
+        pl::st_f2(S, S_Q1 + 2, i, a.y);
+    }
+    if (l == 0) flags[i] = fl;
+}
+
 static inline unsigned nblocks(size_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
 extern "C" {
@@ -145,15 +238,22 @@ size_t cck_prep_var_words(int mode, size_t n, size_t q) {
 }
 
 // Per-credential-verkey prep: vkX n x OtherGroup, vkY n x q x OtherGroup, msgs n x q x 48 B;
-// scratch: cck_prep_var_words words.  Writes the Miller-loop operands and flags like cck_prep.
+// scratch: cck_prep_var_words words.  Writes the Miller-loop operands and flags like cck_prep.  wide:
+// one wave per credential (the small-batch form above).
 int cck_prep_var(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* d_s2, const uint8_t* d_vkX,
                  const uint8_t* d_vkY, const uint8_t* d_msgs, uint32_t* d_scratch, uint32_t* d_prep,
-                 uint32_t* d_flags, hipStream_t st) {
+                 uint32_t* d_flags, int wide, hipStream_t st) {
     if (!n) return 0;
     uint32_t* scal = d_scratch;
     uint32_t* straus = d_scratch + straus_round32(n * (size_t)q * 8);  // 128-byte-aligned task regions
     if (q) hipLaunchKernelGGL(k_scalars_w8, dim3(nblocks(n * (size_t)q, 256)), dim3(256), 0, st, n * (size_t)q, d_msgs, scal);
-    if (mode == 0)
+    if (wide && mode == 0)
+        hipLaunchKernelGGL(k_prep_sigg2_var_wide, dim3((unsigned)n), dim3(64), 0, st, n, q, d_s1, d_s2, d_vkX, d_vkY,
+                           scal, straus, d_prep, d_flags);
+    else if (wide)
+        hipLaunchKernelGGL(k_prep_sigg1_var_wide, dim3((unsigned)n), dim3(64), 0, st, n, q, d_s1, d_s2, d_vkX, d_vkY,
+                           scal, straus, d_prep, d_flags);
+    else if (mode == 0)
         hipLaunchKernelGGL(k_prep_sigg2_var, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_vkX,
                            d_vkY, scal, straus, d_prep, d_flags);
     else

@@ -335,6 +335,68 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
         assert g1 == gt_big[576 * i:576 * (i + 1)], (i, b["kind"][i])
 
 
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_small_batch_pok_paths_agree(ctxs, mode):
+    """PoK batches of <= 1,024 proofs take the one-block-per-proof prep (aggregate.hip
+    k_prep_pok_wide_*: chal J on one wave, the Schnorr and J' table terms spread over the other) and the
+    one-wave fexp; larger ones the lane-pair prep and the quad fexp: the same proofs (1/4 with a bad
+    response) give the same verdicts and GT bytes through both, and one at a time."""
+    import bench_modes
+    from coconut import pok_verify_batch
+    m = MODES[mode]
+    ctx = ctxs[mode]
+    n, q = FEXP_WIDE_MAX + 6, 32
+    b = bench_modes.make_pok_batch(ctx, m, n, q=q, seed=777 + m, bad_every=4)
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    sb, ob = (192, 97) if m == 0 else (97, 192)
+    nr, r = b["nresp"], len(b["revealed"])
+
+    def run(lo, hi):
+        return pok_verify_batch(ctx, hi - lo, q, b["revealed"], nr, b["s1"][lo * sb:hi * sb], b["s2"][lo * sb:hi * sb],
+                                b["J"][lo * ob:hi * ob], b["T"][lo * ob:hi * ob],
+                                b["resp"][lo * nr * 48:hi * nr * 48], b["chal"][lo * 48:hi * 48],
+                                b["rev"][lo * r * 48:hi * r * 48], want_gt=True)
+    v_big, gt_big = run(0, n)
+    assert np.array_equal(v_big, b["expect"])
+    v_w, gt_w = run(0, FEXP_WIDE_MAX)
+    assert np.array_equal(v_w, b["expect"][:FEXP_WIDE_MAX])
+    assert gt_w == gt_big[:576 * FEXP_WIDE_MAX]
+    for i in (0, 3, 4, 7, n - 1):
+        v1, g1 = run(i, i + 1)
+        assert v1[0] == b["expect"][i], i
+        assert g1 == gt_big[576 * i:576 * (i + 1)], i
+
+
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_small_batch_pervk_paths_agree(ctxs, mode):
+    """Per-credential-verkey batches of <= 1,024 take the one-wave-per-credential prep (pervk.hip
+    k_prep_*_var_wide: one base per lane / lane pair), larger ones the lane-pair Straus: the same
+    credentials (every corruption kind of make_pervk_batch) agree in verdicts and GT bytes."""
+    import bench_modes
+    from coconut import verify_batch
+    m = MODES[mode]
+    ctx = ctxs[mode]
+    n, q = FEXP_WIDE_MAX + 6, 6
+    b = bench_modes.make_pervk_batch(ctx, m, n, q, seed=888 + m, bad_every=4)
+    ctx.set_params(b["g_tilde"])
+    sb, ob = (192, 97) if m == 0 else (97, 192)
+
+    def run(lo, hi):
+        return verify_batch(ctx, hi - lo, q, b["s1"][lo * sb:hi * sb], b["s2"][lo * sb:hi * sb],
+                            b["msgs"][lo * q * 48:hi * q * 48],
+                            vk=(b["X"][lo * ob:hi * ob], b["Y"][lo * q * ob:hi * q * ob]), want_gt=True)
+    v_big, gt_big = run(0, n)
+    assert np.array_equal(v_big, b["expect"])
+    v_w, gt_w = run(0, FEXP_WIDE_MAX)
+    assert np.array_equal(v_w, b["expect"][:FEXP_WIDE_MAX])
+    assert gt_w == gt_big[:576 * FEXP_WIDE_MAX]
+    for i in (0, 3, 7, 11, n - 1):
+        v1, g1 = run(i, i + 1)
+        assert v1[0] == b["expect"][i], i
+        assert g1 == gt_big[576 * i:576 * (i + 1)], i
+
+
 def test_full_size_batch_config2(ctxs):
     """BASELINE config 2 size (65,536 credentials, q = 6, shared vk): every verdict equals the one
     known by construction (size-independent property; 1/16 corrupted)."""
