@@ -397,6 +397,39 @@ def test_small_batch_pervk_paths_agree(ctxs, mode):
         assert g1 == gt_big[576 * i:576 * (i + 1)], i
 
 
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+@pytest.mark.parametrize("which", ["X", "Y2"])
+def test_identity_verkey_component_both_paths(ctxs, mode, which):
+    """A verkey component that decodes to the identity (an off-curve encoding, as AMCL reads it) is
+    skipped by the MSM the same way on the one-wave-per-credential prep (small batches) and the
+    lane-pair prep: verdicts and GT bytes of both against the C oracle."""
+    from coconut import verify_batch
+    m = MODES[mode]
+    q, n, k = 6, FEXP_WIDE_MAX + 6, 40
+    b = _gen_batch(m, n, q, seed=55 + m, bad_every=5)
+    ob, sb = (97, 192) if m == 0 else (192, 97)
+    ident = (b"\x04" + bytes(ob - 1)) if m == 0 else bytes(ob)
+    X, Y = b["X"], b["Y"]
+    if which == "X":
+        X = ident
+    else:
+        Y = Y[:2 * ob] + ident + Y[3 * ob:]
+    ctx = ctxs[mode]
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(X, [Y[j * ob:(j + 1) * ob] for j in range(q)])
+    v_big, gt_big = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], want_gt=True)
+    v_w, gt_w = verify_batch(ctx, k, q, b["s1"][:k * sb], b["s2"][:k * sb], b["msgs"][:k * q * 48], want_gt=True)
+    oc = oracle_lib()
+    ver = ctypes.create_string_buffer(k)
+    ref = ctypes.create_string_buffer(576 * k)
+    oc.oc_verify_batch(m, ctypes.c_size_t(k), ctypes.c_size_t(q), b["s1"][:k * sb], b["s2"][:k * sb],
+                       b["msgs"][:k * q * 48], X, Y, 0, b["g_tilde"], ver, ref, host_threads())
+    assert np.array_equal(v_w, np.frombuffer(ver.raw, np.uint8))
+    assert gt_w == ref.raw
+    assert np.array_equal(v_big[:k], v_w)
+    assert gt_big[:576 * k] == gt_w
+
+
 def test_full_size_batch_config2(ctxs):
     """BASELINE config 2 size (65,536 credentials, q = 6, shared vk): every verdict equals the one
     known by construction (size-independent property; 1/16 corrupted)."""
