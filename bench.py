@@ -496,7 +496,9 @@ def kernel_table(phase_ms, n, counts, in_bytes_per_cred, peak, prep_kernel="k_pr
                "frac": round(ach / peak, 4)}
         if k == "prep":
             row["input_GB_s"] = round(n * in_bytes_per_cred / (ms * 1e-3) / 1e9, 2)
-        row.update(pmc({"prep": prep_kernel, "miller": "k_miller", "fexp": "k_fexp"}[k], mode))
+        # the batch kernels by exact name stem: the small-batch paths' k_miller_wide / k_fexp1 (the latency
+        # legs) appear in the same profiles
+        row.update(pmc({"prep": prep_kernel + "(", "miller": "lz::k_miller<", "fexp": "lz::k_fexp_q("}[k], mode))
         out[k] = row
     return out
 
