@@ -289,8 +289,8 @@ def bench_aggregate(args):
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": round(ach / 1e12, 3),
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
                          "frac": round(ach / peak, 4),
-                         "traffic": (rk or {}).get("kernels", {}).get("k_msm_straus_g2lz_g", {}).get(
-                             "hbm_bytes_per_launch"),
+                         "traffic": (rk or {}).get("kernels", {}).get(
+                             "k_msm_straus<cc::Fp, 16>" if sigm else "k_msm_straus_g2lz_g", {}).get("hbm_bytes_per_launch"),
                          "traffic_unit": "HBM-side bytes per launch of the Straus kernel (PMC, 2 x FETCH_SIZE + "
                                          "WRITE_SIZE)"},
             "kernels": {"lagrange_ms": round(phase[0], 3), "msm_ms": round(msm_ms, 3),
@@ -556,7 +556,8 @@ def bench_pervk(args):
             **lib_info(),
             "roofline": {"bound": "valu-int", "kernel": dom, "achieved": kt[dom]["achieved_Tmad_s"],
                          "peak": round(peak / 1e12, 3), "unit": "Tmad/s (v_mad_u64_u32, 32x32->64)",
-                         "frac": kt[dom]["frac"], "traffic": None,
+                         "frac": kt[dom]["frac"], "traffic": kt[dom].get("traffic_bytes"),
+                         "traffic_unit": "HBM-side bytes per launch (PMC, 2 x FETCH_SIZE + WRITE_SIZE)",
                          "algorithmic_mads_per_credential": round(counts[dom] * MADS_PER_M),
                          "opcount_fixture": f"tests/fixtures/opcount.json {key}",
                          "whole_step_frac": round(total / (el / args.steps) / peak, 4)},
