@@ -680,7 +680,7 @@ static cc_status ensure_work(cc_ctx* c, size_t n) {
         drain_slots(c);  // a concurrent batch may still read the buffers about to be reallocated
     if (wide_ensure(c->wide_prep, c->wide_flags, c->wide_f, n)) return CC_ERR_HIP;
     // scratch: the PoK prep's per-proof table of d J (15 Jacobian points, <= 15 x 84 words: SigG1's lazy
-    // G2 points), and the one-element fexp's (fexp_pl.hip k_fexp1: 72 slots of 12 words); the batched
+    // G2 points), and the one-wave fexp's (fexp_pl.hip k_fexp1: 72 slots of 12 words an element); the batched
     // fexp (fexp_q.hip) keeps its chain in registers
     if (c->prep.ensure(words * 4 * PREP_SLOTS) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
         c->scratch.ensure((n * 15 * 84 + 72 * 12) * 4) || c->verdicts.ensure(n))

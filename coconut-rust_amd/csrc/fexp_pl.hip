@@ -171,13 +171,14 @@ DEV void cyc4_expand(Fp12& r, const Cyc4& x, const Fp2& n0, const Fp2& n1, const
     r.c.b = x.c1;
 }
 
-// ---------------------------------------------------------------- wide forms (k_fexp1: one element)
-// A single final exponentiation (the RLC batch mode's one per batch) runs on ONE wave: the 32 lane
-// pairs hold the same element, and the independent Fp2 products of a step are spread over them —
-// the 6 squarings of cyc4_sqr, the 18 products of f12_mul, the 6 of f12_cyc_sqr — as ONE call
-// (same instructions, different data), the results gathered with ds_bpermute shuffles and the
-// remaining additions done redundantly by every pair.  A step's latency then holds one product
-// instead of 6 or 18.
+// ---------------------------------------------------------------- wide forms (k_fexp1: one element a wave)
+// A latency-bound final exponentiation (the RLC batch mode's one per batch, and every credential of
+// a small batch) runs on ONE wave: the 32 lane pairs hold the same element, and the independent Fp2
+// products of a step are spread over them — the 6 squarings of cyc4_sqr, the 18 products of
+// f12_mul, the 6 of f12_cyc_sqr — as ONE call (same instructions, different data), the results
+// gathered with ds_bpermute shuffles.  A step's latency then holds one product instead of 6 or 18.
+// The combinations are spread too (round 5): a lone wave's time is its instruction count, so no
+// pair redoes what another pair computes (f12w_assemble, cyc4_sqr_dist, f12_cyc_sqr_wide).
 DEV int pair_idx() { return (int)(threadIdx.x >> 1); }
 DEV Fp2 bcast_f2(const Fp2& v, int src_pair) {
     const int lane = 2 * src_pair + (int)half_id();
@@ -598,7 +599,7 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i, 
     ld_f2(c.b1, src, 6, i);
     ld_f2(c.c0, src, 8, i);
     ld_f2(c.c1, src, 10, i);
-    if (W) {  // one element (k_fexp1): the squarings' state and the decompression spread over the pairs
+    if (W) {  // one element a wave (k_fexp1): the squarings' state and the decompression spread over the pairs
         Fp2 V;
         ld_f2(V, src, 4 + 2 * (pair_idx() & 3), i);
         for (int k = 1; k <= 57; k++) {
@@ -694,7 +695,7 @@ static __device__ __noinline__ void fx_mul(Soa a, int opa, Soa b, int opb, Soa d
     st_f12(dst, i, x);
 }
 
-// the chain (k_fexp: element i of n; k_fexp1: the one element, wide steps)
+// the chain (W = false: element i of n, per lane pair; k_fexp1: element i on a whole wave, wide steps)
 template <bool W>
 DEV void fexp_chain(size_t n, size_t i, uint32_t* fbuf, uint32_t* scratch) {
     const Soa F{fbuf, n};
