@@ -12,6 +12,7 @@
 #include <cstring>
 #include "codec.h"
 #include "lazy.h"  // LZ_ONE_LIMBS (k_wide_pairs)
+#include "tower_q.h"  // lz::fp_inv_int_quad (the wide forms' inversions)
 #include "tower_pl.h"
 
 namespace cc {
@@ -38,6 +39,12 @@ DEV void fx_apply(Fp12& x, int op) {
         Fp12 t = x;
         f12_frob2(x, t);
     }
+}
+DEV void f12_frobs_wide(Fp12& x, int op);  // the Frobenius maps spread over the lane pairs (below)
+template <bool W>
+DEV void fx_apply_w(Fp12& x, int op) {
+    if (W && (op == OP_FROB || op == OP_FROB2)) f12_frobs_wide(x, op);
+    else fx_apply(x, op);
 }
 
 // dst <- src^-1 (templated like every step: the one-wave kernel's looser register bound must not
@@ -180,6 +187,22 @@ DEV void cyc4_expand(Fp12& r, const Cyc4& x, const Fp2& n0, const Fp2& n1, const
 // The combinations are spread too (round 5): a lone wave's time is its instruction count, so no
 // pair redoes what another pair computes (f12w_assemble, cyc4_sqr_dist, f12_cyc_sqr_wide).
 DEV int pair_idx() { return (int)(threadIdx.x >> 1); }
+// tower_pl.h f2_inv for a value every pair of the wave holds: the norm is then the same on all four
+// lanes of each quad, so its divstep inversion runs in the quad form (tower_q.h fp_inv_int_quad: the
+// iteration's f, g, d, e one per lane, one update chain a lane instead of four)
+DEV void f2_inv_q(Fp2& r, const Fp2& x) {
+    const Fp xs = swp(x.c);
+    Fp n = fp_mul2_v(x.c, x.c, xs, xs), ni;
+    lz::fp_inv_int_quad(ni, n);  // plain integer inverse of the Montgomery residue
+    constexpr uint32_t R3[NL] = {CC_R3_LIMBS};
+    Fp r3;
+#pragma unroll
+    for (int j = 0; j < NL; j++) r3.v[j] = R3[j];
+    fp_mul(n, ni, r3);  // (n R)^-1 R^3 R^-1 = n^-1 R (field.h fp_inv)
+    Fp2 t;
+    fp_mul(t.c, x.c, n);
+    f2_conj(r, t);
+}
 DEV Fp2 bcast_f2(const Fp2& v, int src_pair) {
     const int lane = 2 * src_pair + (int)half_id();
     Fp2 r;
@@ -403,6 +426,32 @@ DEV void f12_cyc_sqr_wide(Fp12& r, const Fp12& x) {
     r.c.b = bcast_f2(v, 5);
 }
 
+// f12_frob / f12_frob2 (pairing.inc) spread: pair q < 6 maps coefficient q (a.a, a.b, b.a, b.b, c.a,
+// c.b; the coefficient of W^k, k = 0 3 1 4 2 5): conj(c) gamma1_k, or c gamma2_k (gamma_0 = 1), then
+// the six are broadcast
+DEV void f12_frobs_wide(Fp12& x, int op) {
+    const int q = pair_idx() % 6, k = (0x524130 >> (4 * q)) & 15;
+    const Fp2 cs[6] = {x.a.a, x.a.b, x.b.a, x.b.b, x.c.a, x.c.b};
+    Fp2 c = f2_pick(q, cs, 6), r;
+    if (op == OP_FROB) {  // wave-uniform
+        Fp2 g, t;
+        load_f2c(g, kGamma1[k]);
+        f2_conj(t, c);
+        f2_mul(r, t, g);
+    } else {
+        Fp g;
+#pragma unroll
+        for (int j = 0; j < NL; j++) g.v[j] = kGamma2[k][j];
+        f2_mul_fp(r, c, g);
+    }
+    x.a.a = bcast_f2(r, 0);
+    x.a.b = bcast_f2(r, 1);
+    x.b.a = bcast_f2(r, 2);
+    x.b.b = bcast_f2(r, 3);
+    x.c.a = bcast_f2(r, 4);
+    x.c.b = bcast_f2(r, 5);
+}
+
 // k Fp4 products x_m y_m (m < k <= 10) as 3k Fp2 products on pairs 0..3k-1 (f4_mul's Karatsuba: pair
 // 3m + p forms x.a y.a, x.b y.b, (x.a + x.b)(y.a + y.b) for p = 0, 1, 2); every pair gets all k results
 DEV void f4w_mul(Fp4* r, const Fp4* x, const Fp4* y, int k) {
@@ -454,7 +503,7 @@ DEV void f12_inv_wide(Fp12& r, const Fp12& x) {
         f2_mul_xi(u, bcast_f2(pr, 1));
         f2_sub(n, bcast_f2(pr, 0), u);  // a^2 - xi b^2
     }
-    f2_inv(n, n);
+    f2_inv_q(n, n);
     {
         const int j = pair_idx() & 1;
         Fp2 in = F.a;
@@ -565,7 +614,7 @@ DEV bool decompress3_wide(Fp12& a16, Fp12& a48, Fp12& a57, const Soa& K, const S
     }
     f2_mul(p2, e[0], d[2]);
     if (f2_is_zero(p2)) return false;  // wave-uniform: every pair holds the same values
-    f2_inv(inv, p2);
+    f2_inv_q(inv, p2);
     Fp2 iv[3];
     {  // pairs 0..2: 1/d16 = inv d48 d57, 1/d48 = inv d16 d57, 1/d57 = inv d16 d48
         const int jj = j % 3;
@@ -688,9 +737,9 @@ template <bool W>
 static __device__ __noinline__ void fx_mul(Soa a, int opa, Soa b, int opb, Soa dst, size_t i) {
     Fp12 x, y;
     ld_f12(x, a, i);
-    fx_apply(x, opa);
+    fx_apply_w<W>(x, opa);
     ld_f12(y, b, i);
-    fx_apply(y, opb);
+    fx_apply_w<W>(y, opb);
     m12<W>(x, x, y);
     st_f12(dst, i, x);
 }
