@@ -284,6 +284,44 @@ DEV void st_cyc4_dist(const Soa& K, int base, size_t i, const Fp2& V) {
     st_f2(K, base + 4, i, c.c0);
     st_f2(K, base + 6, i, c.c1);
 }
+// cyc4_sqr_dist on the lazy field (lazy.h: 14 signed 28-bit limbs, R' form, bounds in the types): the
+// same values, with the squaring's Montgomery product and the combination's additions in the lazy
+// form (carry-free additions, one reduction a step) instead of the storage form's canonical ones.
+using LzF2 = lz::F2<lz::AN, 9>;
+DEV LzF2 bcast_lz(const LzF2& v, int src_pair) {
+    const int lane = 2 * src_pair + (int)half_id();
+    LzF2 r;
+#pragma unroll
+    for (int k = 0; k < lz::LN; k++) r.c.v[k] = __shfl(v.c.v[k], lane);
+    return r;
+}
+template <int A, int B>
+DEV lz::F2<A, B> sel2(bool c, const lz::F2<A, B>& x, const lz::F2<A, B>& y) { return {lz::sel(c, x.c, y.c)}; }
+DEV void cyc4_sqr_dist_lz(LzF2& V) {
+    using namespace lz;
+    const int j = pair_idx(), t = j % 6, q = j & 3;
+    const LzF2 a = bcast_lz(V, (0x232010 >> (4 * t)) & 15), b = bcast_lz(V, (0x300100 >> (4 * t)) & 15);
+    const auto s = add(a, b);
+    const auto in = sel2(t == 2 || t == 5, s, fit<decltype(s)::AV, decltype(s)::BV>(a));
+    const LzF2 sq = reduce(sqrr_in(in));
+    const LzF2 G1 = bcast_lz(sq, (0x2035 >> (4 * q)) & 15), G2 = bcast_lz(sq, (0x0143 >> (4 * q)) & 15),
+               G3 = bcast_lz(sq, (0x1004 >> (4 * q)) & 15);
+    const bool xf = q == 0 || q == 3;  // X family: G1 - G2 - G3 (times xi for b0'); else T: G1 + xi G2
+    const auto x = sub(sub(G1, G2), G3);
+    const auto xx = xi(x);
+    const auto w = add(G1, xi(G2));
+    using U = F2<decltype(xx)::AV, decltype(xx)::BV>;
+    const U u0 = sel2(q == 0, xx, fit<U::AV, U::BV>(x));
+    const auto u = squeeze(sel2(xf, u0, fit<U::AV, U::BV>(w)));
+    const auto y = sel2(xf, V, neg(V));  // 3u + 2V = u + 2 (u + V) (X family), 3u - 2V = u + 2 (u - V) (T)
+    V = reduce(add(u, dbl(add(u, y))));
+}
+// the full compressed state (b0, b1, c0, c1) in the storage form at K slots base.. (each pair converts
+// its own component, then four broadcasts)
+DEV void st_cyc4_dist_lz(const Soa& K, int base, size_t i, const LzF2& V) {
+    const Fp2 own = lz::out_r2(V);
+    st_cyc4_dist(K, base, i, own);
+}
 
 // f4_mul's three products of operand set m, spread: pair 3m + p computes product p
 DEV void f4_from_products(Fp4& r, const Fp2& p0, const Fp2& p1, const Fp2& p2) {
@@ -649,14 +687,18 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i, 
     ld_f2(c.c0, src, 8, i);
     ld_f2(c.c1, src, 10, i);
     if (W) {  // one element a wave (k_fexp1): the squarings' state and the decompression spread over the pairs
-        Fp2 V;
-        ld_f2(V, src, 4 + 2 * (pair_idx() & 3), i);
-        for (int k = 1; k <= 57; k++) {
-            cyc4_sqr_dist(V);
-            if (k == 16) st_cyc4_dist(K, 0, i, V);
-            if (k == 48) st_cyc4_dist(K, 8, i, V);
+        LzF2 V;
+        {
+            Fp2 v;
+            ld_f2(v, src, 4 + 2 * (pair_idx() & 3), i);
+            V = lz::reduce(lz::in_r2(v));
         }
-        st_cyc4_dist(K, 16, i, V);
+        for (int k = 1; k <= 57; k++) {
+            cyc4_sqr_dist_lz(V);
+            if (k == 16) st_cyc4_dist_lz(K, 0, i, V);
+            if (k == 48) st_cyc4_dist_lz(K, 8, i, V);
+        }
+        st_cyc4_dist_lz(K, 16, i, V);
         Fp12 acc, t, y;
         if (!decompress3_wide(acc, t, y, K, X, i)) {
             fx_pow_x_gs<W>(src, dst, i);
