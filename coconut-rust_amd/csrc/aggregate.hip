@@ -17,6 +17,7 @@
 #include "codec.h"
 #include "curve_lz.h"
 #include "curve_pl.h"
+#include "curve_wide_lz.h"
 #include "fixed.h"
 #include "fr.h"
 #include "pairing.h"
@@ -802,41 +803,42 @@ __global__ __launch_bounds__(128) void k_prep_pok_wide_sigg2(size_t n, int q, in
     const bool Jok = decode_pt<FO>(Ja, Jb + i * OB);
     if (!w1) {
         uint32_t fl = 0;
-        {
+        {  // sigma'_1 on lanes 0-31, -sigma'_2 on lanes 32-63
+            const bool second = l >= 32;
             Aff<FS_> a;
             const Fp* pa = reinterpret_cast<const Fp*>(&a);
-            if (!decode_pt<FS_>(a, s1b + i * SB)) fl |= 1u;
-            if (l == 0)
-                for (int c = 0; c < 4; c++) st_fp(S, S_Q1 + c, i, pa[c]);
-            if (!decode_pt<FS_>(a, s2b + i * SB)) fl |= 2u;
-            FT<FS_>::neg(a.y, a.y);
-            if (l == 0)
-                for (int c = 0; c < 4; c++) st_fp(S, S_Q2 + c, i, pa[c]);
+            if (!decode_pt<FS_>(a, (second ? s2b : s1b) + i * SB)) fl |= second ? 2u : 1u;
+            if (second) FT<FS_>::neg(a.y, a.y);
+            if ((l & 31) == 0)
+                for (int c = 0; c < 4; c++) st_fp(S, (second ? S_Q2 : S_Q1) + c, i, pa[c]);
+            fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 32);
         }
         Jac<FO> acc;
         jac_set_inf(acc);
-        if (Jok) {  // chal J in fixed 4-bit windows (k_prep_pok_split), every lane the same chain
+        if (Jok) {  // chal J in fixed 4-bit windows (k_prep_pok_split): one chain, its products spread over lanes
             Fr k;
             fr_from_be48(k, chal + i * 48);
             constexpr int LW = sizeof(lz::JG) / 4;
-            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * LW + w) * n + i]; };
+            __shared__ uint32_t tabl[15][LW];  // d J, d = 1..15 (every lane holds the same point)
             const lz::AG Jl{lz::fit<lz::AN, lz::BC>(lz::reduce(lz::in_r(Ja.x))), lz::fit<lz::AN, lz::BC>(lz::reduce(lz::in_r(Ja.y)))};
-            lz::JG t = lz::jg_add_aff(lz::jg_inf(), Jl);
+            lz::JG t = lz::wide::jg_add_aff(lz::jg_inf(), Jl);
 #pragma unroll 1
             for (int d = 1; d <= 15; d++) {
-                if (d > 1) t = lz::jg_add_aff(t, Jl);
+                if (d > 1) t = lz::wide::jg_add_aff(t, Jl);
                 const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
-                for (int w = 0; w < LW; w++) tab(d, w) = tw[w];
+                if (l == 0)
+                    for (int w = 0; w < LW; w++) tabl[d - 1][w] = tw[w];
             }
+            __builtin_amdgcn_wave_barrier();
             lz::JG sacc = lz::jg_inf();
 #pragma unroll 1
             for (int win = 63; win >= 0; win--) {
-                for (int b = 0; b < 4; b++) sacc = lz::jg_dbl(sacc);
+                for (int b = 0; b < 4; b++) sacc = lz::wide::jg_dbl(sacc);
                 const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
                 if (d) {
                     uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
-                    for (int w = 0; w < LW; w++) tw[w] = tab((int)d, w);
-                    sacc = lz::jg_add(sacc, t);
+                    for (int w = 0; w < LW; w++) tw[w] = tabl[d - 1][w];
+                    sacc = lz::wide::jg_add(sacc, t);
                 }
             }
             acc = lz::jg_to(sacc);
@@ -959,27 +961,29 @@ __global__ __launch_bounds__(128) void k_prep_pok_wide_sigg1(size_t n, int q, in
         }
         fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
         lz::JL sacc = lz::jl_inf();
-        if (Jok) {  // chal J in fixed 4-bit windows (k_prep_pok_g1pl), every pair the same chain
+        if (Jok) {  // chal J in fixed 4-bit windows (k_prep_pok_g1pl): one chain, its products spread over pairs
             Fr k;
             fr_from_be48(k, chal + i * 48);
             constexpr int LW = sizeof(lz::JL) / 4;
-            auto tab = [&](int d, int w) -> uint32_t& { return jtab[((size_t)(d - 1) * LW + w) * 2 * n + 2 * i + h]; };
+            __shared__ uint32_t tabl[15][2][LW];  // d J, d = 1..15, by half (every pair holds the same point)
             const lz::AL Jl{lz::reduce(lz::in_r2(Ja.x)), lz::reduce(lz::in_r2(Ja.y))};
             lz::JL t = lz::jl_from_aff(Jl);
 #pragma unroll 1
             for (int d = 1; d <= 15; d++) {
-                if (d > 1) t = lz::jl_add_aff(t, Jl);
+                if (d > 1) t = lz::wide::jl_add_aff(t, Jl);
                 const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
-                for (int w = 0; w < LW; w++) tab(d, w) = tw[w];
+                if (l < 2)
+                    for (int w = 0; w < LW; w++) tabl[d - 1][h][w] = tw[w];
             }
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
             for (int win = 63; win >= 0; win--) {
-                for (int b = 0; b < 4; b++) sacc = lz::jl_dbl(sacc);
+                for (int b = 0; b < 4; b++) sacc = lz::wide::jl_dbl(sacc);
                 const uint32_t d = (k.v[win >> 3] >> ((win & 7) * 4)) & 15u;
                 if (d) {
                     uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
-                    for (int w = 0; w < LW; w++) tw[w] = tab((int)d, w);
-                    sacc = lz::jl_add(sacc, t);
+                    for (int w = 0; w < LW; w++) tw[w] = tabl[d - 1][h][w];
+                    sacc = lz::wide::jl_add(sacc, t);
                 }
             }
         }

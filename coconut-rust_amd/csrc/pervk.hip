@@ -20,6 +20,7 @@
 #include "codec.h"
 #include "curve_lz.h"
 #include "curve_pl.h"
+#include "curve_wide_lz.h"
 #include "fixed.h"
 #include "fr.h"
 #include "pairing.h"
@@ -135,12 +136,151 @@ __global__ __launch_bounds__(256, 2) void k_prep_sigg1_var(size_t n, int q, cons
     if (!h) flags[i] = fl;
 }
 
-// Small batches (capi.cpp kWideMax): ONE WAVE per credential, one base per lane (pair).  A Straus
-// chain's 260 doublings are the same for one base as for q, so the pair kernels' lane (pair) walking
-// half (all) of the bases spends most of its time in the additions the other lanes of the wave could
-// take: here lane (pair) k < q takes Y~_k alone, lane (pair) q adds X~, and a butterfly sums the
-// partial results (curve.h lane_group_sum / curve_pl.h pair_group_sum).  Same outputs and scratch
-// layout as the pair kernels.
+// Small batches (capi.cpp kFexpWideMax): ONE WAVE per credential.  A Straus chain's 260 doublings are
+// the same for one base as for q, so the wave's lanes are split into GROUPS of 4 lanes (G1) or 4 lane
+// pairs (G2), group g takes the bases k = g, g + NG, ..., and each group runs its chain with the
+// products of every doubling and addition spread over its members (curve_wide_lz.h): 3 product times a
+// doubling, 5 an addition.  The multiples 1P..8P stay Jacobian (a spread full addition costs what a
+// spread mixed one does), so no batch inversion; the groups' sums meet in a butterfly of spread
+// additions.  Same outputs as the pair kernels; the scratch holds the entries (x, y, flag; Z apart)
+// and the digits at the pair kernels' offsets.
+namespace {
+using namespace cc::lz;
+constexpr int WG = wide::G;
+
+DEV JG shfl_xor_jg(const JG& p, int m) {
+    JG r;
+#pragma unroll
+    for (int c = 0; c < LN; c++) {
+        r.x.v[c] = __shfl_xor(p.x.v[c], m);
+        r.y.v[c] = __shfl_xor(p.y.v[c], m);
+        r.z.v[c] = __shfl_xor(p.z.v[c], m);
+    }
+    return r;
+}
+DEV JL shfl_xor_jl(const JL& p, int m) {
+    JL r;
+#pragma unroll
+    for (int c = 0; c < LN; c++) {
+        r.x.c.v[c] = __shfl_xor(p.x.c.v[c], m);
+        r.y.c.v[c] = __shfl_xor(p.y.c.v[c], m);
+        r.z.c.v[c] = __shfl_xor(p.z.c.v[c], m);
+    }
+    return r;
+}
+template <class P>
+DEV P sel_pt(bool c, const P& a, const P& b) {
+    P r;
+    const int32_t* x = reinterpret_cast<const int32_t*>(&a);
+    const int32_t* y = reinterpret_cast<const int32_t*>(&b);
+    int32_t* o = reinterpret_cast<int32_t*>(&r);
+#pragma unroll
+    for (int w = 0; w < (int)(sizeof(P) / 4); w++) o[w] = c ? x[w] : y[w];
+    return r;
+}
+
+// group grp of NG: sum of scal_k P_k over its bases (pts: t G1 encodings of 97 bytes)
+DEV void straus_g1lz_wide(JG& acc, int NG, int grp, size_t t, const uint8_t* __restrict__ pts,
+                          const uint32_t* __restrict__ scal, uint32_t* __restrict__ ent) {
+    uint32_t* zs = ent + t * 8 * SEW;
+    int8_t* dig = reinterpret_cast<int8_t*>(zs + 2 * t * 8 * LN);
+    acc = jg_inf();
+#pragma unroll 1
+    for (size_t k = grp; k < t; k += NG) {
+        cc::Aff<cc::Fp> P1;
+        const bool ok = g1_decode(P1, pts + k * 97);
+        recode_w4(dig + k * 65, scal + k * 8);  // every member writes the same digits
+        const FR px = reduce(in_r(P1.x)), py = reduce(in_r(P1.y));
+        const AG P = ag_of(px, py);
+        JG J = ok ? JG{px, py, r1_one()} : jg_inf();
+#pragma unroll 1
+        for (int d = 0; d < 8; d++) {
+            if (d == 1) J = wide::jg_dbl(J);
+            else if (d > 1 && ok) J = wide::jg_add_aff(J, P);
+            const size_t e = k * 8 + d;
+            uint32_t* w = ent + e * SEW;
+            st_r1(w, J.x);
+            st_r1(w + SEY, J.y);
+            w[SEF] = jg_is_inf(J) ? 1u : 0u;
+            st_r1(zs + e * LN, J.z);
+        }
+    }
+#pragma unroll 1
+    for (int win = 64; win >= 0; win--) {
+        if (win != 64 && !jg_is_inf(acc))
+#pragma unroll 1
+            for (int z = 0; z < 4; z++) acc = wide::jg_dbl(acc);
+#pragma unroll 1
+        for (size_t k = grp; k < t; k += NG) {
+            const int d = dig[k * 65 + win];
+            if (!d) continue;
+            const size_t e = k * 8 + (d < 0 ? -d : d) - 1;
+            const uint32_t* w = ent + e * SEW;
+            if (w[SEF]) continue;  // identity multiple
+            JG E;
+            ld16(E.x.v, w);
+            ld16(E.y.v, w + SEY);
+            E.z = ld_r1(zs + e * LN);
+            if (d < 0) E.y = neg(E.y);
+            acc = wide::jg_add(acc, E);
+        }
+    }
+}
+
+// G2 bases on lane-pair groups: pair group grp of NG, lane half h (straus_g2lz_pair's arguments)
+DEV void straus_g2lz_wide(JL& acc, int NG, int grp, int h, size_t task, size_t t, const uint8_t* __restrict__ pts,
+                          size_t pt_stride, const uint32_t* __restrict__ l, uint32_t* __restrict__ scratch) {
+    const uint8_t* base = pts + task * pt_stride;
+    const uint32_t* lk = l + task * t * 8;
+    uint32_t* ent = scratch + task * straus_lz_words(t);
+    uint32_t* zs = ent + t * 8 * 2 * SEW;
+    int8_t* dig = reinterpret_cast<int8_t*>(zs + 2 * t * 8 * 2 * LN);
+    acc = jl_inf();
+#pragma unroll 1
+    for (size_t k = grp; k < t; k += NG) {
+        cc::Aff<cc::Fp2> P1;
+        const bool ok = pl::pair_all(g2_decode(P1, base + k * 192));
+        recode_w4(dig + k * 65, lk + k * 8);
+        pl::Fp2 hx, hy;
+        hx.c = h ? P1.x.b : P1.x.a;
+        hy.c = h ? P1.y.b : P1.y.a;
+        const AL P{reduce(in_r2(hx)), reduce(in_r2(hy))};
+        JL J = ok ? jl_from_aff(P) : jl_inf();
+#pragma unroll 1
+        for (int d = 0; d < 8; d++) {
+            if (d == 1) J = wide::jl_dbl(J);
+            else if (d > 1 && ok) J = wide::jl_add_aff(J, P);
+            const size_t e = k * 8 + d;
+            uint32_t* w = ent + (e * 2 + h) * SEW;
+            st_w(w, J.x);
+            st_w(w + SEY, J.y);
+            w[SEF] = jl_is_inf(J) ? 1u : 0u;
+            st_w(zs + (e * 2 + h) * LN, J.z);
+        }
+    }
+#pragma unroll 1
+    for (int win = 64; win >= 0; win--) {
+        if (win != 64 && !jl_is_inf(acc))
+#pragma unroll 1
+            for (int z = 0; z < 4; z++) acc = wide::jl_dbl(acc);
+#pragma unroll 1
+        for (size_t k = grp; k < t; k += NG) {
+            const int d = dig[k * 65 + win];
+            if (!d) continue;
+            const size_t e = k * 8 + (d < 0 ? -d : d) - 1;
+            const uint32_t* w = ent + (e * 2 + h) * SEW;
+            if (w[SEF]) continue;  // identity multiple (both halves carry the flag)
+            JL E;
+            ld16(E.x.c.v, w);
+            ld16(E.y.c.v, w + SEY);
+            E.z = ld_w(zs + (e * 2 + h) * LN);
+            if (d < 0) E.y = neg(E.y);
+            acc = wide::jl_add(acc, E);
+        }
+    }
+}
+}  // namespace
+
 __global__ __launch_bounds__(64) void k_prep_sigg2_var_wide(size_t n, int q, const uint8_t* __restrict__ s1b,
                                                             const uint8_t* __restrict__ s2b,
                                                             const uint8_t* __restrict__ vkX,
@@ -163,20 +303,27 @@ __global__ __launch_bounds__(64) void k_prep_sigg2_var_wide(size_t n, int q, con
         }
     }
     fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
-    lz::JG a;
-    straus_g1lz_lane(a, 64, l, (size_t)q, vkY + i * (size_t)q * 97, scal + i * (size_t)q * 8,
+    constexpr int NG = 64 / WG;
+    const int grp = l / WG;
+    JG a;
+    straus_g1lz_wide(a, NG, grp, (size_t)q, vkY + i * (size_t)q * 97, scal + i * (size_t)q * 8,
                      scratch + i * straus_g1lz_words((size_t)q));
-    if (l == (q & 63)) {  // X~ with scalar 1 (q < 64 here: cc_verify_batch_pervk_device takes q <= 4096,
-        Aff<Fp> X;        // the lane then also holds the bases k = q mod 64 + 64 j)
-        if (g1_decode(X, vkX + i * 97)) a = lz::jg_add_aff(a, ag_of(lz::reduce(lz::in_r(X.x)), lz::reduce(lz::in_r(X.y))));
+    // the groups' sums (lower group first, so every group ends with the same coordinates)
+#pragma unroll 1
+    for (int m = WG; m < 64; m <<= 1) {
+        const JG o = shfl_xor_jg(a, m);
+        const bool lo = (l & m) == 0;
+        a = wide::jg_add(sel_pt(lo, a, o), sel_pt(lo, o, a));
     }
-    Jac<Fp> pr = lz::jg_to(a);
-    lane_group_sum<Fp, 64>(pr);  // every lane the same sum
-    if (jac_is_inf(pr)) {
+    {  // X~ with scalar 1
+        Aff<Fp> X;
+        if (g1_decode(X, vkX + i * 97)) a = wide::jg_add_aff(a, ag_of(reduce(in_r(X.x)), reduce(in_r(X.y))));
+    }
+    if (jg_is_inf(a)) {
         fl |= 4u;
     } else {
         Fp x, y;
-        lz::jg_to_aff_rp(x, y, lz::jg_from(pr));
+        jg_to_aff_rp(x, y, a);
         if (l < 2) st_fp(S, S_P1 + h, i, h ? y : x);
     }
     if (l == 0) flags[i] = fl;
@@ -206,19 +353,26 @@ __global__ __launch_bounds__(64) void k_prep_sigg1_var_wide(size_t n, int q, con
         }
     }
     fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
-    lz::JL la;
-    straus_g2lz_pair(la, 32, p, h, i, (size_t)q, vkY, (size_t)q * 192, 0, 192, scal, 1, scratch);
-    if (p == (q & 31)) {  // X~ with scalar 1 (both lanes of the pair decode it)
+    constexpr int NG = 32 / WG;
+    const int grp = p / WG;
+    JL la;
+    straus_g2lz_wide(la, NG, grp, h, i, (size_t)q, vkY, (size_t)q * 192, scal, scratch);
+#pragma unroll 1
+    for (int m = 2 * WG; m < 64; m <<= 1) {
+        const JL o = shfl_xor_jl(la, m);
+        const bool lo = (l & m) == 0;
+        la = wide::jl_add(sel_pt(lo, la, o), sel_pt(lo, o, la));
+    }
+    {  // X~ with scalar 1
         Aff<Fp2> X;
         if (pl::pair_all(g2_decode(X, vkX + i * 192))) {
             pl::Fp2 hx, hy;
             hx.c = h ? X.x.b : X.x.a;
             hy.c = h ? X.y.b : X.y.a;
-            la = lz::jl_add_aff(la, lz::AL{lz::reduce(lz::in_r2(hx)), lz::reduce(lz::in_r2(hy))});
+            la = wide::jl_add_aff(la, AL{reduce(in_r2(hx)), reduce(in_r2(hy))});
         }
     }
     Jac<pl::Fp2> acc = pl::jl_to_pl(la);
-    pl::pair_group_sum<64>(acc);  // every pair the same sum
     Aff<pl::Fp2> a;
     if (!jac_to_aff(a, acc)) fl |= 4u;
     if (p == 0) {
