@@ -848,12 +848,16 @@ __global__ __launch_bounds__(64, 1) void k_fexp1(size_t n, uint32_t* __restrict_
 // The RLC fold's 16 window pairs (fold.hip): few, so each runs alone on a wave in the wide form of
 // k_fexp1 — the 32 lane pairs hold the same values and a step's independent Fp2 products (pairing.inc
 // line_dbl / line_add / eval_line / f12_mul_line, the same formulas) are spread over them, one
-// product a pair, results gathered with shuffles.  A doubling iteration is three product latencies:
-//   A: f^2 (pairs 0..17) with line_dbl's X Y, Y^2, Z^2, (Y + Z)^2, X^2 (pairs 18..22);
-//   B: T's a (b - 3e), e^2, g^2, b h (pairs 0..3) with the line's evaluation at P (pairs 4..6);
-//   C: f times the line as a full Fp12 (A + C w^2).
-// An addition step is four: Q_y Z, Q_x Z | theta^2, lambda^2, theta Q_x, lambda Q_y | lambda d, Z c,
-// X d and the evaluation | T's four products with f times the line (pairs 4..21).
+// product a pair, results gathered with shuffles.  The point T's chain and f's chain are independent
+// until f takes a line, so the loop runs them as a pipeline of LEVELS, one Fp2 product a pair each:
+// pairs 18.. take T's next level — a doubling is two (A: X Y, Y^2, Z^2, (Y + Z)^2, X^2; B: T's a (b -
+// 3e), e^2, g^2, b h with the line's evaluation at P), an addition four (Q_y Z, Q_x Z | theta^2,
+// lambda^2, theta Q_x, lambda Q_y | lambda d, Z c, X d and the evaluation | T's four products) — and
+// pairs 0..17 the oldest of f's pending operations (f^2, or f times a finished line as a full Fp12
+// A + C w^2).  f's operations keep their order, so the result is the sequential loop's, in 147 levels
+// instead of 209 (a doubling iteration 2 instead of 3): X = T's A | f times the previous doubling's
+// line (f^2 after an addition step), Y = T's B | f^2; an addition step's first level takes the
+// doubling's line, its last the addition's.
 // P (slots S_P1..+2) is in evaluation form (X Z, Y, Z^3); an Fp factor multiplies as the Fp2 (k, 0).
 DEV Fp2 f2_of_fp(const Fp& k) {
     Fp z;
@@ -900,11 +904,20 @@ __global__ __launch_bounds__(64, 1) void k_miller_wide(size_t n, const uint32_t*
         T.x = Q.x;
         T.y = Q.y;
         f2_one(T.z);
+        // the doubling line not yet multiplied into f (taken at the next iteration's first level)
+        Fp2 lp0, lp2, lp3;
+        bool havep = false;
 #pragma unroll 1
         for (int b = 62; b >= 0; b--) {
             Fp2 o1, o2, pr, l0, l2c, l3c;
-            {  // A
-                f12w_operands(o1, o2, j, f, f);
+            {  // X: T's A products (pairs 18..22) | f times the pending line, else f^2 (pairs 0..17)
+                if (havep) {
+                    Fp12 L;
+                    line_fp12(L, lp0, lp2, lp3);
+                    f12w_operands(o1, o2, j, f, L);
+                } else {
+                    f12w_operands(o1, o2, j, f, f);
+                }
                 Fp2 yz;
                 f2_add_lz(yz, T.y, T.z);
                 const Fp2 a1[5] = {T.x, T.y, T.z, yz, T.x}, a2[5] = {T.y, T.y, T.z, yz, T.x};
@@ -927,40 +940,47 @@ __global__ __launch_bounds__(64, 1) void k_miller_wide(size_t n, const uint32_t*
             f2_dbl(l2c, t);
             f2_add(l2c, l2c, t);
             f2_neg(l3c, h);
-            {  // B
+            {  // Y: T's B products and the line's evaluation (pairs 18..24) | f^2 if X took the line
                 Fp2 bmf;
                 f2_sub(bmf, bb, ff);
                 const Fp2 a1[7] = {a, e, g, bb, l0, l2c, l3c}, a2[7] = {bmf, e, g, h, PZ, PX, PY};
-                o1 = a1[0];
-                o2 = a2[0];
-                pick2(o1, o2, j, a1, a2, 7);
+                if (havep) {
+                    f12w_operands(o1, o2, j, f, f);
+                } else {
+                    o1 = a1[0];
+                    o2 = a2[0];
+                }
+                pick2(o1, o2, j - 18, a1, a2, 7);
                 f2_mul(pr, o1, o2);
+                if (havep) f12w_assemble(f, pr);
             }
-            T.x = bcast_f2(pr, 0);
+            T.x = bcast_f2(pr, 18);
             {
-                const Fp2 e2 = bcast_f2(pr, 1);
-                T.y = bcast_f2(pr, 2);
+                const Fp2 e2 = bcast_f2(pr, 19);
+                T.y = bcast_f2(pr, 20);
                 f2_sub(T.y, T.y, e2);
                 f2_sub(T.y, T.y, e2);
                 f2_sub(T.y, T.y, e2);
             }
-            T.z = bcast_f2(pr, 3);
-            {  // C
-                Fp12 L;
-                line_fp12(L, bcast_f2(pr, 4), bcast_f2(pr, 5), bcast_f2(pr, 6));
-                f12_mul_wide(f, f, L);
-            }
+            T.z = bcast_f2(pr, 21);
+            lp0 = bcast_f2(pr, 22);
+            lp2 = bcast_f2(pr, 23);
+            lp3 = bcast_f2(pr, 24);
+            havep = true;
             if (!((X_ABS >> b) & 1ull)) continue;
-            // addition step (pairing.inc line_add)
+            // addition step (pairing.inc line_add); its first level also takes the doubling's line
             Fp2 theta, lambda;
-            {  // D1
+            {  // D1: Q_y Z, Q_x Z (pairs 18, 19) | f times the doubling's line (pairs 0..17)
+                Fp12 L;
+                line_fp12(L, lp0, lp2, lp3);
+                f12w_operands(o1, o2, j, f, L);
                 const Fp2 a1[2] = {Q.y, Q.x}, a2[2] = {T.z, T.z};
-                o1 = a1[0];
-                o2 = a2[0];
-                pick2(o1, o2, j, a1, a2, 2);
+                pick2(o1, o2, j - 18, a1, a2, 2);
                 f2_mul(pr, o1, o2);
-                f2_sub(theta, T.y, bcast_f2(pr, 0));
-                f2_sub(lambda, T.x, bcast_f2(pr, 1));
+                f12w_assemble(f, pr);
+                havep = false;
+                f2_sub(theta, T.y, bcast_f2(pr, 18));
+                f2_sub(lambda, T.x, bcast_f2(pr, 19));
             }
             {  // D2
                 const Fp2 a1[4] = {theta, lambda, theta, lambda}, a2[4] = {theta, lambda, Q.x, Q.y};
@@ -1001,6 +1021,14 @@ __global__ __launch_bounds__(64, 1) void k_miller_wide(size_t n, const uint32_t*
                 T.z = bcast_f2(pr, 3);
                 f12w_assemble(f, pr, 4);
             }
+        }
+        if (havep) {  // the last doubling's line
+            Fp2 o1, o2, pr;
+            Fp12 L;
+            line_fp12(L, lp0, lp2, lp3);
+            f12w_operands(o1, o2, j, f, L);
+            f2_mul(pr, o1, o2);
+            f12w_assemble(f, pr);
         }
         f12_conj(f, f);
     }
