@@ -369,6 +369,55 @@ def test_small_batch_pok_paths_agree(ctxs, mode):
 
 
 @pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_small_batch_pok_degenerate_challenges(ctxs, mode):
+    """chal J runs on the one-wave prep as a chain of spread doublings and additions (curve_wide_lz.h):
+    challenges 0, 1, r - 1 and one with only top digits, and (SigG2) J = (0, +-2), a point of order 3
+    outside G1 that the reference does not reject, whose windowed multiples hit the addition's
+    doubling and identity branches.  Verdicts against the C oracle's PoKOfSignatureProof::verify,
+    verdicts and GT bytes between the small-batch and the lane-pair paths."""
+    import bench_modes
+    from coconut import pok_verify_batch
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+    m = MODES[mode]
+    ctx = ctxs[mode]
+    n, q, k = FEXP_WIDE_MAX + 6, 32, 7
+    b = bench_modes.make_pok_batch(ctx, m, n, q=q, seed=991 + m, bad_every=0)
+    ctx.set_params(b["g_tilde"])
+    ctx.set_verkey(b["X"], b["Y"])
+    sb, ob = (192, 97) if m == 0 else (97, 192)
+    nr, r = b["nresp"], len(b["revealed"])
+    chal, J = bytearray(b["chal"]), bytearray(b["J"])
+    for i, c in enumerate([0, 1, R - 1, (1 << 254) | (0xF << 248)]):
+        chal[48 * i:48 * (i + 1)] = c.to_bytes(48, "big")
+    if m == 0:
+        for i, y in ((4, 2), (5, P - 2)):
+            J[ob * i:ob * (i + 1)] = b"\x04" + bytes(48) + y.to_bytes(48, "big")
+            chal[48 * i:48 * (i + 1)] = (7 + i).to_bytes(48, "big")
+    chal, J = bytes(chal), bytes(J)
+
+    def run(lo, hi):
+        return pok_verify_batch(ctx, hi - lo, q, b["revealed"], nr, b["s1"][lo * sb:hi * sb], b["s2"][lo * sb:hi * sb],
+                                J[lo * ob:hi * ob], b["T"][lo * ob:hi * ob], b["resp"][lo * nr * 48:hi * nr * 48],
+                                chal[lo * 48:hi * 48], b["rev"][lo * r * 48:hi * r * 48], want_gt=True)
+    v_w, gt_w = run(0, k)
+    v_big, gt_big = run(0, n)
+    assert np.array_equal(v_big[:k], v_w)
+    assert gt_big[:576 * k] == gt_w
+    assert np.array_equal(v_big[k:], b["expect"][k:])
+    oc = oracle_lib()
+    idx = (ctypes.c_uint64 * r)(*b["revealed"])
+    Yb = b["Y"] if isinstance(b["Y"], (bytes, bytearray)) else b"".join(b["Y"])
+    for i in range(k):
+        gt = ctypes.create_string_buffer(576)
+        v = oc.oc_pok_verify(m, ctypes.c_size_t(q), ctypes.c_size_t(r), b["s1"][i * sb:(i + 1) * sb],
+                             b["s2"][i * sb:(i + 1) * sb], J[i * ob:(i + 1) * ob], b["T"][i * ob:(i + 1) * ob],
+                             b["resp"][i * nr * 48:(i + 1) * nr * 48], ctypes.c_size_t(nr), chal[48 * i:48 * (i + 1)],
+                             idx, b["rev"][i * r * 48:(i + 1) * r * 48], b["X"], Yb, b["g_tilde"], gt)
+        assert v_w[i] == v, i
+
+
+@pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_small_batch_pervk_paths_agree(ctxs, mode):
     """Per-credential-verkey batches of <= 1,024 take the one-wave-per-credential prep (pervk.hip
     k_prep_*_var_wide: one base per lane / lane pair), larger ones the lane-pair Straus: the same
@@ -395,6 +444,69 @@ def test_small_batch_pervk_paths_agree(ctxs, mode):
         v1, g1 = run(i, i + 1)
         assert v1[0] == b["expect"][i], i
         assert g1 == gt_big[576 * i:576 * (i + 1)], i
+
+
+@pytest.mark.parametrize("mode", ["G2", "G1"])
+def test_small_batch_pervk_degenerate_bases(ctxs, mode):
+    """The one-wave per-credential-verkey prep runs each base's Straus on its own lane group and adds the
+    groups' sums in a butterfly of spread additions (curve_wide_lz.h): equal group sums (the doubling
+    branch), opposite ones (the identity), an identity base, a zero scalar and all bases equal reach
+    the exceptional cases.  Verdicts and GT bytes against the C oracle, on the small-batch path and on
+    the lane-pair path (the same credentials inside a batch of > 1,024)."""
+    import bench_modes
+    from coconut import verify_batch
+    R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+    m = MODES[mode]
+    ctx = ctxs[mode]
+    n, q, k = FEXP_WIDE_MAX + 6, 6, 6
+    b = bench_modes.make_pervk_batch(ctx, m, n, q, seed=4242 + m, bad_every=0)
+    ctx.set_params(b["g_tilde"])
+    sb, ob = (192, 97) if m == 0 else (97, 192)
+    ident = (b"\x04" + bytes(ob - 1)) if m == 0 else bytes(ob)
+    Y = bytearray(b["Y"])
+    msgs = bytearray(b["msgs"])
+
+    def ybase(i, j):
+        return bytes(Y[(i * q + j) * ob:(i * q + j + 1) * ob])
+
+    def set_y(i, j, v):
+        Y[(i * q + j) * ob:(i * q + j + 1) * ob] = v
+
+    def msg(i, j):
+        return int.from_bytes(msgs[(i * q + j) * 48:(i * q + j + 1) * 48], "big")
+
+    def set_m(i, j, v):
+        msgs[(i * q + j) * 48:(i * q + j + 1) * 48] = (v % R).to_bytes(48, "big")
+    set_y(0, 1, ybase(0, 0))                  # equal group sums: Y1 = Y0, m1 = m0
+    set_m(0, 1, msg(0, 0))
+    set_y(1, 1, ybase(1, 0))                  # opposite group sums: m1 = -m0
+    set_m(1, 1, R - msg(1, 0))
+    set_y(2, 2, ident)                        # an identity base
+    set_m(3, 4, 0)                            # a zero scalar
+    for j in range(1, q):                     # all bases and scalars equal
+        set_y(4, j, ybase(4, 0))
+        set_m(4, j, msg(4, 0))
+    for j in range(q):                        # every term cancels but X~
+        set_y(5, j, ybase(5, 0))
+        set_m(5, j, msg(5, 0) if j % 2 == 0 else R - msg(5, 0))
+    Y, msgs = bytes(Y), bytes(msgs)
+
+    def run(lo, hi):
+        return verify_batch(ctx, hi - lo, q, b["s1"][lo * sb:hi * sb], b["s2"][lo * sb:hi * sb],
+                            msgs[lo * q * 48:hi * q * 48], vk=(b["X"][lo * ob:hi * ob], Y[lo * q * ob:hi * q * ob]),
+                            want_gt=True)
+    v_w, gt_w = run(0, k)
+    oc = oracle_lib()
+    ver = ctypes.create_string_buffer(k)
+    ref = ctypes.create_string_buffer(576 * k)
+    oc.oc_verify_batch(m, ctypes.c_size_t(k), ctypes.c_size_t(q), b["s1"][:k * sb], b["s2"][:k * sb],
+                       msgs[:k * q * 48], b["X"][:k * ob], Y[:k * q * ob], 1, b["g_tilde"], ver, ref, host_threads())
+    assert np.array_equal(v_w, np.frombuffer(ver.raw, np.uint8))
+    assert gt_w == ref.raw
+    v_big, gt_big = run(0, n)
+    assert np.array_equal(v_big[:k], v_w)
+    assert gt_big[:576 * k] == gt_w
+    assert np.array_equal(v_big[k:], b["expect"][k:])
 
 
 @pytest.mark.parametrize("mode", ["G2", "G1"])
