@@ -765,10 +765,13 @@ __global__ __launch_bounds__(256, 2) void k_prep_pok_g1pl(size_t n, int q, int r
 // The two PoK preps above walk a proof's whole Schnorr MSM (g~ and every hidden Y~ times its response,
 // nwin table windows each), chal J and J' on one lane (pair) or two waves' lanes: for a small batch the
 // launch then lasts that chain (~9 ms at n = 1).  Here one BLOCK of two waves takes one proof: wave 0
-// decodes sigma' and runs chal J (a 256-doubling chain, the part no lane split shortens), wave 1
-// spreads the table terms over its lanes (G1) or lane pairs (G2) — term t = (response or revealed
-// message, window) to lane t mod L — adds -T and X~ + J on two of them, and butterfly-sums the
-// Schnorr part and J'.  The Schnorr parts meet in LDS.  Same outputs as the kernels above.
+// decodes sigma' (sigma'_1 and sigma'_2 on its two halves) and runs chal J — a 256-doubling chain no
+// lane split shortens, so each doubling's and addition's products are spread over lane groups instead
+// (curve_wide_lz.h: 3 product times a doubling, 5 an addition), the multiples dJ in LDS (the jtab
+// argument is unused here) — while wave 1 spreads the table terms over its lanes (G1) or lane pairs
+// (G2) — term t = (response or revealed message, window) to lane t mod L — adds -T and X~ + J on two of
+// them, and butterfly-sums the Schnorr part and J'.  The Schnorr parts meet in LDS.  Same outputs as
+// the kernels above.
 DEV bool pok_revealed(int hh, int r, const uint32_t* rev_idx) {
     bool rv = false;
     for (int z = 0; z < r; z++) rv |= rev_idx[z] == (uint32_t)hh;
