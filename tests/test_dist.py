@@ -1,4 +1,4 @@
-"""Multi-rank control flow of coconut/dist.py on CPU: world_size 2 over the gloo backend.
+"""Multi-rank control flow of coconut/dist.py on CPU: world sizes 2 and 4 over the gloo backend.
 
 The device engine is replaced by a CPU engine whose per-credential verdicts come from the C oracle
 (test infrastructure) and whose PARTIAL_WORDS-word partial carries the shard's "not all valid" flag, so these
@@ -18,7 +18,7 @@ import torch.multiprocessing as mp
 
 from conftest import golden, oracle_lib
 
-WORLD = 2
+WORLDS = (2, 4)
 
 
 def _free_port():
@@ -66,13 +66,13 @@ class OracleEngine:
         return self._v
 
 
-def _worker(rank, port, idx, out_dir):
+def _worker(rank, world, port, idx, out_dir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from coconut.dist import shard_bounds, verify_sharded
         d = golden("verify_g2_q6.json")
-        lo, hi = shard_bounds(len(idx), WORLD, rank)
+        lo, hi = shard_bounds(len(idx), world, rank)
         eng = OracleEngine(_oracle_verdicts(d, idx[lo:hi]))
         v = verify_sharded(eng, rlc=True)
         np.save(os.path.join(out_dir, f"r{rank}.npy"), np.concatenate([v, [int(eng.fell_back)]]))
@@ -80,9 +80,9 @@ def _worker(rank, port, idx, out_dir):
         dist.destroy_process_group()
 
 
-def _run(idx, tmp_path):
-    mp.spawn(_worker, args=(_free_port(), idx, str(tmp_path)), nprocs=WORLD, join=True)
-    outs = [np.load(tmp_path / f"r{r}.npy") for r in range(WORLD)]
+def _run(idx, tmp_path, world):
+    mp.spawn(_worker, args=(world, _free_port(), idx, str(tmp_path)), nprocs=world, join=True)
+    outs = [np.load(tmp_path / f"r{r}.npy") for r in range(world)]
     return np.concatenate([o[:-1] for o in outs]), [bool(o[-1]) for o in outs]
 
 
@@ -95,22 +95,38 @@ def test_shard_bounds_cover_batch():
             assert all(b[r][1] == b[r + 1][0] for r in range(world - 1))
 
 
-def test_rlc_all_valid_batch_accepted_by_every_rank(tmp_path):
+@pytest.mark.parametrize("world", WORLDS)
+def test_rlc_all_valid_batch_accepted_by_every_rank(tmp_path, world):
     d = golden("verify_g2_q6.json")
     idx = [i for i, c in enumerate(d["creds"]) if c["verdict"] == 1]
     assert len(idx) >= 2
-    v, fell = _run(idx, tmp_path)
+    v, fell = _run(idx, tmp_path, world)
     assert v.all() and len(v) == len(idx)
-    assert fell == [False] * WORLD
+    assert fell == [False] * world
 
 
-def test_rlc_reject_is_collective_and_fallback_exact(tmp_path):
+@pytest.mark.parametrize("world", WORLDS)
+def test_rlc_reject_is_collective_and_fallback_exact(tmp_path, world):
     """A bad credential in ONE rank's slice makes EVERY rank fall back (one gathered decision), and
     the concatenated per-credential verdicts equal the fixture's."""
     d = golden("verify_g2_q6.json")
     good = [i for i, c in enumerate(d["creds"]) if c["verdict"] == 1]
     bad = [i for i, c in enumerate(d["creds"]) if c["verdict"] == 0]
     idx = good + bad[:1]  # the bad one lands in the last rank's slice
-    v, fell = _run(idx, tmp_path)
+    v, fell = _run(idx, tmp_path, world)
     assert list(v) == [d["creds"][i]["verdict"] for i in idx]
-    assert fell == [True] * WORLD
+    assert fell == [True] * world
+
+
+def test_rlc_more_ranks_than_credentials(tmp_path):
+    """Three credentials over four ranks: one rank's shard is empty (a neutral partial), the decision
+    is still collective, and a bad credential still makes every rank fall back."""
+    d = golden("verify_g2_q6.json")
+    good = [i for i, c in enumerate(d["creds"]) if c["verdict"] == 1]
+    bad = [i for i, c in enumerate(d["creds"]) if c["verdict"] == 0]
+    v, fell = _run(good[:3], tmp_path, 4)
+    assert v.all() and len(v) == 3 and fell == [False] * 4
+    idx = good[:2] + bad[:1]
+    v, fell = _run(idx, tmp_path, 4)
+    assert list(v) == [d["creds"][i]["verdict"] for i in idx]
+    assert fell == [True] * 4
