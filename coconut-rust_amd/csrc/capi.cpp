@@ -655,13 +655,15 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
 // Small batches run latency-bound: their Miller loops one wave per pair (n <= kWideMax: fexp_pl.hip
 // k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide) instead of one lane pair per credential (k_miller:
 // one 2-pair loop's latency on a lone wave, ~7.5 ms for any batch up to a few thousand), and their
-// final exponentiation one wave per credential (n <= kFexpWideMax: k_fexp1, ~1.9 ms) instead of a lane
-// quad (k_fexp_q: ~2.8 ms floor).  Both wide kernels hold one wave a SIMD: 1,024 waves a round of the
-// chip, i.e. 512 credentials a round of the Miller path, 1,024 of the fexp.  Measured
-// (profiles/r05/wide_spread): Miller 0.89 ms at n = 1 .. 512, 1.86 ms at 1,024 against 7.5 ms; fexp
-// 1.9 - 2.0 ms up to 1,024 (a second round would double it against the quad kernel's 2.8).
+// final exponentiation one wave per credential (n <= kFexpWideMax: k_fexp1, 1.33 ms) instead of a lane
+// quad (k_fexp_q: ~3 ms floor).  Both wide kernels hold one wave a SIMD: 1,024 waves a round of the
+// chip, i.e. 512 credentials a round of the Miller path, 1,024 of the fexp (two rounds, ~2.7 ms, still
+// under the quad kernel's floor at 2,048).  The PoK and per-credential-verkey preps take their one-wave
+// form up to kPrepWideMax (the shared-verkey prep up to kWideMax).  Measured: profiles/r05/wide_spread,
+// thresholds, miller_wide_pipe, fexp_thr.
 constexpr size_t kWideMax = 2048;
-constexpr size_t kFexpWideMax = 1024;
+constexpr size_t kFexpWideMax = 2048;
+constexpr size_t kPrepWideMax = 1024;
 static bool wide_short(DevBuf& p, DevBuf& f, DevBuf& v, size_t n) {
     const size_t m = 2 * n, words = m * 12;
     return n <= kWideMax && (p.bytes < words * 4 * PREP_SLOTS || f.bytes < m * 4 || v.bytes < words * 4 * 12);
@@ -723,7 +725,7 @@ static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t 
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     if (d_vkX)
         KCK(cck_prep_var(c->mode, n, (int)q, d_s1, d_s2, d_vkX, d_vkY, d_msgs, w.vkb->as<uint32_t>(),
-                         w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), n <= kFexpWideMax, st));
+                         w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), n <= kPrepWideMax, st));
     else  // small batches: one wave per credential, the MSM's window terms over its lanes
         KCK((n <= kWideMax ? cck_prep_wide : cck_prep)(c->mode, n, (int)q, d_s1, d_s2, d_msgs,
                                                        c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(),
@@ -1680,7 +1682,7 @@ static cc_status launch_pok(cc_ctx* c, const VerifyWork& w, size_t n, size_t q, 
                             uint8_t* d_gt, hipStream_t st) {
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     // small batches: one block of two waves per proof (the Schnorr terms over a wave's lanes)
-    KCK((n <= kFexpWideMax ? cck_prep_pok_wide : cck_prep_pok)(
+    KCK((n <= kPrepWideMax ? cck_prep_pok_wide : cck_prep_pok)(
         c->mode, n, (int)q, (int)r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, d_rev_msgs, d_idx, c->vk_aff.as<uint32_t>(),
         c->X_inf, c->table.as<uint32_t>(), c->wbits, c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(),
         w.flags->as<uint32_t>(), w.scratch->as<uint32_t>(), st));  // J*chal window table: the fexp scratch, free until fexp

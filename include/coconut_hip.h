@@ -99,8 +99,8 @@ cc_status cc_table_bits(const cc_ctx* ctx, int* verkey_bits, int* issuer_bits);
  *   rlc            : 0 = per-credential; 1 = random-linear-combination batch (all-or-fallback)
  * Returns CC_ERR_LEN if q differs from the shared verkey's q (the reference panics there).
  * Batch size picks the kernels, not the results: a batch of up to 2,048 credentials runs latency-bound
- * (one wave per Miller pair; up to 1,024 also one wave per final exponentiation and, shared verkey, per
- * prep), a larger one throughput-bound (one lane pair per credential); verdicts and GT bytes are the
+ * (one wave per Miller pair, one per final exponentiation, one per shared-verkey prep; up to 1,024 also
+ * one per per-credential-verkey or PoK prep), a larger one throughput-bound (one lane pair per credential); verdicts and GT bytes are the
  * same either way. */
 cc_status cc_verify_batch(cc_ctx* ctx, size_t n, size_t q, const uint8_t* sigma1, const uint8_t* sigma2,
                           const uint8_t* msgs, const uint8_t* vk_X, const uint8_t* vk_Y, uint8_t* verdicts,

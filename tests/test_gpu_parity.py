@@ -302,16 +302,16 @@ def test_ragged_batch_sizes_pair_lanes(ctxs, n):
     assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v)
 
 
-WIDE_MAX, FEXP_WIDE_MAX = 2048, 1024  # capi.cpp kWideMax, kFexpWideMax
+WIDE_MAX, FEXP_WIDE_MAX, PREP_WIDE_MAX = 2048, 2048, 1024  # capi.cpp kWideMax, kFexpWideMax, kPrepWideMax
 
 
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
     """Batches of <= 2,048 credentials take the one-wave-per-pair Miller path (capi.cpp kWideMax:
-    k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide) and those of <= 1,024 also the one-wave-per-
-    credential final exponentiation (kFexpWideMax: k_fexp1); larger ones the pair-lane loop and the
-    quad-lane fexp.  The same credentials through every combination (a 2,056 batch; its first 2,048,
-    1,024 and a ragged 37; then single credentials) give the same verdicts and GT bytes, with every
+    k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide), the one-wave-per-credential final
+    exponentiation (kFexpWideMax: k_fexp1) and the one-wave prep; larger ones the pair-lane loop, the
+    quad-lane fexp and the lane-pair prep.  The same credentials (a 2,056 batch; its first 2,049, 2,048,
+    1,025 and a ragged 37; then single credentials) give the same verdicts and GT bytes, with every
     corruption kind (identity sigmas included) in the batch."""
     import bench
     from coconut import verify_batch
@@ -324,7 +324,7 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
     sb = 192 if m == 0 else 97
     v_big, gt_big = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], want_gt=True)
     assert np.array_equal(v_big, b["expect"])
-    for k in (WIDE_MAX, FEXP_WIDE_MAX + 1, FEXP_WIDE_MAX, 37):
+    for k in (WIDE_MAX, WIDE_MAX + 1, PREP_WIDE_MAX + 1, 37):
         v_w, gt_w = verify_batch(ctx, k, q, b["s1"][:k * sb], b["s2"][:k * sb], b["msgs"][:k * q * 48], want_gt=True)
         assert np.array_equal(v_w, b["expect"][:k]), k
         assert gt_w == gt_big[:576 * k], k
@@ -338,9 +338,10 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_small_batch_pok_paths_agree(ctxs, mode):
     """PoK batches of <= 1,024 proofs take the one-block-per-proof prep (aggregate.hip
-    k_prep_pok_wide_*: chal J on one wave, the Schnorr and J' table terms spread over the other) and the
-    one-wave fexp; larger ones the lane-pair prep and the quad fexp: the same proofs (1/4 with a bad
-    response) give the same verdicts and GT bytes through both, and one at a time."""
+    k_prep_pok_wide_*: chal J on one wave, the Schnorr and J' table terms spread over the other), up to
+    2,048 the one-wave Miller loop and fexp, larger ones the lane-pair prep and Miller loop and the quad
+    fexp: the same proofs (1/4 with a bad response) give the same verdicts and GT bytes through all
+    three mixes (2,054 / 2,048 / one at a time)."""
     import bench_modes
     from coconut import pok_verify_batch
     m = MODES[mode]
@@ -420,8 +421,9 @@ def test_small_batch_pok_degenerate_challenges(ctxs, mode):
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_small_batch_pervk_paths_agree(ctxs, mode):
     """Per-credential-verkey batches of <= 1,024 take the one-wave-per-credential prep (pervk.hip
-    k_prep_*_var_wide: one base per lane / lane pair), larger ones the lane-pair Straus: the same
-    credentials (every corruption kind of make_pervk_batch) agree in verdicts and GT bytes."""
+    k_prep_*_var_wide: one lane group per base, spread point arithmetic), larger ones the lane-pair
+    Straus (and beyond 2,048 the batch Miller loop and fexp): the same credentials (every corruption kind
+    of make_pervk_batch) agree in verdicts and GT bytes through all three mixes."""
     import bench_modes
     from coconut import verify_batch
     m = MODES[mode]
@@ -452,7 +454,7 @@ def test_small_batch_pervk_degenerate_bases(ctxs, mode):
     groups' sums in a butterfly of spread additions (curve_wide_lz.h): equal group sums (the doubling
     branch), opposite ones (the identity), an identity base, a zero scalar and all bases equal reach
     the exceptional cases.  Verdicts and GT bytes against the C oracle, on the small-batch path and on
-    the lane-pair path (the same credentials inside a batch of > 1,024)."""
+    the lane-pair path (the same credentials inside a batch of > 2,048)."""
     import bench_modes
     from coconut import verify_batch
     R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
