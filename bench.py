@@ -284,8 +284,8 @@ def latency_of(ctx, launch, expect, dev, ns=(1, 256), reps=5, what="credentials"
         out[str(nn)] = {"ms": round(float(np.median(ms)), 3), "phase_ms": {"prep": round(ph[0], 3),
                         "miller": round(ph[1], 3), "fexp": round(ph[2], 3)}}
     return {what: out, "note": "one device call + synchronize on resident inputs, median of %d; batches of "
-                               "<= 2,048 run the one-wave-per-pair Miller loop, one-wave fexp and verify prep (PoK / "
-                               "per-verkey preps: <= 1,024)" % reps}
+                               "<= 4,096 run the one-wave-per-pair Miller loop (<= 2,048: one-wave fexp and verify prep; "
+                               "PoK / per-verkey preps: <= 1,024)" % reps}
 
 
 def latency_leg(ctx, d_s1, d_s2, d_m, q, expect, dev, ns=(1, 256), reps=5):

@@ -657,11 +657,12 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
 // one 2-pair loop's latency on a lone wave, ~7.5 ms for any batch up to a few thousand), and their
 // final exponentiation one wave per credential (n <= kFexpWideMax: k_fexp1, 1.33 ms) instead of a lane
 // quad (k_fexp_q: ~3 ms floor).  Both wide kernels hold one wave a SIMD: 1,024 waves a round of the
-// chip, i.e. 512 credentials a round of the Miller path, 1,024 of the fexp (two rounds, ~2.7 ms, still
-// under the quad kernel's floor at 2,048).  The PoK and per-credential-verkey preps take their one-wave
-// form up to kPrepWideMax (the shared-verkey prep up to kWideMax).  Measured: profiles/r05/wide_spread,
-// thresholds, miller_wide_pipe, fexp_thr.
-constexpr size_t kWideMax = 2048;
+// chip, i.e. 512 credentials a round of the Miller path (0.8 ms a round: eight rounds at 4,096, 6.4 ms,
+// under the pair-lane loop's ~7.5-9 ms latency there), 1,024 of the fexp (two rounds, ~2.7 ms, still
+// under the quad kernel's floor at 2,048).  The shared-verkey prep takes its one-wave form up to
+// kFexpWideMax, the PoK and per-credential-verkey preps up to kPrepWideMax.  Measured:
+// profiles/r05/wide_spread, thresholds, miller_wide_pipe, fexp_thr.
+constexpr size_t kWideMax = 4096;
 constexpr size_t kFexpWideMax = 2048;
 constexpr size_t kPrepWideMax = 1024;
 static bool wide_short(DevBuf& p, DevBuf& f, DevBuf& v, size_t n) {
@@ -727,7 +728,7 @@ static cc_status launch_verify(cc_ctx* c, const VerifyWork& w, size_t n, size_t 
         KCK(cck_prep_var(c->mode, n, (int)q, d_s1, d_s2, d_vkX, d_vkY, d_msgs, w.vkb->as<uint32_t>(),
                          w.prep->as<uint32_t>(), w.flags->as<uint32_t>(), n <= kPrepWideMax, st));
     else  // small batches: one wave per credential, the MSM's window terms over its lanes
-        KCK((n <= kWideMax ? cck_prep_wide : cck_prep)(c->mode, n, (int)q, d_s1, d_s2, d_msgs,
+        KCK((n <= kFexpWideMax ? cck_prep_wide : cck_prep)(c->mode, n, (int)q, d_s1, d_s2, d_msgs,
                                                        c->vk_aff.as<uint32_t>(), c->X_inf, c->table.as<uint32_t>(),
                                                        c->wbits, c->table_inf.as<uint32_t>(), w.prep->as<uint32_t>(),
                                                        w.flags->as<uint32_t>(), st));

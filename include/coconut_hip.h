@@ -98,9 +98,9 @@ cc_status cc_table_bits(const cc_ctx* ctx, int* verkey_bits, int* issuer_bits);
  *   gt_or_null     : n x 576 B, e(.,.)*e(.,.) as amcl_wrapper GT::to_bytes, or NULL
  *   rlc            : 0 = per-credential; 1 = random-linear-combination batch (all-or-fallback)
  * Returns CC_ERR_LEN if q differs from the shared verkey's q (the reference panics there).
- * Batch size picks the kernels, not the results: a batch of up to 2,048 credentials runs latency-bound
- * (one wave per Miller pair, one per final exponentiation, one per shared-verkey prep; up to 1,024 also
- * one per per-credential-verkey or PoK prep), a larger one throughput-bound (one lane pair per credential); verdicts and GT bytes are the
+ * Batch size picks the kernels, not the results: a batch of up to 4,096 credentials runs latency-bound
+ * (one wave per Miller pair; up to 2,048 also one per final exponentiation and per shared-verkey prep,
+ * up to 1,024 one per per-credential-verkey or PoK prep), a larger one throughput-bound (one lane pair per credential); verdicts and GT bytes are the
  * same either way. */
 cc_status cc_verify_batch(cc_ctx* ctx, size_t n, size_t q, const uint8_t* sigma1, const uint8_t* sigma2,
                           const uint8_t* msgs, const uint8_t* vk_X, const uint8_t* vk_Y, uint8_t* verdicts,

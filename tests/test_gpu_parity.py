@@ -302,17 +302,17 @@ def test_ragged_batch_sizes_pair_lanes(ctxs, n):
     assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v)
 
 
-WIDE_MAX, FEXP_WIDE_MAX, PREP_WIDE_MAX = 2048, 2048, 1024  # capi.cpp kWideMax, kFexpWideMax, kPrepWideMax
+WIDE_MAX, FEXP_WIDE_MAX, PREP_WIDE_MAX = 4096, 2048, 1024  # capi.cpp kWideMax, kFexpWideMax, kPrepWideMax
 
 
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
-    """Batches of <= 2,048 credentials take the one-wave-per-pair Miller path (capi.cpp kWideMax:
-    k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide), the one-wave-per-credential final
-    exponentiation (kFexpWideMax: k_fexp1) and the one-wave prep; larger ones the pair-lane loop, the
-    quad-lane fexp and the lane-pair prep.  The same credentials (a 2,056 batch; its first 2,049, 2,048,
-    1,025 and a ragged 37; then single credentials) give the same verdicts and GT bytes, with every
-    corruption kind (identity sigmas included) in the batch."""
+    """Batches of <= 4,096 credentials take the one-wave-per-pair Miller path (capi.cpp kWideMax:
+    k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide), those of <= 2,048 also the one-wave-per-
+    credential final exponentiation (kFexpWideMax: k_fexp1) and the one-wave prep; larger ones the
+    pair-lane loop, the quad-lane fexp and the lane-pair prep.  The same credentials (a 4,104 batch; its
+    first 4,096, 2,049, 2,048, 1,025 and a ragged 37; then single credentials) give the same verdicts
+    and GT bytes, with every corruption kind (identity sigmas included) in the batch."""
     import bench
     from coconut import verify_batch
     m = MODES[mode]
@@ -324,7 +324,7 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
     sb = 192 if m == 0 else 97
     v_big, gt_big = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], want_gt=True)
     assert np.array_equal(v_big, b["expect"])
-    for k in (WIDE_MAX, WIDE_MAX + 1, PREP_WIDE_MAX + 1, 37):
+    for k in (WIDE_MAX, FEXP_WIDE_MAX + 1, FEXP_WIDE_MAX, PREP_WIDE_MAX + 1, 37):
         v_w, gt_w = verify_batch(ctx, k, q, b["s1"][:k * sb], b["s2"][:k * sb], b["msgs"][:k * q * 48], want_gt=True)
         assert np.array_equal(v_w, b["expect"][:k]), k
         assert gt_w == gt_big[:576 * k], k
@@ -339,14 +339,14 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
 def test_small_batch_pok_paths_agree(ctxs, mode):
     """PoK batches of <= 1,024 proofs take the one-block-per-proof prep (aggregate.hip
     k_prep_pok_wide_*: chal J on one wave, the Schnorr and J' table terms spread over the other), up to
-    2,048 the one-wave Miller loop and fexp, larger ones the lane-pair prep and Miller loop and the quad
-    fexp: the same proofs (1/4 with a bad response) give the same verdicts and GT bytes through all
-    three mixes (2,054 / 2,048 / one at a time)."""
+    2,048 the one-wave fexp, up to 4,096 the one-wave Miller loop, larger ones the lane-pair prep and
+    Miller loop and the quad fexp: the same proofs (1/4 with a bad response) give the same verdicts and
+    GT bytes through every mix (4,102 / 2,049 / 2,048 / one at a time)."""
     import bench_modes
     from coconut import pok_verify_batch
     m = MODES[mode]
     ctx = ctxs[mode]
-    n, q = FEXP_WIDE_MAX + 6, 32
+    n, q = WIDE_MAX + 6, 32
     b = bench_modes.make_pok_batch(ctx, m, n, q=q, seed=777 + m, bad_every=4)
     ctx.set_params(b["g_tilde"])
     ctx.set_verkey(b["X"], b["Y"])
@@ -360,9 +360,10 @@ def test_small_batch_pok_paths_agree(ctxs, mode):
                                 b["rev"][lo * r * 48:hi * r * 48], want_gt=True)
     v_big, gt_big = run(0, n)
     assert np.array_equal(v_big, b["expect"])
-    v_w, gt_w = run(0, FEXP_WIDE_MAX)
-    assert np.array_equal(v_w, b["expect"][:FEXP_WIDE_MAX])
-    assert gt_w == gt_big[:576 * FEXP_WIDE_MAX]
+    for k in (FEXP_WIDE_MAX + 1, FEXP_WIDE_MAX):
+        v_w, gt_w = run(0, k)
+        assert np.array_equal(v_w, b["expect"][:k]), k
+        assert gt_w == gt_big[:576 * k], k
     for i in (0, 3, 4, 7, n - 1):
         v1, g1 = run(i, i + 1)
         assert v1[0] == b["expect"][i], i
@@ -382,7 +383,7 @@ def test_small_batch_pok_degenerate_challenges(ctxs, mode):
     P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
     m = MODES[mode]
     ctx = ctxs[mode]
-    n, q, k = FEXP_WIDE_MAX + 6, 32, 7
+    n, q, k = WIDE_MAX + 6, 32, 7
     b = bench_modes.make_pok_batch(ctx, m, n, q=q, seed=991 + m, bad_every=0)
     ctx.set_params(b["g_tilde"])
     ctx.set_verkey(b["X"], b["Y"])
@@ -422,13 +423,13 @@ def test_small_batch_pok_degenerate_challenges(ctxs, mode):
 def test_small_batch_pervk_paths_agree(ctxs, mode):
     """Per-credential-verkey batches of <= 1,024 take the one-wave-per-credential prep (pervk.hip
     k_prep_*_var_wide: one lane group per base, spread point arithmetic), larger ones the lane-pair
-    Straus (and beyond 2,048 the batch Miller loop and fexp): the same credentials (every corruption kind
-    of make_pervk_batch) agree in verdicts and GT bytes through all three mixes."""
+    Straus (beyond 2,048 the quad fexp, beyond 4,096 the batch Miller loop): the same credentials (every
+    corruption kind of make_pervk_batch) agree in verdicts and GT bytes through every mix."""
     import bench_modes
     from coconut import verify_batch
     m = MODES[mode]
     ctx = ctxs[mode]
-    n, q = FEXP_WIDE_MAX + 6, 6
+    n, q = WIDE_MAX + 6, 6
     b = bench_modes.make_pervk_batch(ctx, m, n, q, seed=888 + m, bad_every=4)
     ctx.set_params(b["g_tilde"])
     sb, ob = (192, 97) if m == 0 else (97, 192)
@@ -439,9 +440,10 @@ def test_small_batch_pervk_paths_agree(ctxs, mode):
                             vk=(b["X"][lo * ob:hi * ob], b["Y"][lo * q * ob:hi * q * ob]), want_gt=True)
     v_big, gt_big = run(0, n)
     assert np.array_equal(v_big, b["expect"])
-    v_w, gt_w = run(0, FEXP_WIDE_MAX)
-    assert np.array_equal(v_w, b["expect"][:FEXP_WIDE_MAX])
-    assert gt_w == gt_big[:576 * FEXP_WIDE_MAX]
+    for k in (FEXP_WIDE_MAX + 1, FEXP_WIDE_MAX):
+        v_w, gt_w = run(0, k)
+        assert np.array_equal(v_w, b["expect"][:k]), k
+        assert gt_w == gt_big[:576 * k], k
     for i in (0, 3, 7, 11, n - 1):
         v1, g1 = run(i, i + 1)
         assert v1[0] == b["expect"][i], i
@@ -454,13 +456,13 @@ def test_small_batch_pervk_degenerate_bases(ctxs, mode):
     groups' sums in a butterfly of spread additions (curve_wide_lz.h): equal group sums (the doubling
     branch), opposite ones (the identity), an identity base, a zero scalar and all bases equal reach
     the exceptional cases.  Verdicts and GT bytes against the C oracle, on the small-batch path and on
-    the lane-pair path (the same credentials inside a batch of > 2,048)."""
+    the lane-pair path (the same credentials inside a batch of > 4,096)."""
     import bench_modes
     from coconut import verify_batch
     R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
     m = MODES[mode]
     ctx = ctxs[mode]
-    n, q, k = FEXP_WIDE_MAX + 6, 6, 6
+    n, q, k = WIDE_MAX + 6, 6, 6
     b = bench_modes.make_pervk_batch(ctx, m, n, q, seed=4242 + m, bad_every=0)
     ctx.set_params(b["g_tilde"])
     sb, ob = (192, 97) if m == 0 else (97, 192)
@@ -519,7 +521,7 @@ def test_identity_verkey_component_both_paths(ctxs, mode, which):
     lane-pair prep: verdicts and GT bytes of both against the C oracle."""
     from coconut import verify_batch
     m = MODES[mode]
-    q, n, k = 6, FEXP_WIDE_MAX + 6, 40
+    q, n, k = 6, WIDE_MAX + 6, 40
     b = _gen_batch(m, n, q, seed=55 + m, bad_every=5)
     ob, sb = (97, 192) if m == 0 else (192, 97)
     ident = (b"\x04" + bytes(ob - 1)) if m == 0 else bytes(ob)
