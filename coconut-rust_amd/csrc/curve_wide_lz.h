@@ -41,11 +41,13 @@ DEV auto pick(int k, const X0& x0, const Xs&... xs) {
     return r;
 }
 
-// dbl-2009-l: level 1 X^2, Y^2, Y Z; level 2 C = B^2, (X + B)^2, E^2; level 3 E (D - X3)
+// dbl-2009-l: level 1 X^2, Y^2, Z^2, (Y + Z)^2 (all squarings: Z3 = 2 Y Z = (Y + Z)^2 - Y^2 - Z^2);
+// level 2 C = B^2, (X + B)^2, E^2; level 3 E (D - X3)
 DEV JG jg_dbl(const JG& p) {
     const int k = member();
-    const auto m1 = mulr1(pick(k, p.x, p.y, p.y), pick(k, p.x, p.y, p.z));
-    const auto A = gat(m1, 0), B = gat(m1, 1), YZ = gat(m1, 2);
+    const auto m1 = sqrr1(pick(k, p.x, p.y, p.z, add(p.y, p.z)));
+    const auto A = gat(m1, 0), B = gat(m1, 1);
+    const auto Z3 = sub(sub(gat(m1, 3), B), gat(m1, 2));
     const auto E = smul<3>(A);
     const auto m2 = sqrr1(pick(k, B, add(p.x, B), E));
     const auto C = gat(m2, 0), XB = gat(m2, 1), E2 = gat(m2, 2);
@@ -53,7 +55,6 @@ DEV JG jg_dbl(const JG& p) {
     const auto D = squeeze(add(t, t));  // 2 ((X + B)^2 - A - C)
     const auto X3 = sub(E2, add(D, D));
     const auto Y3 = sub(mulr1(E, sub(D, X3)), smul<2>(squeeze(smul<4>(C))));  // E (D - X3) - 8 C
-    const auto Z3 = smul<2>(YZ);
     return {reduce(X3), reduce(Y3), reduce(Z3)};
 }
 
@@ -127,15 +128,15 @@ DEV auto pick2(int k, const X0& x0, const Xs&... xs) {
 
 DEV JL jl_dbl(const JL& p) {
     const int k = pmember();
-    const auto m1 = mulr(pick2(k, p.x, p.y, p.y), pick2(k, p.x, p.y, p.z));
-    const auto A = gat(m1, 0), B = gat(m1, 1), YZ = gat(m1, 2);
+    const auto m1 = sqrr(pick2(k, p.x, p.y, p.z, add(p.y, p.z)));
+    const auto A = gat(m1, 0), B = gat(m1, 1);
+    const auto Z3 = sub(sub(gat(m1, 3), B), gat(m1, 2));
     const auto E = smul<3>(A);
     const auto m2 = sqrr(pick2(k, B, add(p.x, B), E));
     const auto C = gat(m2, 0), XB = gat(m2, 1), E2 = gat(m2, 2);
     const auto D = norm(dbl(sub(sub(XB, A), C)));  // 2 ((X + B)^2 - A - C)
     const auto X3 = sub(E2, dbl(D));
     const auto Y3 = sub(mulr(E, sub(D, X3)), dbl(norm(smul<4>(C))));  // E (D - X3) - 8 C
-    const auto Z3 = dbl(YZ);
     return {reduce(X3), reduce(Y3), reduce(Z3)};
 }
 
