@@ -666,9 +666,9 @@ def test_rlc_partials_gathered_across_shards(ctxs, mode):
 
 @pytest.mark.parametrize("mode", ["G2", "G1"])
 def test_concurrent_verify_slots(ctxs, mode):
-    """cc_set_concurrency(3): six cc_verify_batch_device calls on three caller streams with no host
-    synchronisation in between (each slot reused twice, batches of different sizes so a slot's buffers
-    grow while the other slots' batches run), an n = 1 call (the serialized path) in the middle, then a
+    """cc_set_concurrency(3): eight cc_verify_batch_device calls on three caller streams with no host
+    synchronisation in between (each slot reused, batches of sizes on both sides of every small-batch
+    threshold so a slot's buffers grow while the other slots' batches run), an n = 1 call in the middle, then a
     host-buffer call and a set_verkey rebind that must wait for the slots; every verdict equals
     construction.  Then the per-credential-verkey fixture through cc_verify_batch_pervk_device on two
     streams.  The context is returned to one slot."""
@@ -677,7 +677,8 @@ def test_concurrent_verify_slots(ctxs, mode):
     m = MODES[mode]
     q = 6
     ctx = ctxs[mode]
-    b = _gen_batch(m, 1024, q, seed=2024 + m, bad_every=7)
+    N = WIDE_MAX + 8
+    b = _gen_batch(m, N, q, seed=2024 + m, bad_every=7)
     ctx.set_params(b["g_tilde"])
     ctx.set_verkey(b["X"], b["Y"])
     sb = 192 if m == 0 else 97
@@ -690,7 +691,9 @@ def test_concurrent_verify_slots(ctxs, mode):
         assert ctx.concurrency() == 3
         streams = [torch.cuda.Stream(dev) for _ in range(3)]
         torch.cuda.synchronize()
-        sizes = [256, 512, 1024, 1024, 1, 768, 1024]
+        # every kernel mix (one-wave Miller / fexp / prep up to their thresholds, the batch kernels past
+        # them) on the same slots, their buffers growing across the thresholds
+        sizes = [256, N, 1024, FEXP_WIDE_MAX + 1, 1, 768, N, WIDE_MAX]
         outs = []
         for k, n in enumerate(sizes):
             v = torch.zeros(n, dtype=torch.uint8, device=dev)
@@ -700,14 +703,14 @@ def test_concurrent_verify_slots(ctxs, mode):
                                                    ctypes.c_void_p(st.cuda_stream)) == 0
             v.record_stream(st)
             outs.append((n, v))
-        vh = verify_batch(ctx, 1024, q, b["s1"], b["s2"], b["msgs"])  # host path: waits for the slots
+        vh = verify_batch(ctx, N, q, b["s1"], b["s2"], b["msgs"])  # host path: waits for the slots
         assert np.array_equal(vh, b["expect"])
         torch.cuda.synchronize()
         for n, v in outs:
             assert np.array_equal(v.cpu().numpy(), b["expect"][:n]), n
         # a verkey rebind while batches are in flight: the rebuild waits for them, later batches see it
-        v0 = torch.zeros(1024, dtype=torch.uint8, device=dev)
-        assert _lib.lib.cc_verify_batch_device(ctx.h, 1024, q, P(d1), P(d2), P(dm), P(v0), None,
+        v0 = torch.zeros(N, dtype=torch.uint8, device=dev)
+        assert _lib.lib.cc_verify_batch_device(ctx.h, N, q, P(d1), P(d2), P(dm), P(v0), None,
                                                ctypes.c_void_p(streams[0].cuda_stream)) == 0
         b2 = _gen_batch(m, 512, q, seed=4048 + m, bad_every=5)
         ctx.set_verkey(b2["X"], b2["Y"])
