@@ -464,6 +464,59 @@ DEV void f12_cyc_sqr_wide(Fp12& r, const Fp12& x) {
     r.c.b = bcast_f2(v, 5);
 }
 
+// acc <- x z (f12_mul_wide, pairs 0..17) and y <- y^2 (f12_cyc_sqr_wide, pairs 18..23) in ONE level:
+// pow-by-x's tail multiplies acc by snapshots of y while y keeps squaring (each operand read before
+// either result is written, so z may be y)
+DEV void f12_mul_cs_wide(Fp12& acc, const Fp12& x, const Fp12& z, Fp12& y) {
+    const int j = pair_idx();
+    Fp2 o1, o2, prod;
+    f12w_operands(o1, o2, j, x, z);
+    {
+        const int jc = j % 6;  // pairs 18..23: product jc = j - 18
+        const int m = jc >> 1;
+        Fp2 oa[3] = {y.a.a, y.b.a, y.c.a}, ob[3] = {y.a.b, y.b.b, y.c.b};
+        const Fp2 a = f2_pick(m, oa, 3), b = f2_pick(m, ob, 3);
+        Fp2 c1 = a, c2 = b, s0, s1;
+        f2_add_lz(s0, a, b);
+        f2_mul_xi(s1, b);
+        f2_add_lz(s1, s1, a);
+        c1.c = fp_sel(jc & 1, s0.c, c1.c);
+        c2.c = fp_sel(jc & 1, s1.c, c2.c);
+        o1.c = fp_sel(j >= 18, c1.c, o1.c);
+        o2.c = fp_sel(j >= 18, c2.c, o2.c);
+    }
+    f2_mul(prod, o1, o2);
+    Fp2 v;
+    {  // f12_cyc_sqr_wide's combination, its products on pairs 18..23
+        const int q = j % 6;
+        const Fp2 Gab = bcast_f2(prod, 18 + ((0x224400 >> (4 * q)) & 15)),
+                  Gt = bcast_f2(prod, 18 + ((0x135111 >> (4 * q)) & 15));
+        const bool fa = q == 0 || q == 3 || q == 4;
+        Fp2 u, w, t;
+        f2_sub(u, Gt, Gab);
+        f2_mul_xi(t, Gab);
+        f2_sub(u, u, t);
+        f2_dbl(w, Gab);
+        f2_mul_xi(t, w);
+        w.c = fp_sel(q == 2, t.c, w.c);
+        u.c = fp_sel(fa, u.c, w.c);
+        const Fp2 cs[6] = {y.a.a, y.a.b, y.b.a, y.b.b, y.c.a, y.c.b};
+        Fp2 yy = f2_pick(q, cs, 6);
+        f2_neg(t, yy);
+        yy.c = fp_sel(fa, t.c, yy.c);
+        f2_add(w, u, yy);
+        f2_dbl(w, w);
+        f2_add(v, w, u);
+    }
+    f12w_assemble(acc, prod);
+    y.a.a = bcast_f2(v, 0);
+    y.a.b = bcast_f2(v, 1);
+    y.b.a = bcast_f2(v, 2);
+    y.b.b = bcast_f2(v, 3);
+    y.c.a = bcast_f2(v, 4);
+    y.c.b = bcast_f2(v, 5);
+}
+
 // f12_frob / f12_frob2 (pairing.inc) spread: pair q < 6 maps coefficient q (a.a, a.b, b.a, b.b, c.a,
 // c.b; the coefficient of W^k, k = 0 3 1 4 2 5): conj(c) gamma1_k, or c gamma2_k (gamma_0 = 1), then
 // the six are broadcast
@@ -704,14 +757,15 @@ static __device__ __noinline__ void fx_pow_x(Soa src, Soa dst, Soa K, size_t i, 
             fx_pow_x_gs<W>(src, dst, i);
             return;
         }
-        m12<W>(acc, acc, t);
-        m12<W>(acc, acc, y);
-        for (int k = 0; k < 3; k++) cs12<W>(y, y);
-        m12<W>(acc, acc, y);  // 2^60
-        for (int k = 0; k < 2; k++) cs12<W>(y, y);
-        m12<W>(acc, acc, y);  // 2^62
-        cs12<W>(y, y);
-        m12<W>(acc, acc, y);  // 2^63
+        // the tail's products of acc and its squarings of y pair up: 7 levels instead of 11
+        const Fp12 y57 = y;
+        f12_mul_cs_wide(acc, acc, t, y);    // acc = g^(2^16 + 2^48), y = g^(2^58)
+        f12_mul_cs_wide(acc, acc, y57, y);  // acc *= g^(2^57), y = g^(2^59)
+        f12_cyc_sqr_wide(y, y);             // 2^60
+        f12_mul_cs_wide(acc, acc, y, y);    // acc *= g^(2^60), y = g^(2^61)
+        f12_cyc_sqr_wide(y, y);             // 2^62
+        f12_mul_cs_wide(acc, acc, y, y);    // acc *= g^(2^62), y = g^(2^63)
+        f12_mul_wide(acc, acc, y);          // acc *= g^(2^63)
         f12_conj(acc, acc);
         st_f12(dst, i, acc);
         return;
