@@ -18,7 +18,7 @@ constexpr int vmax() { return 0; }
 template <class... I>
 constexpr int vmax(int a, I... b) { return a > vmax(b...) ? a : vmax(b...); }
 
-// ---------------------------------------------------------------- G1: product k on lane k
+// ---------------------------------------------------------------- G1: product k on member k of a lane group
 constexpr int G = 4;
 DEV int lane() { return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 DEV int member() { return lane() & (G - 1); }
@@ -31,7 +31,7 @@ DEV Fq<A, B> gat(const Fq<A, B>& x, int src) {
     for (int k = 0; k < LN; k++) r.v[k] = __shfl(x.v[k], from);
     return r;
 }
-// operand k of a level: x_k for lanes k < N, the last one beyond (fitted to the widest bound)
+// operand k of a level: x_k on members k < N, the last one beyond (fitted to the widest bound)
 template <class X0, class... Xs>
 DEV auto pick(int k, const X0& x0, const Xs&... xs) {
     constexpr int A = vmax(X0::AV, Xs::AV...), B = vmax(X0::BV, Xs::BV...);
@@ -103,7 +103,7 @@ DEV JG jg_add(const JG& p, const JG& q) {
     return {X3, reduce(Y3), reduce(Z3)};
 }
 
-// ---------------------------------------------------------------- G2 (pair-lane): product k on pair k
+// ---------------------------------------------------------------- G2 (pair-lane): product k on member pair k
 DEV int pmember() { return (lane() >> 1) & (G - 1); }
 template <int A, int B>
 DEV F2<A, B> gat(const F2<A, B>& x, int src_pair) {
