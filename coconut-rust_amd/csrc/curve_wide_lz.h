@@ -140,12 +140,14 @@ DEV JL jl_dbl(const JL& p) {
     return {reduce(X3), reduce(Y3), reduce(Z3)};
 }
 
-DEV JL jl_add_aff(const JL& p, const AL& q) {
-    if (jl_is_inf(p)) return jl_from_aff(q);
+// qx, qy: a reduced affine point (AL) or a canonical table entry (F2<AN, BC>, as curve_lz.h jl_add_aff_c)
+template <class QX, class QY>
+DEV JL jl_add_aff_c(const JL& p, const QX& qx, const QY& qy) {
+    if (jl_is_inf(p)) return {reduce(qx), reduce(qy), r_one()};
     const int k = pmember();
-    const auto m1 = mulr(pick2(k, p.z, q.y), p.z);  // Z1^2, y2 Z1
+    const auto m1 = mulr(pick2(k, p.z, qy), p.z);  // Z1^2, y2 Z1
     const auto z1z1 = gat(m1, 0), t = gat(m1, 1);
-    const auto m2 = mulr(pick2(k, q.x, t), z1z1);  // u2, s2
+    const auto m2 = mulr(pick2(k, qx, t), z1z1);  // u2, s2
     const F2R h = reduce(sub(gat(m2, 0), p.x));
     const F2R r0 = reduce(sub(gat(m2, 1), p.y));
     if (rz_is_zero(h)) return rz_is_zero(r0) ? wide::jl_dbl(p) : jl_inf();
@@ -161,6 +163,11 @@ DEV JL jl_add_aff(const JL& p, const AL& q) {
     const auto Y3 = sub(gat(m5, 0), dbl(gat(m5, 1)));
     const auto Z3 = sub(sub(zh, z1z1), hh);
     return {X3r, reduce(Y3), reduce(Z3)};
+}
+
+DEV JL jl_add_aff(const JL& p, const AL& q) {
+    if (jl_is_inf(p)) return jl_from_aff(q);
+    return jl_add_aff_c(p, q.x, q.y);
 }
 
 DEV JL jl_add(const JL& p, const JL& q) {
@@ -183,6 +190,48 @@ DEV JL jl_add(const JL& p, const JL& q) {
     const auto m5 = mulr(pick2(k, rr, s1), pick2(k, sub(v, X3), j));  // rr (v - X3), s1 j
     const auto Y3 = sub(gat(m5, 0), dbl(gat(m5, 1)));
     return {X3, reduce(Y3), reduce(Z3)};
+}
+
+// ---------------------------------------------------------------- sums of the groups' points
+// Every member of a group holds its group's point; a butterfly of spread additions (the lower group's
+// point first, so every group ends with the same coordinates) leaves the sum of all groups' points on
+// every lane.  G1: 16 groups a wave; G2: 8.
+template <class P>
+DEV P sel_pt(bool c, const P& a, const P& b) {
+    P r;
+    const int32_t* x = reinterpret_cast<const int32_t*>(&a);
+    const int32_t* y = reinterpret_cast<const int32_t*>(&b);
+    int32_t* o = reinterpret_cast<int32_t*>(&r);
+#pragma unroll
+    for (int w = 0; w < (int)(sizeof(P) / 4); w++) o[w] = c ? x[w] : y[w];
+    return r;
+}
+template <class P>
+DEV P shfl_xor_pt(const P& p, int m) {
+    P r;
+    const int32_t* x = reinterpret_cast<const int32_t*>(&p);
+    int32_t* o = reinterpret_cast<int32_t*>(&r);
+#pragma unroll
+    for (int w = 0; w < (int)(sizeof(P) / 4); w++) o[w] = __shfl_xor(x[w], m);
+    return r;
+}
+DEV JG jg_group_sum(JG a) {
+#pragma unroll 1
+    for (int m = G; m < 64; m <<= 1) {
+        const JG o = shfl_xor_pt(a, m);
+        const bool lo = (lane() & m) == 0;
+        a = wide::jg_add(sel_pt(lo, a, o), sel_pt(lo, o, a));
+    }
+    return a;
+}
+DEV JL jl_group_sum(JL a) {
+#pragma unroll 1
+    for (int m = 2 * G; m < 64; m <<= 1) {
+        const JL o = shfl_xor_pt(a, m);
+        const bool lo = (lane() & m) == 0;
+        a = wide::jl_add(sel_pt(lo, a, o), sel_pt(lo, o, a));
+    }
+    return a;
 }
 
 }  // namespace wide

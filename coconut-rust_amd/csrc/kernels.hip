@@ -18,6 +18,7 @@
 #include "soa.h"
 #include "subgroup.h"
 #include "curve_pl.h"  // pair-lane G2 (FT<pl::Fp2>), pl::swp
+#include "curve_wide_lz.h"
 
 using namespace cc;
 
@@ -408,33 +409,40 @@ __global__ __launch_bounds__(64) void k_prep_sigg2_wide(size_t n, int q, const u
         }
     }
     fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
+    // the window terms over 16 groups of 4 lanes (term t to group t mod 16), each group's sum by spread
+    // mixed additions (curve_wide_lz.h: the products of a step on the group's members), then the
+    // groups' butterfly of spread additions
     const int nwin = ft_nwin(wbits), nt = q * nwin;
-    Jac<Fp> acc;
-    if (l == 0 && !Xinf) {
+    constexpr int NG = 64 / lz::wide::G, EW = sizeof(Aff<Fp>) / 4;
+    const int grp = l / lz::wide::G;
+    lz::JG a = lz::jg_inf();
+    if (grp == 0 && !Xinf) {
         Aff<Fp> x;
+        Jac<Fp> xj;
         ld_aff_aos<Fp>(x, Xaff);
-        jac_from_aff(acc, x);
-    } else {
-        jac_set_inf(acc);
+        jac_from_aff(xj, x);
+        a = lz::jg_from(xj);
     }
-    {
-        lz::JG a = lz::jg_from(acc);
+    const size_t went = ft_went(wbits);
 #pragma unroll 1
-        for (int t = l; t < nt; t += 64) {
-            const int j = t / nwin, w = t - j * nwin;
-            if (binf_fixed[j]) continue;
-            Fr m;
-            fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
-            ft_add_lz(a, m.v, table, wbits, j, w, w + 1);
-        }
-        acc = lz::jg_to(a);
+    for (int t = grp; t < nt; t += NG) {  // group-uniform
+        const int j = t / nwin, w = t - j * nwin;
+        if (binf_fixed[j]) continue;
+        Fr m;
+        fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
+        const uint32_t d = ft_digit(m.v, w, wbits);
+        if (!d) continue;
+        Aff<Fp> e;
+        ft_load<Fp>(e, table + (size_t)j * ft_base_words<Fp>(wbits) + ((size_t)w * went + d - 1) * EW);
+        if (ft_is_empty(e)) continue;
+        a = lz::wide::jg_add_aff(a, lz::AG{lz::from_fp(e.x), lz::from_fp(e.y)});
     }
-    lane_group_sum<Fp, 64>(acc);  // every lane the same sum
-    if (jac_is_inf(acc)) {
+    a = lz::wide::jg_group_sum(a);  // every lane the same sum
+    if (lz::jg_is_inf(a)) {
         fl |= 4u;
     } else {
         Fp x, y;
-        lz::jg_to_aff_rp(x, y, lz::jg_from(acc));
+        lz::jg_to_aff_rp(x, y, a);
         if (l < 2) st_fp(S, S_P1 + h, i, h ? y : x);
     }
     if (l == 0) flags[i] = fl;
@@ -464,31 +472,47 @@ __global__ __launch_bounds__(64) void k_prep_sigg1_wide(size_t n, int q, const u
         }
     }
     fl = (uint32_t)__shfl((int)fl, 0) | (uint32_t)__shfl((int)fl, 1);
-    Jac<pl::Fp2> acc;
-    if (p == 0 && !Xinf) {
+    // the window terms over 8 groups of 4 lane pairs (term t to group t mod 8), spread mixed additions
+    // within a group, then the groups' butterfly (curve_wide_lz.h)
+    constexpr int NG = 32 / lz::wide::G, EW = sizeof(Aff<Fp2>) / 4;
+    const int grp = p / lz::wide::G;
+    lz::JL la = lz::jl_inf();
+    if (grp == 0 && !Xinf) {
         Aff<pl::Fp2> x;
+        Jac<pl::Fp2> xj;
         for (int c = 0; c < NL; c++) {
             x.x.c.v[c] = Xaff[NL * h + c];
             x.y.c.v[c] = Xaff[2 * NL + NL * h + c];
         }
-        jac_from_aff(acc, x);
-    } else {
-        jac_set_inf(acc);
+        jac_from_aff(xj, x);
+        la = pl::jl_from_pl(xj);
     }
     {
         const int nwin = ft_nwin(wbits), nt = q * nwin;
-        lz::JL la = pl::jl_from_pl(acc);
+        const size_t went = ft_went(wbits);
 #pragma unroll 1
-        for (int t = p; t < nt; t += 32) {  // pair-uniform
+        for (int t = grp; t < nt; t += NG) {  // group-uniform
             const int j = t / nwin, w = t - j * nwin;
             if (binf_fixed[j]) continue;
             Fr m;
             fr_from_be48(m, msgs + (i * (size_t)q + j) * 48);
-            pl::ft_add_g2_lz(la, m.v, table, wbits, j, w, w + 1);
+            const uint32_t d = ft_digit(m.v, w, wbits);
+            if (!d) continue;
+            const uint32_t* e = table + (size_t)j * ft_base_words<Fp2>(wbits) + ((size_t)w * went + d - 1) * EW;
+            Fp ex, ey;
+            uint32_t o = 0;
+#pragma unroll
+            for (int c = 0; c < NL; c++) {
+                ex.v[c] = e[NL * h + c];
+                ey.v[c] = e[2 * NL + NL * h + c];
+                o |= ex.v[c] | ey.v[c];
+            }
+            if (pl::pair_all(o == 0)) continue;  // (0, 0): an identity entry
+            la = lz::wide::jl_add_aff_c(la, lz::F2<lz::AN, lz::BC>{lz::from_fp(ex)}, lz::F2<lz::AN, lz::BC>{lz::from_fp(ey)});
         }
-        acc = pl::jl_to_pl(la);
     }
-    pl::pair_group_sum<64>(acc);  // every pair the same sum
+    la = lz::wide::jl_group_sum(la);  // every pair the same sum
+    Jac<pl::Fp2> acc = pl::jl_to_pl(la);
     Aff<pl::Fp2> a;
     if (!jac_to_aff(a, acc)) fl |= 4u;
     if (p == 0) {

@@ -148,37 +148,6 @@ namespace {
 using namespace cc::lz;
 constexpr int WG = wide::G;
 
-DEV JG shfl_xor_jg(const JG& p, int m) {
-    JG r;
-#pragma unroll
-    for (int c = 0; c < LN; c++) {
-        r.x.v[c] = __shfl_xor(p.x.v[c], m);
-        r.y.v[c] = __shfl_xor(p.y.v[c], m);
-        r.z.v[c] = __shfl_xor(p.z.v[c], m);
-    }
-    return r;
-}
-DEV JL shfl_xor_jl(const JL& p, int m) {
-    JL r;
-#pragma unroll
-    for (int c = 0; c < LN; c++) {
-        r.x.c.v[c] = __shfl_xor(p.x.c.v[c], m);
-        r.y.c.v[c] = __shfl_xor(p.y.c.v[c], m);
-        r.z.c.v[c] = __shfl_xor(p.z.c.v[c], m);
-    }
-    return r;
-}
-template <class P>
-DEV P sel_pt(bool c, const P& a, const P& b) {
-    P r;
-    const int32_t* x = reinterpret_cast<const int32_t*>(&a);
-    const int32_t* y = reinterpret_cast<const int32_t*>(&b);
-    int32_t* o = reinterpret_cast<int32_t*>(&r);
-#pragma unroll
-    for (int w = 0; w < (int)(sizeof(P) / 4); w++) o[w] = c ? x[w] : y[w];
-    return r;
-}
-
 // group grp of NG: sum of scal_k P_k over its bases (pts: t G1 encodings of 97 bytes)
 DEV void straus_g1lz_wide(JG& acc, int NG, int grp, size_t t, const uint8_t* __restrict__ pts,
                           const uint32_t* __restrict__ scal, uint32_t* __restrict__ ent) {
@@ -308,13 +277,7 @@ __global__ __launch_bounds__(64) void k_prep_sigg2_var_wide(size_t n, int q, con
     JG a;
     straus_g1lz_wide(a, NG, grp, (size_t)q, vkY + i * (size_t)q * 97, scal + i * (size_t)q * 8,
                      scratch + i * straus_g1lz_words((size_t)q));
-    // the groups' sums (lower group first, so every group ends with the same coordinates)
-#pragma unroll 1
-    for (int m = WG; m < 64; m <<= 1) {
-        const JG o = shfl_xor_jg(a, m);
-        const bool lo = (l & m) == 0;
-        a = wide::jg_add(sel_pt(lo, a, o), sel_pt(lo, o, a));
-    }
+    a = wide::jg_group_sum(a);  // the groups' sums
     {  // X~ with scalar 1
         Aff<Fp> X;
         if (g1_decode(X, vkX + i * 97)) a = wide::jg_add_aff(a, ag_of(reduce(in_r(X.x)), reduce(in_r(X.y))));
@@ -357,12 +320,7 @@ __global__ __launch_bounds__(64) void k_prep_sigg1_var_wide(size_t n, int q, con
     const int grp = p / WG;
     JL la;
     straus_g2lz_wide(la, NG, grp, h, i, (size_t)q, vkY, (size_t)q * 192, scal, scratch);
-#pragma unroll 1
-    for (int m = 2 * WG; m < 64; m <<= 1) {
-        const JL o = shfl_xor_jl(la, m);
-        const bool lo = (l & m) == 0;
-        la = wide::jl_add(sel_pt(lo, la, o), sel_pt(lo, o, la));
-    }
+    la = wide::jl_group_sum(la);  // the groups' sums
     {  // X~ with scalar 1
         Aff<Fp2> X;
         if (pl::pair_all(g2_decode(X, vkX + i * 192))) {
