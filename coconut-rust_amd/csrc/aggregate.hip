@@ -906,7 +906,7 @@ __global__ __launch_bounds__(128) void k_prep_pok_wide_sigg2(size_t n, int q, in
         fl |= 4u;
     } else {
         Fp x, y;
-        lz::jg_to_aff_rp(x, y, lz::jg_from(jp));
+        lz::wide::jg_to_aff_rp(x, y, lz::jg_from(jp));  // every lane the same point (lane_group_sum)
         if (l == 0) {
             st_fp(S, S_P1, i, x);
             st_fp(S, S_P1 + 1, i, y);

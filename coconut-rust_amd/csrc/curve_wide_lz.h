@@ -9,6 +9,7 @@
 // (G = 4); members past a level's last product compute a duplicate that nobody gathers.
 #pragma once
 #include "curve_lz.h"
+#include "tower_q.h"  // qinv: the quad divstep inversion
 
 namespace cc {
 namespace lz {
@@ -190,6 +191,15 @@ DEV JL jl_add(const JL& p, const JL& q) {
     const auto m5 = mulr(pick2(k, rr, s1), pick2(k, sub(v, X3), j));  // rr (v - X3), s1 j
     const auto Y3 = sub(gat(m5, 0), dbl(gat(m5, 1)));
     return {X3, reduce(Y3), reduce(Z3)};
+}
+
+// curve_lz.h jg_to_aff_rp for a point every lane holds alike: the inversion in the quad divstep form
+// (tower_q.h qinv: the iteration's four update chains one per lane of a quad)
+DEV void jg_to_aff_rp(Fp& x, Fp& y, const JG& p) {
+    const auto zi = qinv(p.z);
+    const auto zi2 = sqrr1(zi);
+    x = canon(mulr1(p.x, zi2));
+    y = canon(mulr1(p.y, mulr1(zi2, zi)));
 }
 
 // ---------------------------------------------------------------- sums of the groups' points

@@ -442,7 +442,7 @@ __global__ __launch_bounds__(64) void k_prep_sigg2_wide(size_t n, int q, const u
         fl |= 4u;
     } else {
         Fp x, y;
-        lz::jg_to_aff_rp(x, y, a);
+        lz::wide::jg_to_aff_rp(x, y, a);
         if (l < 2) st_fp(S, S_P1 + h, i, h ? y : x);
     }
     if (l == 0) flags[i] = fl;

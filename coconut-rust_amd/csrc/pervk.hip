@@ -286,7 +286,7 @@ __global__ __launch_bounds__(64) void k_prep_sigg2_var_wide(size_t n, int q, con
         fl |= 4u;
     } else {
         Fp x, y;
-        jg_to_aff_rp(x, y, a);
+        wide::jg_to_aff_rp(x, y, a);  // every lane the same point: the quad-form inversion
         if (l < 2) st_fp(S, S_P1 + h, i, h ? y : x);
     }
     if (l == 0) flags[i] = fl;
