@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(128) void k_prep_pok_wide_sigg1(size_t n, int q, in
     pl::pair_group_sum<64>(acc);
     pl::pair_group_sum<64>(jp);
     Aff<G2> a;
-    const uint32_t fl = jac_to_aff(a, jp) ? 0u : 4u;
+    const uint32_t fl = lz::wide::jac_to_aff(a, jp) ? 0u : 4u;  // every pair the same J': quad-form inversion
     if (p == 0) {
         pl::st_f2(S, S_Q1, i, a.x);
         pl::st_f2(S, S_Q1 + 2, i, a.y);

@@ -9,6 +9,7 @@
 // (G = 4); members past a level's last product compute a duplicate that nobody gathers.
 #pragma once
 #include "curve_lz.h"
+#include "curve_pl.h"
 #include "tower_q.h"  // qinv: the quad divstep inversion
 
 namespace cc {
@@ -200,6 +201,35 @@ DEV void jg_to_aff_rp(Fp& x, Fp& y, const JG& p) {
     const auto zi2 = sqrr1(zi);
     x = canon(mulr1(p.x, zi2));
     y = canon(mulr1(p.y, mulr1(zi2, zi)));
+}
+
+// curve.h jac_to_aff for a pair-lane G2 point every pair holds alike (storage form): the Fp2 inversion's
+// norm inverted in the quad divstep form, as fexp_pl.hip f2_inv_q
+DEV bool jac_to_aff(Aff<pl::Fp2>& r, const Jac<pl::Fp2>& p) {
+    if (cc::jac_is_inf(p)) {
+        pl::f2_zero(r.x);
+        pl::f2_zero(r.y);
+        return false;
+    }
+    pl::Fp2 zi, zi2, zi3;
+    {
+        const Fp zs = pl::swp(p.z.c);
+        Fp nn = pl::fp_mul2_v(p.z.c, p.z.c, zs, zs), ni;  // |z|^2 on both lanes
+        fp_inv_int_quad(ni, nn);                          // plain integer inverse of the Montgomery residue
+        constexpr uint32_t R3[NL] = {CC_R3_LIMBS};
+        Fp r3;
+#pragma unroll
+        for (int j = 0; j < NL; j++) r3.v[j] = R3[j];
+        fp_mul(nn, ni, r3);  // |z|^-2 R (field.h fp_inv)
+        pl::Fp2 t;
+        fp_mul(t.c, p.z.c, nn);
+        pl::f2_conj(zi, t);
+    }
+    pl::f2_sqr(zi2, zi);
+    pl::f2_mul(zi3, zi2, zi);
+    pl::f2_mul(r.x, p.x, zi2);
+    pl::f2_mul(r.y, p.y, zi3);
+    return true;
 }
 
 // ---------------------------------------------------------------- sums of the groups' points

@@ -514,7 +514,7 @@ __global__ __launch_bounds__(64) void k_prep_sigg1_wide(size_t n, int q, const u
     la = lz::wide::jl_group_sum(la);  // every pair the same sum
     Jac<pl::Fp2> acc = pl::jl_to_pl(la);
     Aff<pl::Fp2> a;
-    if (!jac_to_aff(a, acc)) fl |= 4u;
+    if (!lz::wide::jac_to_aff(a, acc)) fl |= 4u;  // the quad-form inversion
     if (p == 0) {
         pl::st_f2(S, S_Q1, i, a.x);
         pl::st_f2(S, S_Q1 + 2, i, a.y);

@@ -332,7 +332,7 @@ __global__ __launch_bounds__(64) void k_prep_sigg1_var_wide(size_t n, int q, con
     }
     Jac<pl::Fp2> acc = pl::jl_to_pl(la);
     Aff<pl::Fp2> a;
-    if (!jac_to_aff(a, acc)) fl |= 4u;
+    if (!wide::jac_to_aff(a, acc)) fl |= 4u;  // every pair the same point: the quad-form inversion
     if (p == 0) {
         pl::st_f2(S, S_Q1, i, a.x);
         pl::st_f2(S, S_Q1 + 2, i, a.y);
