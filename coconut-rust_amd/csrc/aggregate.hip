@@ -825,14 +825,31 @@ __global__ __launch_bounds__(128) void k_prep_pok_wide_sigg2(size_t n, int q, in
             __shared__ uint32_t tabl[15][LW];  // d J, d = 1..15 (every lane holds the same point)
             const lz::AG Jl{lz::fit<lz::AN, lz::BC>(lz::reduce(lz::in_r(Ja.x))), lz::fit<lz::AN, lz::BC>(lz::reduce(lz::in_r(Ja.y)))};
             lz::JG t = lz::wide::jg_add_aff(lz::jg_inf(), Jl);
-#pragma unroll 1
-            for (int d = 1; d <= 15; d++) {
-                if (d > 1) t = lz::wide::jg_add_aff(t, Jl);
+            const int grp = l / lz::wide::G, mem = l & (lz::wide::G - 1);
+            auto ld_tab = [&](int d) {
+                lz::JG v;
+                uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+                for (int w = 0; w < LW; w++) vw[w] = tabl[d - 1][w];
+                return v;
+            };
+            if (l == 0) {
                 const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
-                if (l == 0)
-                    for (int w = 0; w < LW; w++) tabl[d - 1][w] = tw[w];
+                for (int w = 0; w < LW; w++) tabl[0][w] = tw[w];
             }
             __builtin_amdgcn_wave_barrier();
+            // d J, d = 2..15, as a tree: level s forms d = s + 1 .. 2s as (s J) + ((d - s) J), one multiple
+            // a lane group (2s J through the addition's P = Q branch): 4 levels instead of 14 additions
+#pragma unroll 1
+            for (int s = 1; s <= 8; s <<= 1) {
+                const int d = s + 1 + grp;
+                const bool mine = grp < s && d <= 15;
+                const lz::JG r = lz::wide::jg_add(ld_tab(s), ld_tab(mine ? d - s : 1));
+                if (mine && mem == 0) {
+                    const uint32_t* rw = reinterpret_cast<const uint32_t*>(&r);
+                    for (int w = 0; w < LW; w++) tabl[d - 1][w] = rw[w];
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
             lz::JG sacc = lz::jg_inf();
 #pragma unroll 1
             for (int win = 63; win >= 0; win--) {
@@ -971,14 +988,30 @@ __global__ __launch_bounds__(128) void k_prep_pok_wide_sigg1(size_t n, int q, in
             __shared__ uint32_t tabl[15][2][LW];  // d J, d = 1..15, by half (every pair holds the same point)
             const lz::AL Jl{lz::reduce(lz::in_r2(Ja.x)), lz::reduce(lz::in_r2(Ja.y))};
             lz::JL t = lz::jl_from_aff(Jl);
-#pragma unroll 1
-            for (int d = 1; d <= 15; d++) {
-                if (d > 1) t = lz::wide::jl_add_aff(t, Jl);
+            const int grp = p / lz::wide::G, mem = p & (lz::wide::G - 1);
+            auto ld_tab = [&](int d) {
+                lz::JL v;
+                uint32_t* vw = reinterpret_cast<uint32_t*>(&v);
+                for (int w = 0; w < LW; w++) vw[w] = tabl[d - 1][h][w];
+                return v;
+            };
+            if (l < 2) {
                 const uint32_t* tw = reinterpret_cast<const uint32_t*>(&t);
-                if (l < 2)
-                    for (int w = 0; w < LW; w++) tabl[d - 1][h][w] = tw[w];
+                for (int w = 0; w < LW; w++) tabl[0][h][w] = tw[w];
             }
             __builtin_amdgcn_wave_barrier();
+            // d J, d = 2..15, as a tree (8 lane-pair groups), as in k_prep_pok_wide_sigg2
+#pragma unroll 1
+            for (int s = 1; s <= 8; s <<= 1) {
+                const int d = s + 1 + grp;
+                const bool mine = grp < s && d <= 15;
+                const lz::JL r = lz::wide::jl_add(ld_tab(s), ld_tab(mine ? d - s : 1));
+                if (mine && mem == 0) {
+                    const uint32_t* rw = reinterpret_cast<const uint32_t*>(&r);
+                    for (int w = 0; w < LW; w++) tabl[d - 1][h][w] = rw[w];
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
 #pragma unroll 1
             for (int win = 63; win >= 0; win--) {
                 for (int b = 0; b < 4; b++) sacc = lz::wide::jl_dbl(sacc);
