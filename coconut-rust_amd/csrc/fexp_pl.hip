@@ -1089,6 +1089,177 @@ __global__ __launch_bounds__(64, 1) void k_miller_wide(size_t n, const uint32_t*
     if (threadIdx.x < 2) st_f12(Soa{fout, fstride}, foff + i, f);
 }
 
+// The same loop on TWO waves a pair, for launches of up to kWide2Max pairs (fewer waves than the chip
+// has SIMDs, so the second wave is free): wave 1 walks T's chain (its A / B levels, the addition's four)
+// and leaves each iteration's evaluated lines in LDS; wave 0 squares f and multiplies it by them one
+// iteration behind.  A block barrier per iteration hands the lines over (two LDS slots).  Wave 0's
+// iteration is then its two or three Fp12 operations alone (no T products or glue in its levels).
+constexpr size_t kWide2Max = 256;
+__global__ __launch_bounds__(128, 1) void k_miller_wide2(size_t n, const uint32_t* __restrict__ prep,
+                                                      const uint32_t* __restrict__ flags, uint32_t* __restrict__ fout,
+                                                      size_t fstride, size_t foff) {
+    const size_t i = blockIdx.x;
+    if (i >= n) return;  // block-uniform
+    const bool twave = threadIdx.x >= 64;  // wave-uniform
+    const int j = (int)((threadIdx.x & 63) >> 1), h = (int)(threadIdx.x & 1);
+    __shared__ uint32_t lbuf[2][2][3][2][NL];  // [slot][doubling / addition line][coefficient][half][word]
+    const Soa S{const_cast<uint32_t*>(prep), n};
+    Fp12 f;
+    f12_one(f);
+    if (!(flags[i] & 5u)) {  // block-uniform
+        if (twave) {
+            Aff<Fp2> Q;
+            ld_f2(Q.x, S, S_Q1, i);
+            ld_f2(Q.y, S, S_Q1 + 2, i);
+            Fp px, py, pz;
+            cc::ld_fp(px, S, S_P1, i);
+            cc::ld_fp(py, S, S_P1 + 1, i);
+            cc::ld_fp(pz, S, S_P1 + 2, i);
+            const Fp2 PX = f2_of_fp(px), PY = f2_of_fp(py), PZ = f2_of_fp(pz);
+            G2Proj T;
+            T.x = Q.x;
+            T.y = Q.y;
+            f2_one(T.z);
+            auto put = [&](int slot, int which, const Fp2& x0, const Fp2& x2, const Fp2& x3) {
+                if (j == 0) {
+#pragma unroll
+                    for (int w = 0; w < NL; w++) {
+                        lbuf[slot][which][0][h][w] = x0.c.v[w];
+                        lbuf[slot][which][1][h][w] = x2.c.v[w];
+                        lbuf[slot][which][2][h][w] = x3.c.v[w];
+                    }
+                }
+            };
+#pragma unroll 1
+            for (int k = 0; k <= 63; k++) {
+                if (k <= 62) {
+                    const int b = 62 - k;
+                    Fp2 o1, o2, pr, l0, l2c, l3c;
+                    {  // A: X Y, Y^2, Z^2, (Y + Z)^2, X^2
+                        Fp2 yz;
+                        f2_add_lz(yz, T.y, T.z);
+                        const Fp2 a1[5] = {T.x, T.y, T.z, yz, T.x}, a2[5] = {T.y, T.y, T.z, yz, T.x};
+                        o1 = a1[0];
+                        o2 = a2[0];
+                        pick2(o1, o2, j, a1, a2, 5);
+                        f2_mul(pr, o1, o2);
+                    }
+                    Fp2 a = bcast_f2(pr, 0), bb = bcast_f2(pr, 1), c = bcast_f2(pr, 2), hh = bcast_f2(pr, 3),
+                        t = bcast_f2(pr, 4), e, ff, g;
+                    f2_half(a, a);
+                    f2_sub(hh, hh, bb);
+                    f2_sub(hh, hh, c);
+                    f2_mul_xi(e, c);
+                    f2_mul12(e, e);  // e = 3 b' Z^2
+                    f2_dbl(ff, e);
+                    f2_add(ff, ff, e);
+                    f2_add(g, bb, ff);
+                    f2_half(g, g);
+                    f2_sub(l0, e, bb);
+                    f2_dbl(l2c, t);
+                    f2_add(l2c, l2c, t);
+                    f2_neg(l3c, hh);
+                    {  // B: T's a (b - 3e), e^2, g^2, b h and the line's evaluation at P
+                        Fp2 bmf;
+                        f2_sub(bmf, bb, ff);
+                        const Fp2 a1[7] = {a, e, g, bb, l0, l2c, l3c}, a2[7] = {bmf, e, g, hh, PZ, PX, PY};
+                        o1 = a1[0];
+                        o2 = a2[0];
+                        pick2(o1, o2, j, a1, a2, 7);
+                        f2_mul(pr, o1, o2);
+                    }
+                    T.x = bcast_f2(pr, 0);
+                    {
+                        const Fp2 e2 = bcast_f2(pr, 1);
+                        T.y = bcast_f2(pr, 2);
+                        f2_sub(T.y, T.y, e2);
+                        f2_sub(T.y, T.y, e2);
+                        f2_sub(T.y, T.y, e2);
+                    }
+                    T.z = bcast_f2(pr, 3);
+                    put(b & 1, 0, bcast_f2(pr, 4), bcast_f2(pr, 5), bcast_f2(pr, 6));
+                    if ((X_ABS >> b) & 1ull) {  // addition step (pairing.inc line_add)
+                        Fp2 theta, lambda;
+                        {
+                            const Fp2 a1[2] = {Q.y, Q.x}, a2[2] = {T.z, T.z};
+                            o1 = a1[0];
+                            o2 = a2[0];
+                            pick2(o1, o2, j, a1, a2, 2);
+                            f2_mul(pr, o1, o2);
+                            f2_sub(theta, T.y, bcast_f2(pr, 0));
+                            f2_sub(lambda, T.x, bcast_f2(pr, 1));
+                        }
+                        {
+                            const Fp2 a1[4] = {theta, lambda, theta, lambda}, a2[4] = {theta, lambda, Q.x, Q.y};
+                            o1 = a1[0];
+                            o2 = a2[0];
+                            pick2(o1, o2, j, a1, a2, 4);
+                            f2_mul(pr, o1, o2);
+                        }
+                        c = bcast_f2(pr, 0);
+                        const Fp2 d = bcast_f2(pr, 1);
+                        f2_sub(l0, bcast_f2(pr, 2), bcast_f2(pr, 3));
+                        f2_neg(l2c, theta);
+                        l3c = lambda;
+                        {
+                            const Fp2 a1[6] = {lambda, T.z, T.x, l0, l2c, l3c}, a2[6] = {d, c, d, PZ, PX, PY};
+                            o1 = a1[0];
+                            o2 = a2[0];
+                            pick2(o1, o2, j, a1, a2, 6);
+                            f2_mul(pr, o1, o2);
+                        }
+                        e = bcast_f2(pr, 0);
+                        ff = bcast_f2(pr, 1);
+                        g = bcast_f2(pr, 2);
+                        put(b & 1, 1, bcast_f2(pr, 3), bcast_f2(pr, 4), bcast_f2(pr, 5));
+                        f2_add(hh, e, ff);
+                        f2_sub(hh, hh, g);
+                        f2_sub(hh, hh, g);
+                        {
+                            Fp2 gmh;
+                            f2_sub(gmh, g, hh);
+                            const Fp2 a1[4] = {lambda, theta, e, T.z}, a2[4] = {hh, gmh, T.y, e};
+                            o1 = a1[0];
+                            o2 = a2[0];
+                            pick2(o1, o2, j, a1, a2, 4);
+                            f2_mul(pr, o1, o2);
+                            T.x = bcast_f2(pr, 0);
+                            f2_sub(T.y, bcast_f2(pr, 1), bcast_f2(pr, 2));
+                            T.z = bcast_f2(pr, 3);
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        } else {
+            auto get = [&](int slot, int which) {
+                Fp12 L;
+                Fp2 x0, x2, x3;
+#pragma unroll
+                for (int w = 0; w < NL; w++) {
+                    x0.c.v[w] = lbuf[slot][which][0][h][w];
+                    x2.c.v[w] = lbuf[slot][which][1][h][w];
+                    x3.c.v[w] = lbuf[slot][which][2][h][w];
+                }
+                line_fp12(L, x0, x2, x3);
+                return L;
+            };
+#pragma unroll 1
+            for (int k = 0; k <= 63; k++) {
+                if (k >= 1) {  // iteration b = 63 - k, its lines written in round k - 1
+                    const int b = 63 - k;
+                    f12_mul_wide(f, f, f);
+                    f12_mul_wide(f, f, get(b & 1, 0));
+                    if ((X_ABS >> b) & 1ull) f12_mul_wide(f, f, get(b & 1, 1));
+                }
+                __syncthreads();
+            }
+            f12_conj(f, f);
+        }
+    }
+    if (threadIdx.x < 2) st_f12(Soa{fout, fstride}, foff + i, f);
+}
+
 // ================================================================ small batches: one wave per pair
 // A batch of n credentials fills 2n lanes of the pair-lane Miller kernel (k_miller): for small n that is
 // a handful of waves, each the latency of a 2-pair loop on one lane pair (~7.5 ms alone on its SIMD,
@@ -1228,7 +1399,11 @@ extern "C" int cck_miller_wide(size_t n, const uint32_t* d_prep, const uint32_t*
                                size_t fstride, size_t foff, hipStream_t st) {
     if (!n) return 0;
     if (fstride < foff + n) return -1;
-    hipLaunchKernelGGL(cc::pl::k_miller_wide, dim3((unsigned)n), dim3(64), 0, st, n, d_prep, d_flags, d_f, fstride,
-                       foff);
+    if (n <= cc::pl::kWide2Max)  // fewer pairs than SIMDs: a second wave a pair takes T's chain
+        hipLaunchKernelGGL(cc::pl::k_miller_wide2, dim3((unsigned)n), dim3(128), 0, st, n, d_prep, d_flags, d_f, fstride,
+                           foff);
+    else
+        hipLaunchKernelGGL(cc::pl::k_miller_wide, dim3((unsigned)n), dim3(64), 0, st, n, d_prep, d_flags, d_f, fstride,
+                           foff);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
