@@ -498,16 +498,20 @@ def kernel_table(phase_ms, n, counts, in_bytes_per_cred, peak, prep_kernel="k_pr
             row["input_GB_s"] = round(n * in_bytes_per_cred / (ms * 1e-3) / 1e9, 2)
         # the batch kernels by exact name stem: the small-batch paths' k_miller_wide / k_fexp1 (the latency
         # legs) appear in the same profiles
-        row.update(pmc({"prep": prep_kernel + "(", "miller": "lz::k_miller<", "fexp": "lz::k_fexp_q("}[k], mode))
+        mk = "lz::k_miller<1, false>" if mode and mode.endswith("g1") else "lz::k_miller<2, false>"
+        row.update(pmc({"prep": prep_kernel + "(", "miller": mk, "fexp": "lz::k_fexp_q("}[k], mode))
         out[k] = row
     return out
 
 
-def bench_verify(args, mode):
+def bench_verify(args, mode, sub=None):
+    """sub: None for a mode's own line; else (world, rank, local, dist) of the running headline, and this
+    call is its same-run SigG1 leg: the same workload, batches in flight and verdict check, returned as a
+    compact dict (no PCIe / default-table / latency / CPU legs) for the line's `sigg1` object."""
     import numpy as np
     import torch
     import coconut
-    world, rank, local, dist = _dist_setup()
+    world, rank, local, dist = sub if sub else _dist_setup()
     dev = torch.device("cuda", local)
     n, q = args.n or 65536, 6
     ctx = coconut.Context(local, coconut.GroupMode(mode))
@@ -515,7 +519,7 @@ def bench_verify(args, mode):
     batch = make_verify_batch(ctx, mode, n, q, seed=1000 + rank + 100 * mode)
     ctx.set_params(batch["g_tilde"])
     t_vk = time.perf_counter()
-    ctx.set_table_bits(vk_bits_for(args), 0)
+    ctx.set_table_bits(args.vk_bits if args.vk_bits is not None else BENCH_VK_BITS["verify" if mode == 0 else "verify-g1"], 0)
     ctx.set_verkey(batch["X"], batch["Y"])
     vk_ms = (time.perf_counter() - t_vk) * 1e3
     # --inflight K: K batches in flight on ONE context (cc_set_concurrency: K workspace slots, one set of
@@ -585,6 +589,16 @@ def bench_verify(args, mode):
     elapsed = _max_over_ranks(elapsed, dist, dev)
     value = n * world * args.steps / elapsed
     opt_in = table_config(ctx, q)
+    if sub:
+        kt = kernel_table(phase / max(args.steps, 1), n, opcounts("verify_sigg1_q6_shared_vk"), 97 * 2 + q * 48,
+                          peak_mad_per_s(), "k_prep_sigg1_pair", "verify-g1")
+        ctx.close()
+        return {"layout": "SigG1 (BASELINE config 2 wording: 'G2 MSM + 2-pairing check': verkey MSM in G2, "
+                          "sigma in G1)",
+                "value": round(value, 1), "unit": "credentials/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+                "steps": args.steps, "warmup": args.warmup, "batches_in_flight": K, "credentials_per_gpu": n,
+                "verdicts_checked": "against construction (1/16 corrupted), every slot", **opt_in,
+                "kernels": kt, "rocprof_kernels": kernel_pmc_report("verify-g1")}
     # PCIe-inclusive rate: the host-buffer entry point (H2D of the serialized batch + D2H of verdicts);
     # --no-pcie skips it (profiling runs: then every launch of the trace is a warmup or a timed step)
     pcie_rate = None
@@ -610,6 +624,13 @@ def bench_verify(args, mode):
     dflt["batches_in_flight"] = K
     dflt.update(table_config(ctx, q))
     latency = latency_leg(ctx, d_s1, d_s2, d_m, q, batch["expect"], dev)
+    sigg1 = None
+    if mode == 0 and not args.no_sigg1:  # BASELINE config 2's own wording, same run, same K
+        ctx.close()
+        ctx = None
+        del d_s1, d_s2, d_m, d_vs, d_v
+        torch.cuda.empty_cache()
+        sigg1 = bench_verify(args, 1, sub=(world, rank, local, dist))
     if rank == 0:
         key = "verify_sigg2_q6_shared_vk" if mode == 0 else "verify_sigg1_q6_shared_vk"
         counts = opcounts(key)
@@ -658,12 +679,15 @@ def bench_verify(args, mode):
             "setup": {"verkey_tables_ms": round(vk_ms, 1), "verkey_table_bits": opt_in["verkey_table_bits"],
                       "synthetic_data_s": round(setup_s, 2)},
         }
+        if sigg1:
+            out["sigg1"] = sigg1
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline_verify(batch, value)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
 
 
 def bench_rlc(args):
@@ -858,6 +882,8 @@ def main():
                          "library's <= 16 GiB choice; default: bench_modes.BENCH_ISS_BITS = 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the host-buffer (PCIe-inclusive) rate")
+    ap.add_argument("--no-sigg1", action="store_true",
+                    help="default verify line: skip its same-run SigG1 leg (the `sigg1` object)")
     ap.add_argument("--vk-bits", type=int, default=None,
                     help="verkey table window width (cc_set_table_bits; 0 = the library's <= 4 GiB default; "
                          "unset = the mode's opt-in width, BENCH_VK_BITS)")

@@ -15,6 +15,7 @@
 
 #include "../../include/coconut_hip.h"
 #include "rlc_part.h"
+#include "slots.h"
 
 extern "C" {
 int cck_decode_points(int group, size_t n, const uint8_t* d_bytes, uint32_t* d_out, uint32_t* d_inf, hipStream_t st);
@@ -117,7 +118,7 @@ static size_t free_hbm() {
     }
     return fr;
 }
-constexpr int PREP_SLOTS = 14;  // soa.h
+constexpr size_t PREP_SLOTS = cc::slots::kPrepSlots;  // soa.h
 // default HBM budget of a context's shared-verkey tables (wider: cc_set_table_bits)
 constexpr double kVkTableBudget = 4.0 * (double)(1ull << 30);
 
@@ -144,17 +145,67 @@ struct DevBuf {
     }
 };
 
-// One in-flight verify batch's workspaces (cc_set_concurrency): the prep SoA, flags, Miller values and
-// the per-credential-verkey MSM scratch; `done` marks the end of the slot's last batch on its stream.
-struct VerifySlot {
-    DevBuf prep, flags, fbuf, vkb, scratch, idx;  // scratch, idx: PoK (the d J tables, the revealed indices)
-    DevBuf wprep, wflags, wf;                     // small batches' one-wave-per-pair Miller path
-    DevBuf rkey, rany, rpts, rdig, rwork;         // RLC partial: delta key, flag, fold points, digits, fold
-    hipEvent_t done = nullptr;
-    bool recorded = false;
+// The device policy of the slot bookkeeping (slots.h): hipMalloc'd buffers, HIP events and streams.
+struct HipDev {
+    using Buf = DevBuf;
+    using Event = hipEvent_t;
+    using Stream = hipStream_t;
+    int ensure(DevBuf& b, size_t n) { return b.ensure(n); }
+    int sync(hipEvent_t e) { return hipEventSynchronize(e) == hipSuccess ? 0 : -1; }
+    int record(hipEvent_t e, hipStream_t s) { return hipEventRecord(e, s) == hipSuccess ? 0 : -1; }
+    int wait(hipStream_t s, hipEvent_t e) { return hipStreamWaitEvent(s, e, 0) == hipSuccess ? 0 : -1; }
+};
+using VerifyWork = cc::slots::Work<DevBuf>;
+using VerifySlot = cc::slots::SlotBufs<DevBuf>;  // slots 1 .. K-1 (slot 0: the context's workspaces)
+using SlotPool = cc::slots::Pool<HipDev>;
+using SlotFence = cc::slots::Fence<HipDev>;
+
+// Pinned host staging for the few bytes a slot's batch uploads per call (the RLC delta seed, the PoK
+// revealed indices): a copy from pageable memory may hold the host until the stream reaches it, i.e.
+// until the slot's previous batch has run, which would serialize the in-flight batches.  A ring of kR
+// entries, each reused only after its own copy (kR calls earlier on this slot) has completed.
+struct Staging {
+    static constexpr int kR = 4;
+    uint8_t* host = nullptr;
+    size_t bytes = 0;  // per entry
+    hipEvent_t ev[kR] = {};
+    bool used[kR] = {};
+    int next = 0;
+    // copies len bytes of src to d_dst on st through the next entry
+    int upload(void* d_dst, const void* src, size_t len, hipStream_t st) {
+        if (!len) return 0;
+        if (len > bytes) {
+            for (int e = 0; e < kR; e++)
+                if (used[e] && hipEventSynchronize(ev[e]) != hipSuccess) return -1;
+            if (host) (void)hipHostFree(host);
+            host = nullptr;
+            bytes = 0;
+            const size_t want = (len + 63) & ~(size_t)63;
+            if (hipHostMalloc((void**)&host, want * kR, hipHostMallocDefault) != hipSuccess) return -1;
+            bytes = want;
+            for (int e = 0; e < kR; e++) used[e] = false;
+        }
+        const int e = next;
+        next = (next + 1) % kR;
+        if (!ev[e] && hipEventCreateWithFlags(&ev[e], hipEventDisableTiming) != hipSuccess) return -1;
+        if (used[e] && hipEventSynchronize(ev[e]) != hipSuccess) return -1;  // its copy kR calls ago
+        uint8_t* h = host + (size_t)e * bytes;
+        memcpy(h, src, len);
+        if (hipMemcpyAsync(d_dst, h, len, hipMemcpyHostToDevice, st) != hipSuccess) return -1;
+        if (hipEventRecord(ev[e], st) != hipSuccess) return -1;
+        used[e] = true;
+        return 0;
+    }
     void release() {
-        for (DevBuf* b : {&prep, &flags, &fbuf, &vkb, &scratch, &idx, &wprep, &wflags, &wf, &rkey, &rany, &rpts, &rdig, &rwork})
-            b->release();
+        for (int e = 0; e < kR; e++) {
+            if (used[e]) (void)hipEventSynchronize(ev[e]);
+            if (ev[e]) (void)hipEventDestroy(ev[e]);
+            ev[e] = nullptr;
+            used[e] = false;
+        }
+        if (host) (void)hipHostFree(host);
+        host = nullptr;
+        bytes = 0;
     }
 };
 
@@ -225,14 +276,17 @@ struct cc_ctx {
     std::vector<ncclComm_t> comms;
     DevBuf rlc_gath;  // per peer: gathered partials (ndev x RLC_PART_WORDS words)
     // concurrent verify batches (cc_set_concurrency): with K > 1 slots, cc_verify_batch_device /
-    // cc_verify_batch_pervk_device calls take the slots round-robin and are ordered only after the
-    // context's earlier work (tables, params) and the same slot's previous batch, so K batches on K
-    // caller streams overlap.  Slot 0 is the context's own prep / flags / fbuf / vkb; vslots holds
-    // slots 1 .. K-1.  Every other entry point first waits for every slot's last batch.
+    // cc_verify_batch_pervk_device / cc_pok_verify_batch_device / cc_rlc_partial_device calls take the
+    // slots round-robin and are ordered only after the context's earlier work (tables, params) and the
+    // same slot's previous batch, so K batches on K caller streams overlap (slots.h).  pool.recs[0] is
+    // the context's own workspaces (prep / flags / fbuf / vkb / scratch / pok_idx / wide_*); vslots
+    // holds the buffers of slots 1 .. K-1; stage[k] slot k's pinned upload ring.  Every other entry point
+    // first waits for every slot's last batch.
     int concurrency = 1;
-    int vslot_next = 0;
-    VerifySlot slot0;  // only its event fields: the buffers are the context's
+    HipDev dev;
+    SlotPool pool;
     std::vector<VerifySlot*> vslots;
+    std::vector<Staging> stage;
 };
 
 // Every *_device entry point may run on a caller stream while the context's workspaces (prep, flags,
@@ -241,18 +295,10 @@ struct cc_ctx {
 // at entry, and c->stream wait for the call's work at exit, so calls on any mix of streams touch the
 // workspaces in program order (two device calls on different streams are chained through c->stream).
 // stream st waits (on the device) for every concurrent verify slot's last batch
-static void wait_slots(cc_ctx* c, hipStream_t st) {
-    if (c->slot0.recorded) (void)hipStreamWaitEvent(st, c->slot0.done, 0);
-    for (VerifySlot* v : c->vslots)
-        if (v->recorded) (void)hipStreamWaitEvent(st, v->done, 0);
-}
+static void wait_slots(cc_ctx* c, hipStream_t st) { c->pool.wait_all(c->dev, st); }
 // the host waits for every concurrent verify slot's last batch (before buffers a slot may still read
 // are freed or rebuilt: tables, params, workspaces)
-static void drain_slots(cc_ctx* c) {
-    if (c->slot0.recorded) (void)hipEventSynchronize(c->slot0.done);
-    for (VerifySlot* v : c->vslots)
-        if (v->recorded) (void)hipEventSynchronize(v->done);
-}
+static void drain_slots(cc_ctx* c) { c->pool.drain(c->dev); }
 
 struct StreamOrder {
     cc_ctx* c;
@@ -295,6 +341,12 @@ static inline int oth_bytes(int mode) { return mode == 0 ? 97 : 192; }
 static inline int oth_group(int mode) { return mode == 0 ? 1 : 2; }
 static inline int sig_group(int mode) { return mode == 0 ? 2 : 1; }
 static inline size_t aff_words(int group) { return group == 1 ? 24 : 48; }
+
+// the context's own workspaces: concurrency slot 0, and every single-slot entry point
+static VerifyWork ctx_work(cc_ctx* c) {
+    return VerifyWork(&c->prep, &c->flags, &c->fbuf, &c->vkb, &c->scratch, &c->pok_idx, &c->wide_prep, &c->wide_flags,
+                      &c->wide_f);
+}
 
 static inline cc_ctx* primary(cc_ctx* c) { return c && !c->peers.empty() ? c->peers[0] : c; }
 static inline const cc_ctx* primary(const cc_ctx* c) { return c && !c->peers.empty() ? c->peers[0] : c; }
@@ -357,6 +409,9 @@ cc_status cc_ctx_create(int device, cc_group_mode mode, cc_ctx** out) {
         (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
         if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, hi) != hipSuccess) c->side = nullptr;
     }
+    c->pool.recs.resize(1);
+    c->pool.recs[0].w = ctx_work(c);  // slot 0: the context's own workspaces
+    c->stage.resize(1);
     *out = c;
     return CC_OK;
 }
@@ -376,12 +431,14 @@ cc_status cc_ctx_destroy(cc_ctx* c) {
     drain_slots(c);
     (void)hipStreamSynchronize(c->stream);
     for (VerifySlot* v : c->vslots) {
-        v->release();
-        if (v->done) (void)hipEventDestroy(v->done);
+        v->each([](DevBuf& b) { b.release(); });
         delete v;
     }
     c->vslots.clear();
-    if (c->slot0.done) (void)hipEventDestroy(c->slot0.done);
+    for (auto& r : c->pool.recs)
+        if (r.done) (void)hipEventDestroy(r.done);
+    c->pool.recs.clear();
+    for (Staging& g : c->stage) g.release();
     DevBuf* bufs[] = {&c->gtilde_aff, &c->gtilde_lines, &c->gtilde_lz, &c->vk_aff, &c->vk_inf, &c->table, &c->table_inf,
                       &c->in_s1, &c->in_s2, &c->in_msgs, &c->in_vkX, &c->in_vkY, &c->prep, &c->flags,
                       &c->fbuf, &c->scratch, &c->verdicts, &c->gt, &c->vkb, &c->lag, &c->wide_prep, &c->wide_flags, &c->wide_f,
@@ -662,49 +719,29 @@ cc_status cc_table_bits(const cc_ctx* c, int* verkey_bits, int* issuer_bits) {
 // under the quad kernel's floor at 2,048).  The shared-verkey prep takes its one-wave form up to
 // kFexpWideMax, the PoK and per-credential-verkey preps up to kPrepWideMax.  Measured:
 // profiles/r05/wide_spread, thresholds, miller_wide_pipe, fexp_thr.
-constexpr size_t kWideMax = 4096;
-constexpr size_t kFexpWideMax = 2048;
-constexpr size_t kPrepWideMax = 1024;
-static bool wide_short(DevBuf& p, DevBuf& f, DevBuf& v, size_t n) {
-    const size_t m = 2 * n, words = m * 12;
-    return n <= kWideMax && (p.bytes < words * 4 * PREP_SLOTS || f.bytes < m * 4 || v.bytes < words * 4 * 12);
-}
-static int wide_ensure(DevBuf& p, DevBuf& f, DevBuf& v, size_t n) {
-    if (n > kWideMax) return 0;
-    const size_t m = 2 * n, words = m * 12;
-    return p.ensure(words * 4 * PREP_SLOTS) || f.ensure(m * 4) || v.ensure(words * 4 * 12) ? -1 : 0;
-}
-
+// (the thresholds live in slots.h with the workspace sizes they decide; k_miller_wide2, two waves a
+// pair, takes launches of <= kWide2Max = 256 pairs, i.e. <= 128 credentials: fexp_pl.hip)
+using cc::slots::kFexpWideMax;
+using cc::slots::kPrepWideMax;
+using cc::slots::kWideMax;
+// the context's own workspaces (slot 0) grown to n credentials; scratch: the PoK prep's per-proof table
+// of d J (15 Jacobian points, <= 15 x 84 words: SigG1's lazy G2 points), and the one-wave fexp's
+// (fexp_pl.hip k_fexp1: 72 slots of 12 words an element); the batched fexp (fexp_q.hip) keeps its chain
+// in registers
 static cc_status ensure_work(cc_ctx* c, size_t n) {
-    size_t words = n * 12;  // one Fp slot
-    if (c->prep.bytes < words * 4 * PREP_SLOTS || c->flags.bytes < n * 4 || c->fbuf.bytes < words * 4 * 12 ||
-        c->scratch.bytes < (n * 15 * 84 + 72 * 12) * 4 || c->verdicts.bytes < n ||
-        wide_short(c->wide_prep, c->wide_flags, c->wide_f, n))
+    const cc::slots::Sizes sz = cc::slots::verify_sizes(n, 0, (n * 15 * 84 + 72 * 12) * 4, 0);
+    const VerifyWork w = ctx_work(c);
+    if (w.short_of(sz) || c->verdicts.bytes < n)
         drain_slots(c);  // a concurrent batch may still read the buffers about to be reallocated
-    if (wide_ensure(c->wide_prep, c->wide_flags, c->wide_f, n)) return CC_ERR_HIP;
-    // scratch: the PoK prep's per-proof table of d J (15 Jacobian points, <= 15 x 84 words: SigG1's lazy
-    // G2 points), and the one-wave fexp's (fexp_pl.hip k_fexp1: 72 slots of 12 words an element); the batched
-    // fexp (fexp_q.hip) keeps its chain in registers
-    if (c->prep.ensure(words * 4 * PREP_SLOTS) || c->flags.ensure(n * 4) || c->fbuf.ensure(words * 4 * 12) ||
-        c->scratch.ensure((n * 15 * 84 + 72 * 12) * 4) || c->verdicts.ensure(n))
-        return CC_ERR_HIP;
+    for (int j = 0; j < VerifyWork::kN; j++)
+        if (w.at(j)->ensure(sz.at(j))) return CC_ERR_HIP;
+    if (c->verdicts.ensure(n)) return CC_ERR_HIP;
     return CC_OK;
 }
 
-// the three verify launches on device buffers; timing per phase when enabled.  d_vkX == NULL: the
-// shared verkey's tables; else one verkey per credential (d_vkX n x OtherGroup, d_vkY n x q x
-// OtherGroup; the Straus MSM of pervk.hip, its scratch in c->vkb, sized by the caller)
-struct VerifyWork {
-    DevBuf *prep = nullptr, *flags = nullptr, *fbuf = nullptr, *vkb = nullptr, *scratch = nullptr, *idx = nullptr;
-    DevBuf *wprep = nullptr, *wflags = nullptr, *wf = nullptr;  // the small-batch Miller path's
-    VerifyWork() = default;
-    // every workspace named: a partial list does not compile (a missing one would be a null pointer)
-    VerifyWork(DevBuf* p, DevBuf* f, DevBuf* fb, DevBuf* v, DevBuf* s, DevBuf* i, DevBuf* wp, DevBuf* wfl, DevBuf* wv)
-        : prep(p), flags(f), fbuf(fb), vkb(v), scratch(s), idx(i), wprep(wp), wflags(wfl), wf(wv) {}
-};
-static VerifyWork ctx_work(cc_ctx* c) {
-    return {&c->prep, &c->flags, &c->fbuf, &c->vkb, &c->scratch, &c->pok_idx, &c->wide_prep, &c->wide_flags, &c->wide_f};
-}
+// the three verify launches on device buffers (VerifyWork, slots.h); timing per phase when enabled.
+// d_vkX == NULL: the shared verkey's tables; else one verkey per credential (d_vkX n x OtherGroup, d_vkY
+// n x q x OtherGroup; the Straus MSM of pervk.hip, its scratch in w.vkb, sized by the caller)
 // the batch's Miller values into w.fbuf (SoA stride n): n <= kWideMax one wave per pair, else the
 // pair-lane loop (one lane pair per credential, both pairs with a shared squaring)
 static cc_status launch_miller(cc_ctx* c, const VerifyWork& w, size_t n, hipStream_t st) {
@@ -749,39 +786,15 @@ static void collect_timing(cc_ctx* c) {
     for (int k = 0; k < 3; k++) (void)hipEventElapsedTime(&c->last_ms[k], c->ev[k], c->ev[k + 1]);
 }
 
-// The next concurrent slot (round-robin): its workspaces grown to n credentials (vkw bytes of per-verkey
-// MSM scratch, scratch_bytes of PoK tables, idx_bytes of revealed indices) once its last batch is done,
-// and stream st ordered after the context stream's queued work (tables, params, other entry points) and
-// after that last batch.  slot_end records the slot's completion on st.
-static cc_status slot_begin(cc_ctx* c, hipStream_t st, size_t n, size_t vkw, size_t scratch_bytes, size_t idx_bytes,
-                            VerifySlot*& sl, VerifyWork& w) {
-    const int k = c->vslot_next;
-    c->vslot_next = (k + 1) % c->concurrency;
-    sl = k ? c->vslots[k - 1] : &c->slot0;
-    w = k ? VerifyWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->vkb, &sl->scratch, &sl->idx, &sl->wprep, &sl->wflags, &sl->wf}
-          : ctx_work(c);
-    const size_t words = n * 12;
-    if (n <= kFexpWideMax && scratch_bytes < 72 * 12 * n * 4) scratch_bytes = 72 * 12 * n * 4;  // k_fexp1's chain
-    if (w.prep->bytes < words * 4 * PREP_SLOTS || w.flags->bytes < n * 4 || w.fbuf->bytes < words * 4 * 12 ||
-        w.vkb->bytes < vkw || w.scratch->bytes < scratch_bytes || w.idx->bytes < idx_bytes ||
-        wide_short(*w.wprep, *w.wflags, *w.wf, n)) {
-        if (sl->recorded) HIPCK(hipEventSynchronize(sl->done));  // the slot's last batch still reads them
-        if (w.prep->ensure(words * 4 * PREP_SLOTS) || w.flags->ensure(n * 4) || w.fbuf->ensure(words * 4 * 12) ||
-            (vkw && w.vkb->ensure(vkw)) || (scratch_bytes && w.scratch->ensure(scratch_bytes)) ||
-            (idx_bytes && w.idx->ensure(idx_bytes)) || wide_ensure(*w.wprep, *w.wflags, *w.wf, n))
-            return CC_ERR_HIP;
-    }
-    if (st != c->stream) {
-        HIPCK(hipEventRecord(c->ev_order, c->stream));
-        HIPCK(hipStreamWaitEvent(st, c->ev_order, 0));
-    }
-    if (sl->recorded) HIPCK(hipStreamWaitEvent(st, sl->done, 0));
-    return CC_OK;
-}
-static cc_status slot_end(hipStream_t st, VerifySlot* sl) {
-    HIPCK(hipEventRecord(sl->done, st));
-    sl->recorded = true;
-    return CC_OK;
+// The next concurrent slot (round-robin, slots.h Pool): its workspaces grown to the batch's sizes once
+// its last batch is done, and stream st ordered after the context stream's queued work (tables, params,
+// other entry points) and after that last batch.  The caller holds a SlotFence that records the slot's
+// completion on st on every exit.
+static cc_status slot_begin(cc_ctx* c, hipStream_t st, const cc::slots::Sizes& sz, int& k, VerifyWork& w) {
+    k = c->pool.take();
+    w = c->pool.recs[(size_t)k].w;
+    const int rc = c->pool.begin(c->dev, k, sz, st, c->stream, c->ev_order);
+    return rc == -2 ? CC_ERR_STATE : rc ? CC_ERR_HIP : CC_OK;
 }
 
 // the *_device verify calls: with one slot, ordered against everything on the context (StreamOrder);
@@ -792,18 +805,23 @@ static cc_status verify_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d_s
                                uint8_t* d_gt, hipStream_t st) {
     const size_t vkw = d_vkX ? cck_prep_var_words(c->mode, n, q) * 4 : 0;
     if (c->concurrency <= 1) {
+        cc_status s = ensure_work(c, n);
+        if (s) return s;
         if (d_vkX && c->vkb.bytes < vkw) drain_slots(c);  // slot 0's batch may still read it
         StreamOrder order(c, st);
         if (d_vkX && c->vkb.ensure(vkw)) return CC_ERR_HIP;
         return launch_verify(c, ctx_work(c), n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
     }
-    VerifySlot* sl = nullptr;
+    // the slot sizes its own workspaces (slot 0's too): no ensure_work, which would grow slot 0 for a
+    // batch landing on another slot and drain every slot in flight
+    int k = 0;
     VerifyWork w;
-    cc_status s = slot_begin(c, st, n, vkw, 0, 0, sl, w);
+    cc_status s = slot_begin(c, st, cc::slots::verify_sizes(n, vkw, 0, 0), k, w);
     if (s) return s;
+    SlotFence fence(c->pool, c->dev, k, st);
     s = launch_verify(c, w, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
     if (s) return s;
-    return slot_end(st, sl);
+    return fence.close() ? CC_ERR_HIP : CC_OK;
 }
 
 cc_status cc_set_concurrency(cc_ctx* c, int slots) {
@@ -818,24 +836,28 @@ cc_status cc_set_concurrency(cc_ctx* c, int slots) {
     }
     HIPCK(hipSetDevice(c->device));
     drain_slots(c);
-    if (!c->slot0.done) HIPCK(hipEventCreateWithFlags(&c->slot0.done, hipEventDisableTiming));
     while ((int)c->vslots.size() > slots - 1) {
         VerifySlot* v = c->vslots.back();
         c->vslots.pop_back();
-        v->release();
-        if (v->done) (void)hipEventDestroy(v->done);
+        v->each([](DevBuf& b) { b.release(); });
         delete v;
+        if (c->pool.recs.back().done) (void)hipEventDestroy(c->pool.recs.back().done);
+        c->pool.recs.pop_back();
+        c->stage.back().release();
+        c->stage.pop_back();
     }
+    if (!c->pool.recs[0].done) HIPCK(hipEventCreateWithFlags(&c->pool.recs[0].done, hipEventDisableTiming));
     while ((int)c->vslots.size() < slots - 1) {
+        SlotPool::Rec r;
+        if (hipEventCreateWithFlags(&r.done, hipEventDisableTiming) != hipSuccess) return CC_ERR_HIP;
         VerifySlot* v = new VerifySlot;
-        if (hipEventCreateWithFlags(&v->done, hipEventDisableTiming) != hipSuccess) {
-            delete v;
-            return CC_ERR_HIP;
-        }
+        r.w = v->work();
         c->vslots.push_back(v);
+        c->pool.recs.push_back(r);
+        c->stage.emplace_back();
     }
     c->concurrency = slots;
-    c->vslot_next = 0;
+    c->pool.next = 0;
     return CC_OK;
 }
 
@@ -853,10 +875,8 @@ cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d
     if (q != c->q) return CC_ERR_LEN;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
-    cc_status s = ensure_work(c, n);
-    if (s) return s;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    s = verify_device(c, n, q, d_s1, d_s2, d_msgs, nullptr, nullptr, d_verdicts, d_gt, st);
+    cc_status s = verify_device(c, n, q, d_s1, d_s2, d_msgs, nullptr, nullptr, d_verdicts, d_gt, st);
     if (s) return s;
     if (c->timing) collect_timing(c);
     return CC_OK;
@@ -871,10 +891,8 @@ cc_status cc_verify_batch_pervk_device(cc_ctx* c, size_t n, size_t q, const uint
     if (!c->have_params) return CC_ERR_STATE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
-    cc_status s = ensure_work(c, n);
-    if (s) return s;
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    s = verify_device(c, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
+    cc_status s = verify_device(c, n, q, d_s1, d_s2, d_msgs, d_vkX, d_vkY, d_verdicts, d_gt, st);
     if (s) return s;
     if (c->timing) collect_timing(c);
     return CC_OK;
@@ -899,7 +917,7 @@ static RlcWork ctx_rlc_work(cc_ctx* c) {
     return {&c->prep, &c->flags, &c->fbuf, &c->scratch, &c->rlc_key, &c->rlc_any, &c->rlc_pts, &c->rlc_dig, &c->rlc_work};
 }
 // sizes for n credentials; a concurrency slot whose buffers must grow waits for its last batch first
-static int rlc_ensure(cc_ctx* c, const RlcWork& r, size_t n, bool slot, VerifySlot* sl) {
+static int rlc_ensure(cc_ctx* c, const RlcWork& r, size_t n, SlotPool::Rec* sl) {
     const size_t PS = (n + 1) / 2, N = (n + 3) / 4;
     const size_t prep_b = (size_t)PREP_SLOTS * 12 * 4 * std::max(PS, n), flags_b = n * 4, fbuf_b = N * 144 * 4,
                  scr_b = ((N + 1) / 2) * 144 * 4 + n * 12 * 4 * 72, pts_b = n * 48 * 4, dig_b = 16 * n,
@@ -908,7 +926,7 @@ static int rlc_ensure(cc_ctx* c, const RlcWork& r, size_t n, bool slot, VerifySl
                       r.scratch->bytes < scr_b || r.key->bytes < 32 || r.any->bytes < 4 || r.pts->bytes < pts_b ||
                       r.dig->bytes < dig_b || r.work->bytes < work_b;
     if (!grow) return 0;
-    if (slot && sl && sl->recorded && hipEventSynchronize(sl->done) != hipSuccess) return -1;
+    if (sl && sl->recorded && hipEventSynchronize(sl->done) != hipSuccess) return -1;
     return r.prep->ensure(prep_b) || r.flags->ensure(flags_b) || r.fbuf->ensure(fbuf_b) || r.scratch->ensure(scr_b) ||
            r.key->ensure(32) || r.any->ensure(4) || r.pts->ensure(pts_b) || r.dig->ensure(dig_b) ||
            r.work->ensure(work_b);
@@ -916,11 +934,14 @@ static int rlc_ensure(cc_ctx* c, const RlcWork& r, size_t n, bool slot, VerifySl
 
 static cc_status launch_rlc_partial(cc_ctx* c, const RlcWork& w, size_t n, size_t q, uint64_t base_index,
                                     const uint8_t* seed32, const uint8_t* d_s1, const uint8_t* d_s2,
-                                    const uint8_t* d_msgs, uint32_t* d_partial, hipStream_t st) {
+                                    const uint8_t* d_msgs, uint32_t* d_partial, hipStream_t st, Staging* stage) {
     const size_t PS = (n + 1) / 2;  // prep SoA stride (the twin layout: credentials 2 t, 2 t + 1 at element t)
     const size_t N = (n + 3) / 4;   // Miller values (four credentials' pairs each, k_miller4)
-    // pageable source: the copy is staged before the call returns
-    HIPCK(hipMemcpyAsync(w.key->p, seed32, 32, hipMemcpyHostToDevice, st));
+    if (stage) {  // a concurrency slot: through its pinned ring, so the host does not wait for the stream
+        KCK(stage->upload(w.key->p, seed32, 32, st));
+    } else {  // pageable source: the copy is staged before the call returns
+        HIPCK(hipMemcpyAsync(w.key->p, seed32, 32, hipMemcpyHostToDevice, st));
+    }
     HIPCK(hipMemsetAsync(w.any->p, 0, 4, st));
     if (c->timing) (void)hipEventRecord(c->ev[0], st);
     auto prep_part = [&](int part) {
@@ -993,25 +1014,27 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
         return CC_OK;
     }
     if (c->concurrency > 1) {  // the next concurrency slot (cc_set_concurrency): its own workspaces
-        VerifySlot* sl = nullptr;
+        int k = 0;
         VerifyWork w;
-        cc_status s = slot_begin(c, st, n, 0, 0, 0, sl, w);
+        cc_status s = slot_begin(c, st, cc::slots::verify_sizes(n, 0, 0, 0), k, w);
         if (s) return s;
-        RlcWork r = sl == &c->slot0 ? ctx_rlc_work(c)
-                                    : RlcWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->scratch, &sl->rkey, &sl->rany,
-                                              &sl->rpts, &sl->rdig, &sl->rwork};
-        if (rlc_ensure(c, r, n, true, sl)) return CC_ERR_HIP;
-        s = launch_rlc_partial(c, r, n, q, base_index, seed32, d_s1, d_s2, d_msgs, d_partial, st);
+        SlotFence fence(c->pool, c->dev, k, st);
+        VerifySlot* sl = k ? c->vslots[(size_t)k - 1] : nullptr;
+        RlcWork r = sl ? RlcWork{&sl->prep, &sl->flags, &sl->fbuf, &sl->scratch, &sl->rkey, &sl->rany, &sl->rpts,
+                                 &sl->rdig, &sl->rwork}
+                       : ctx_rlc_work(c);
+        if (rlc_ensure(c, r, n, &c->pool.recs[(size_t)k])) return CC_ERR_HIP;
+        s = launch_rlc_partial(c, r, n, q, base_index, seed32, d_s1, d_s2, d_msgs, d_partial, st, &c->stage[(size_t)k]);
         if (s) return s;
-        return slot_end(st, sl);
+        return fence.close() ? CC_ERR_HIP : CC_OK;
     }
     drain_slots(c);  // concurrent batches (cc_set_concurrency) may still use the buffers sized below
     cc_status s = ensure_work(c, n);
     if (s) return s;
     RlcWork r = ctx_rlc_work(c);
-    if (rlc_ensure(c, r, n, false, nullptr)) return CC_ERR_HIP;
+    if (rlc_ensure(c, r, n, nullptr)) return CC_ERR_HIP;
     StreamOrder order(c, st);
-    return launch_rlc_partial(c, r, n, q, base_index, seed32, d_s1, d_s2, d_msgs, d_partial, st);
+    return launch_rlc_partial(c, r, n, q, base_index, seed32, d_s1, d_s2, d_msgs, d_partial, st, nullptr);
 }
 
 cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_partials, uint8_t* d_accept,
@@ -1715,16 +1738,16 @@ cc_status cc_pok_verify_batch_device(cc_ctx* c, size_t n, size_t q, size_t r, si
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     if (c->concurrency > 1) {  // the next concurrency slot (cc_set_concurrency): its own tables of d J
-        VerifySlot* sl = nullptr;
+        int k = 0;
         VerifyWork w;
-        s = slot_begin(c, st, n, 0, (n * 15 * 84 + 72 * 12) * 4, idx.size() * 4 + 4, sl, w);
+        s = slot_begin(c, st, cc::slots::verify_sizes(n, 0, (n * 15 * 84 + 72 * 12) * 4, idx.size() * 4 + 4), k, w);
         if (s) return s;
-        // pageable host memory: the copy is staged before the call returns, so idx may go out of scope
-        if (r) HIPCK(hipMemcpyAsync(w.idx->p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, st));
+        SlotFence fence(c->pool, c->dev, k, st);
+        if (r) KCK(c->stage[(size_t)k].upload(w.idx->p, idx.data(), idx.size() * 4, st));  // pinned ring
         s = launch_pok(c, w, n, q, r, d_s1, d_s2, d_J, d_T, d_resp, d_chal, w.idx->as<uint32_t>(), d_rev_msgs,
                        d_verdicts, d_gt, st);
         if (s) return s;
-        return slot_end(st, sl);
+        return fence.close() ? CC_ERR_HIP : CC_OK;
     }
     s = ensure_work(c, n);
     if (s) return s;

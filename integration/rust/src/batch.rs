@@ -1,6 +1,9 @@
 // src/batch.rs — batch entry points on the reference crate's own types (src/signature.rs), through
 // src/hip.rs.  Encodings are exactly amcl_wrapper's to_bytes() (G1 97 B, G2 192 B, Fr 48 B), so the
 // glue only concatenates.  Where the reference panics the shim panics too (HipCtx::check).
+// Every wrapper asserts, before its unsafe call, each length the C side derives its reads from
+// (`len-guard` lines; tests/test_rust_binding.py checks they are present): the C ABI reads n * q * 48
+// bytes of messages, n * len entries of a batch, ..., so a shorter Vec would be a heap over-read.
 use crate::hip::*;
 use crate::signature::{BlindSignature, Params, Signature, SignatureRequest, Sigkey, Verkey};
 use crate::{OtherGroup, SignatureGroup};
@@ -14,7 +17,8 @@ impl Signature {
     pub fn verify_batch(sigs: &[Signature], messages: &[Vec<FieldElement>], vk: &Verkey,
                         params: &Params, ctx: &HipCtx) -> Vec<bool> {
         let q = vk.Y_tilde.len();
-        assert!(messages.iter().all(|m| m.len() == q), "Verkey valid for {} messages", q);
+        assert_eq!(messages.len(), sigs.len(), "one message vector per signature");  // len-guard
+        assert!(messages.iter().all(|m| m.len() == q), "Verkey valid for {} messages", q);  // len-guard
         let s1: Vec<u8> = sigs.iter().flat_map(|s| s.sigma_1.to_bytes()).collect();
         let s2: Vec<u8> = sigs.iter().flat_map(|s| s.sigma_2.to_bytes()).collect();
         let m:  Vec<u8> = messages.iter().flatten().flat_map(|f| f.to_bytes()).collect();
@@ -31,12 +35,15 @@ impl Signature {
 
     /// Batch form of `Signature::aggregate` (signature.rs:448-470).
     pub fn aggregate_batch(threshold: usize, batches: &[Vec<(usize, Signature)>], ctx: &HipCtx) -> Vec<Signature> {
+        if batches.is_empty() { return Vec::new(); }
         let len = batches[0].len();
+        assert!(batches.iter().all(|b| b.len() == len), "every batch has the same length");  // len-guard
         assert!(len >= threshold);                                   // signature.rs:449
         let ids: Vec<u64> = batches.iter().flatten().map(|(i, _)| *i as u64).collect();
         let s1: Vec<u8> = batches.iter().flatten().flat_map(|(_, s)| s.sigma_1.to_bytes()).collect();
         let s2: Vec<u8> = batches.iter().flatten().flat_map(|(_, s)| s.sigma_2.to_bytes()).collect();
-        let sb = s1.len() / ids.len();
+        let sb = ctx.sig_bytes();
+        assert!(s1.len() == ids.len() * sb && s2.len() == ids.len() * sb, "signature encodings");  // len-guard
         let (mut o1, mut o2) = (vec![0u8; sb * batches.len()], vec![0u8; sb * batches.len()]);
         let st = unsafe { cc_signature_aggregate_batch(ctx.raw, batches.len(), len, threshold, ids.as_ptr(),
                                                        s1.as_ptr(), s2.as_ptr(), o1.as_mut_ptr(), o2.as_mut_ptr()) };
@@ -78,13 +85,17 @@ impl BlindSignature {
     /// has k hidden and q - k known messages.
     pub fn new_batch(reqs: &[SignatureRequest], sigkey: &Sigkey, ctx: &HipCtx) -> Vec<BlindSignature> {
         let (n, q) = (reqs.len(), sigkey.y.len());
+        if n == 0 { return Vec::new(); }
         let k = reqs[0].ciphertexts.len();
+        assert!(k <= q && reqs.iter().all(|r| r.ciphertexts.len() == k && r.known_messages.len() == q - k),
+                "every request has k hidden and q - k known messages");  // len-guard
         let cm: Vec<u8> = reqs.iter().flat_map(|r| r.commitment.to_bytes()).collect();
         let kn: Vec<u8> = reqs.iter().flat_map(|r| r.known_messages.iter().flat_map(|m| m.to_bytes())).collect();
         let ct: Vec<u8> = reqs.iter().flat_map(|r| r.ciphertexts.iter()
                               .flat_map(|c| [c.0.to_bytes(), c.1.to_bytes()].concat())).collect();
         let y: Vec<u8> = sigkey.y.iter().flat_map(|v| v.to_bytes()).collect();
-        let sb = cm.len() / n;
+        let sb = ctx.sig_bytes();
+        assert_eq!(cm.len(), n * sb, "commitment encodings");  // len-guard
         let (mut h, mut c1, mut c2) = (vec![0u8; n * sb], vec![0u8; n * sb], vec![0u8; n * sb]);
         ctx.check(unsafe { cc_blind_sign_batch(ctx.raw, n, q, k, cm.as_ptr(), kn.as_ptr(), ct.as_ptr(),
                                                sigkey.x.to_bytes().as_ptr(), y.as_ptr(),
@@ -100,6 +111,9 @@ impl BlindSignature {
 /// commitment set set_of[i] (each set t x G1 bytes).
 pub fn verify_shares_batch(t: usize, g: &G1, h: &G1, sets: &[Vec<G1>], set_of: &[u32], ids: &[u64],
                            shares: &[(FieldElement, FieldElement)], ctx: &HipCtx) -> Vec<bool> {
+    assert!(set_of.len() == ids.len() && shares.len() == ids.len(), "one set, id and share per check");  // len-guard
+    assert!(sets.iter().all(|s| s.len() == t), "every commitment set has t points");  // len-guard
+    assert!(set_of.iter().all(|&k| (k as usize) < sets.len()), "set index in range");  // len-guard
     let cm: Vec<u8> = sets.iter().flatten().flat_map(|c| c.to_bytes()).collect();
     let sh: Vec<u8> = shares.iter().flat_map(|(s, st)| [s.to_bytes(), st.to_bytes()].concat()).collect();
     let mut v = vec![0u8; ids.len()];
@@ -113,7 +127,9 @@ impl Verkey {
     /// Batch form of `Verkey::aggregate` (signature.rs:483-526): n aggregations of `len` (id, Verkey)
     /// entries each; only the first `threshold` are used (HashSet semantics of the ids as there).
     pub fn aggregate_batch(threshold: usize, batches: &[Vec<(usize, &Verkey)>], ctx: &HipCtx) -> Vec<Verkey> {
+        if batches.is_empty() { return Vec::new(); }
         let (n, len) = (batches.len(), batches[0].len());
+        assert!(batches.iter().all(|b| b.len() == len), "every batch has the same length");  // len-guard
         assert!(len >= threshold);                                   // signature.rs:484
         let q = batches[0][0].1.Y_tilde.len();
         assert!(batches.iter().flatten().all(|(_, vk)| vk.Y_tilde.len() == q));  // signature.rs:486-488
@@ -121,7 +137,8 @@ impl Verkey {
         let x: Vec<u8> = batches.iter().flatten().flat_map(|(_, vk)| vk.X_tilde.to_bytes()).collect();
         let y: Vec<u8> = batches.iter().flatten()
             .flat_map(|(_, vk)| vk.Y_tilde.iter().flat_map(|v| v.to_bytes())).collect();
-        let ob = x.len() / ids.len();
+        let ob = ctx.oth_bytes();
+        assert!(x.len() == ids.len() * ob && y.len() == ids.len() * q * ob, "verkey encodings");  // len-guard
         let (mut ox, mut oy) = (vec![0u8; n * ob], vec![0u8; n * q * ob]);
         ctx.check(unsafe { cc_verkey_aggregate_batch(ctx.raw, n, len, threshold, q, ids.as_ptr(), x.as_ptr(),
                                                      y.as_ptr(), ox.as_mut_ptr(), oy.as_mut_ptr()) });
@@ -140,7 +157,15 @@ pub fn pok_verify_batch(proofs: &[(Vec<u8>, Vec<u8>, Vec<u8>, Vec<u8>, Vec<Field
                         revealed_idx: &[u64], revealed_msgs: &[Vec<FieldElement>], vk: &Verkey, params: &Params,
                         ctx: &HipCtx) -> Vec<bool> {
     let (n, q, r) = (proofs.len(), vk.Y_tilde.len(), revealed_idx.len());
+    if n == 0 { return Vec::new(); }
     let nresp = proofs[0].4.len();
+    let (sb, ob) = (ctx.sig_bytes(), ctx.oth_bytes());
+    assert_eq!(chal.len(), n, "one challenge per proof");  // len-guard
+    assert!(revealed_msgs.len() == n && revealed_msgs.iter().all(|m| m.len() == r),
+            "r revealed messages per proof");  // len-guard
+    assert!(proofs.iter().all(|p| p.4.len() == nresp), "the same response count for every proof");  // len-guard
+    assert!(proofs.iter().all(|p| p.0.len() == sb && p.1.len() == sb && p.2.len() == ob && p.3.len() == ob),
+            "proof part encodings (sigma'_1, sigma'_2: SignatureGroup; J, T: OtherGroup)");  // len-guard
     ctx.set_params(&params.g_tilde.to_bytes());
     ctx.set_verkey(&vk.X_tilde.to_bytes(), &vk.Y_tilde.iter().flat_map(|y| y.to_bytes()).collect::<Vec<u8>>(), q);
     let cat = |f: &dyn Fn(&(Vec<u8>, Vec<u8>, Vec<u8>, Vec<u8>, Vec<FieldElement>)) -> Vec<u8>| -> Vec<u8> {

@@ -126,12 +126,18 @@ impl HipCtx {
     pub fn check(&self, st: c_int) {
         assert_eq!(st, 0, "{}", self.status_str(st));
     }
+    /// Encoded sizes (amcl_wrapper to_bytes): SignatureGroup / OtherGroup element under this context's mode.
+    pub fn sig_bytes(&self) -> usize { if self.mode() == CC_SIG_G2 { 192 } else { 97 } }
+    pub fn oth_bytes(&self) -> usize { if self.mode() == CC_SIG_G2 { 97 } else { 192 } }
     /// Idempotent: the same g~ again is a byte compare.
     pub fn set_params(&self, g_tilde: &[u8]) {
+        assert_eq!(g_tilde.len(), self.oth_bytes(), "g~ encoding");  // len-guard: the C side reads oth_bytes
         self.check(unsafe { cc_set_params(self.raw, g_tilde.as_ptr()) });
     }
     /// Idempotent: the same verkey again is a byte compare; a new one builds fixed-base tables.
     pub fn set_verkey(&self, x: &[u8], y: &[u8], q: usize) {
+        let ob = self.oth_bytes();
+        assert!(x.len() == ob && y.len() == q * ob, "verkey encoding");  // len-guard: X 1 x ob, Y q x ob
         self.check(unsafe { cc_set_verkey(self.raw, x.as_ptr(), y.as_ptr(), q) });
     }
 }

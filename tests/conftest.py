@@ -24,8 +24,12 @@ def golden(name):
 
 
 def oracle_lib():
-    """The C oracle (test infrastructure only), built on demand."""
+    """The C oracle (test infrastructure only), built on demand.  CC_ORACLE_SAN=1: the same entry points
+    run in the ASan/UBSan build (tests/san_oracle.py; tests/test_sanitizers.py sets it)."""
     import ctypes
+    if os.environ.get("CC_ORACLE_SAN") == "1":
+        from san_oracle import SanOracle
+        return SanOracle()
     so = os.path.join(ROOT, "oracle", "build", "liboracle.so")
     if not os.path.exists(so):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle", "c")])

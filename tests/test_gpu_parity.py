@@ -302,7 +302,8 @@ def test_ragged_batch_sizes_pair_lanes(ctxs, n):
     assert np.array_equal(np.frombuffer(ver.raw, np.uint8), v)
 
 
-WIDE_MAX, FEXP_WIDE_MAX, PREP_WIDE_MAX = 4096, 2048, 1024  # capi.cpp kWideMax, kFexpWideMax, kPrepWideMax
+WIDE_MAX, FEXP_WIDE_MAX, PREP_WIDE_MAX = 4096, 2048, 1024  # slots.h kWideMax, kFexpWideMax, kPrepWideMax
+WIDE2_MAX_CREDS = 128  # fexp_pl.hip kWide2Max = 256 pairs: k_miller_wide2 (two waves a pair) up to 128 credentials
 
 
 @pytest.mark.parametrize("mode", ["G2", "G1"])
@@ -310,9 +311,11 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
     """Batches of <= 4,096 credentials take the one-wave-per-pair Miller path (capi.cpp kWideMax:
     k_wide_pairs -> k_miller_wide -> k_f12_reduce_wide), those of <= 2,048 also the one-wave-per-
     credential final exponentiation (kFexpWideMax: k_fexp1) and the one-wave prep; larger ones the
-    pair-lane loop, the quad-lane fexp and the lane-pair prep.  The same credentials (a 4,104 batch; its
-    first 4,096, 2,049, 2,048, 1,025 and a ragged 37; then single credentials) give the same verdicts
-    and GT bytes, with every corruption kind (identity sigmas included) in the batch."""
+    pair-lane loop, the quad-lane fexp and the lane-pair prep; up to 128 credentials (256 pairs,
+    fexp_pl.hip kWide2Max) the wide loop runs two waves a pair (k_miller_wide2).  The same credentials (a
+    4,104 batch; its first 4,096, 2,049, 2,048, 1,025, 129, 128 and a ragged 37; then single credentials)
+    give the same verdicts and GT bytes, with every corruption kind (identity sigmas included) in the
+    batch."""
     import bench
     from coconut import verify_batch
     m = MODES[mode]
@@ -324,7 +327,7 @@ def test_small_batch_wide_miller_path_matches_pair_lane_path(ctxs, mode):
     sb = 192 if m == 0 else 97
     v_big, gt_big = verify_batch(ctx, n, q, b["s1"], b["s2"], b["msgs"], want_gt=True)
     assert np.array_equal(v_big, b["expect"])
-    for k in (WIDE_MAX, FEXP_WIDE_MAX + 1, FEXP_WIDE_MAX, PREP_WIDE_MAX + 1, 37):
+    for k in (WIDE_MAX, FEXP_WIDE_MAX + 1, FEXP_WIDE_MAX, PREP_WIDE_MAX + 1, WIDE2_MAX_CREDS + 1, WIDE2_MAX_CREDS, 37):
         v_w, gt_w = verify_batch(ctx, k, q, b["s1"][:k * sb], b["s2"][:k * sb], b["msgs"][:k * q * 48], want_gt=True)
         assert np.array_equal(v_w, b["expect"][:k]), k
         assert gt_w == gt_big[:576 * k], k

@@ -73,3 +73,36 @@ def test_build_script_builds_and_links_the_engine():
     assert "COCONUT_HIP_DIR" in b and "rustc-link-lib=dylib=coconut_hip" in b and "make" in b
     mk = open(os.path.join(ROOT, "coconut-rust_amd", "Makefile")).read()
     assert "--offload-arch=$(ARCH)" in mk and "ARCH ?= gfx950" in mk and "libcoconut_hip.so" in mk
+
+
+def _fn_body(src, name):
+    i = src.index(f"fn {name}(")
+    j = src.find("\n    pub fn ", i + 1)
+    k = src.find("\npub fn ", i + 1)
+    ends = [e for e in (j, k) if e > 0]
+    return src[i:min(ends) if ends else len(src)]
+
+
+def test_safe_wrappers_guard_every_length_the_c_side_reads():
+    """the safe wrappers must assert, before the unsafe call, every length the C ABI derives
+    its reads from (else a shorter Vec is a heap over-read reachable from safe code)."""
+    b = open(os.path.join(RS, "batch.rs")).read()
+    h = open(os.path.join(RS, "hip.rs")).read()
+    need = {
+        "verify_batch": ["messages.len(), sigs.len()", "m.len() == q"],
+        "aggregate_batch": ["b.len() == len", "len >= threshold"],
+        "new_batch": ["r.ciphertexts.len() == k", "r.known_messages.len() == q - k", "cm.len(), n * sb"],
+        "verify_shares_batch": ["set_of.len() == ids.len()", "shares.len() == ids.len()", "s.len() == t",
+                                "(k as usize) < sets.len()"],
+        "pok_verify_batch": ["chal.len(), n", "revealed_msgs.len() == n", "m.len() == r", "p.4.len() == nresp",
+                             "p.0.len() == sb", "p.2.len() == ob", "p.3.len() == ob"],
+    }
+    for fn, guards in need.items():
+        bodies = [_fn_body(b, fn)] if fn != "aggregate_batch" else \
+            [b[m.start():] for m in re.finditer(r"fn aggregate_batch\(", b)]
+        for body in bodies:
+            body = body[:body.index("unsafe")]  # the guards come before the FFI call
+            for g in guards:
+                assert g in body, (fn, g)
+    assert "x.len() == ob && y.len() == q * ob" in _fn_body(h, "set_verkey")
+    assert "g_tilde.len(), self.oth_bytes()" in _fn_body(h, "set_params")

@@ -14,6 +14,6 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS" "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_WAIT_ANY" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   echo "[pmc] pass $i: $grp"
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/p$i" -o pmc --output-format csv -- python3 "$R/bench.py" $BARGS --steps 1 --warmup 0 --no-cpu-baseline --no-pcie > "$OUT/p$i.log" 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/p$i" -o pmc --output-format csv -- python3 "$R/bench.py" $BARGS --steps 1 --warmup 0 --no-cpu-baseline --no-pcie --no-sigg1 > "$OUT/p$i.log" 2>&1
 done
 echo "[pmc] done"
