@@ -42,7 +42,12 @@ __global__ __launch_bounds__(256) void k_scalars_w8(size_t nm, const uint8_t* __
     o[1] = make_uint4(m.v[4], m.v[5], m.v[6], m.v[7]);
 }
 
-// SigG2, per-credential verkey (G1 bases), one credential per lane pair
+// SigG2, per-credential verkey (G1 bases), ONE credential per LANE (round 6; round 4-5 ran one per
+// lane pair, each lane over half the bases, both lanes running the whole 260-doubling chain): one chain
+// of 65 windows over all q + 1 bases, so the doublings are paid once per credential (260 x 7 products
+// instead of 2 x 260 x 7 a pair) and the two halves' Jacobian sum and storage-form round trip go away.
+// 65,536 credentials are 1,024 waves, one a SIMD; a verifier keeps a second batch in flight
+// (cc_set_concurrency), whose kernels fill the SIMD beside it (profiles/r06/pervk_lane).
 __global__ __launch_bounds__(256, 2) void k_prep_sigg2_var(size_t n, int q, const uint8_t* __restrict__ s1b,
                                                            const uint8_t* __restrict__ s2b,
                                                            const uint8_t* __restrict__ vkX,
@@ -50,46 +55,35 @@ __global__ __launch_bounds__(256, 2) void k_prep_sigg2_var(size_t n, int q, cons
                                                            const uint32_t* __restrict__ scal,
                                                            uint32_t* __restrict__ scratch,
                                                            uint32_t* __restrict__ prep, uint32_t* __restrict__ flags) {
-    const size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-    const size_t i = g >> 1;
-    const int h = (int)(g & 1);
-    if (i >= n) return;  // pair-uniform
+    const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
     Soa S{prep, n};
     uint32_t fl = 0;
-    {
+#pragma unroll 1
+    for (int h = 0; h < 2; h++) {  // sigma_1 -> Q1, -sigma_2 -> Q2
         Aff<Fp2> a;
         if (!g2_decode(a, (h ? s2b : s1b) + i * 192)) fl |= h ? 2u : 1u;
-        if (h) f2_neg(a.y, a.y);  // -sigma_2
+        if (h) f2_neg(a.y, a.y);
         const int slot = h ? S_Q2 : S_Q1;
         st_f2(S, slot, i, a.x);
         st_f2(S, slot + 2, i, a.y);
     }
     lz::JG a;
-    straus_g1lz_lane(a, 2, h, (size_t)q, vkY + i * (size_t)q * 97, scal + i * (size_t)q * 8,
+    straus_g1lz_lane(a, 1, 0, (size_t)q, vkY + i * (size_t)q * 97, scal + i * (size_t)q * 8,
                      scratch + i * straus_g1lz_words((size_t)q));
-    if (!h) {  // X~ with scalar 1
+    {  // X~ with scalar 1
         Aff<Fp> X;
         if (g1_decode(X, vkX + i * 97)) a = lz::jg_add_aff(a, ag_of(lz::reduce(lz::in_r(X.x)), lz::reduce(lz::in_r(X.y))));
     }
-    Jac<Fp> pr = lz::jg_to(a), o;
-    o.x = pl::swp(pr.x);
-    o.y = pl::swp(pr.y);
-    o.z = pl::swp(pr.z);
-    fl |= pl::swp(fl);
-    if (h) {
-        Jac<Fp> t = pr;
-        pr = o;
-        o = t;
-    }
-    jac_add(pr, pr, o);  // (even lane's sum) + (odd lane's sum), the same operand order on both lanes
-    if (jac_is_inf(pr)) {
+    if (lz::jg_is_inf(a)) {
         fl |= 4u;
-    } else {  // affine in the R' form (the Miller loop's kAffRp operand): x on the even lane, y on the odd
+    } else {  // affine in the R' form (the Miller loop's kAffRp operand)
         Fp x, y;
-        lz::jg_to_aff_rp(x, y, lz::jg_from(pr));
-        st_fp(S, S_P1 + h, i, h ? y : x);
+        lz::jg_to_aff_rp(x, y, a);
+        st_fp(S, S_P1, i, x);
+        st_fp(S, S_P1 + 1, i, y);
     }
-    if (!h) flags[i] = fl;
+    flags[i] = fl;
 }
 
 // SigG1, per-credential verkey (G2 bases on the lazy pair-lane field), one credential per lane pair
@@ -366,7 +360,7 @@ int cck_prep_var(int mode, size_t n, int q, const uint8_t* d_s1, const uint8_t* 
         hipLaunchKernelGGL(k_prep_sigg1_var_wide, dim3((unsigned)n), dim3(64), 0, st, n, q, d_s1, d_s2, d_vkX, d_vkY,
                            scal, straus, d_prep, d_flags);
     else if (mode == 0)
-        hipLaunchKernelGGL(k_prep_sigg2_var, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_vkX,
+        hipLaunchKernelGGL(k_prep_sigg2_var, dim3(nblocks(n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_vkX,
                            d_vkY, scal, straus, d_prep, d_flags);
     else
         hipLaunchKernelGGL(k_prep_sigg1_var, dim3(nblocks(2 * n, 256)), dim3(256), 0, st, n, q, d_s1, d_s2, d_vkX,
