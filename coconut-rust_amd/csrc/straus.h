@@ -11,12 +11,16 @@
 
 namespace cc {
 
-// signed radix-16 digits of a canonical 255-bit scalar: 65 digits in [-8, 8], least significant first
+// signed radix-16 digits of a canonical 255-bit scalar: 65 digits in [-8, 8], least significant first.
+// The scalar's 8 words are loaded once, up front (two 16-byte loads; k is 16-byte aligned): read
+// inside the loop, every digit waited on a global load, since the digit stores may alias them.
 DEV void recode_w4(int8_t* d, const uint32_t k[8]) {
+    const uint4 a = reinterpret_cast<const uint4*>(k)[0], b = reinterpret_cast<const uint4*>(k)[1];
+    const uint32_t kk[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     int carry = 0;
-#pragma unroll 1
+#pragma unroll
     for (int w = 0; w < 64; w++) {
-        int v = (int)((k[w >> 3] >> (4 * (w & 7))) & 0xfu) + carry;
+        const int v = (int)((kk[w >> 3] >> (4 * (w & 7))) & 0xfu) + carry;
         carry = v > 8;
         d[w] = (int8_t)(v - 16 * carry);
     }

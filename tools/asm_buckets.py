@@ -152,6 +152,24 @@ def dyn(funcs, fname, weights, spec_callees, memo, depth=0):
     return r
 
 
+def region(funcs, fname, weights, labels, spec_callees):
+    """dynamic bucket counts of the blocks `labels` of fname (their own instructions and their calls)"""
+    tot = collections.Counter()
+    w = 1.0
+    for b in funcs[fname]:
+        w = weights.get(b["label"], w)
+        if b["label"] not in labels:
+            continue
+        for k, v in b["counts"].items():
+            tot[k] += w * v
+        for c in b["calls"]:
+            if c in funcs:
+                sub = dyn(funcs, c, spec_callees.get(short(c), {}), spec_callees, {})
+                for k2, v2 in sub["total"].items():
+                    tot[k2] += w * v2
+    return tot
+
+
 def summarize(c, alg_mads=None, pmc_valu=None):
     valu = sum(c.get(b, 0) for b in VALU_BUCKETS)
     out = {b: round(c.get(b, 0)) for b in ORDER}
@@ -188,6 +206,14 @@ def main():
                     for c, v in sorted(r["calls"].items(), key=lambda kv: -kv[1]["calls"])},
         "kernel_own_top_ops": {k: round(v) for k, v in r["own_ops"].most_common(25)},
     }
+    if spec.get("regions"):
+        res["regions"] = {}
+        for name, labels in spec["regions"].items():
+            c = region(funcs, kern, spec["blocks"], set(labels), spec.get("callees", {}))
+            sm = summarize(c)
+            sm["share_of_total_valu"] = round(sm["valu"] / res["total"]["valu"], 4)
+            sm["non_mad_share_of_region_valu"] = round(1 - sm["mad"] / max(sm["valu"], 1), 4)
+            res["regions"][name] = sm
     for c, v in r["calls"].items():
         res["callees"][short(c)]["share_of_total_valu"] = round(
             v["calls"] * sum(v["per_call"].get(b, 0) for b in VALU_BUCKETS) / res["total"]["valu"], 4)

@@ -4,7 +4,7 @@
 # MODES and every argument set in ARGS_LIST (';'-separated), then (PROF=1) rocprofv3 kernel stats and the
 # PMC passes of the current build for each mode at one batch in flight.  Each GPU step has its own time
 # limit; the first failure ends the script.
-#   TESTS="tests/test_gpu_parity.py -k pervk" MODES="verify-pervk" ARGS_LIST="--inflight 2;--inflight 1" \
+#   TESTS="tests/test_gpu_parity.py" KEXPR="pervk" MODES="verify-pervk" ARGS_LIST="--inflight 2;--inflight 1" \
 #     PROF=1 bash tools/gpu_ab6.sh <tag>
 set -o pipefail
 TAG=${1:-ab}
@@ -14,7 +14,9 @@ R=$(pwd)
 export TMPDIR=/tmp
 if [ -n "${TESTS:-}" ]; then
   echo "[ab] tests $TESTS"
-  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
+  KX=()
+  [ -n "${KEXPR:-}" ] && KX=(-k "$KEXPR")
+  timeout -k 10 900 python -u -m pytest $TESTS "${KX[@]}" -m gpu -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1 || { tail -30 "$OUT/pytest_gpu.log"; exit 1; }
   tail -1 "$OUT/pytest_gpu.log"
 fi
 IFS=';' read -ra ARGSETS <<< "${ARGS_LIST:-}"
@@ -30,7 +32,7 @@ for m in ${MODES:-verify}; do
         [ -f "$lib" ] || continue
         f="$OUT/${m}_a${a}_${v}.$k.json"
         COCONUT_HIP_LIB=$lib timeout -k 10 400 python -u bench.py --mode $m --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-pcie --no-sigg1 $args > "$f" 2> "${f%.json}.err" || { tail -20 "${f%.json}.err"; exit 1; }
-        python3 -c "import json,sys;d=json.load(open('$f'));k=d.get('kernels',{});print('[ab] $m [$args] $v $k', d['value'], d['ms_per_step'], {x:y.get('ms') for x,y in k.items()})"
+        python3 -c "import json,sys;d=json.load(open('$f'));k=d.get('kernels',{});print('[ab] $m [$args] $v $k', d['value'], d['ms_per_step'], {x:(y.get('ms') if isinstance(y, dict) else y) for x,y in k.items()})"
       done
     done
   done
