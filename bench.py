@@ -48,7 +48,7 @@ HBM_PEAK_GBS = 8000.0
 OPCOUNT = os.path.join(ROOT, "tests", "fixtures", "opcount.json")
 # per-mode rocprofv3 evidence of the current build (tools/gpu_modes_prof.sh): kernel-trace stats and the
 # PMC passes of one bench step, summarised per kernel by tools/pmc_summary.py
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r05", "modes")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r06", "modes")
 
 
 def peak_mad_per_s():
@@ -94,7 +94,7 @@ def opcounts(key):
 
 
 def pmc(kernel_key, mode=None):
-    """Per-launch PMC figures of the same build (profiles/r05/modes/<mode>/pmc_summary.json; separate
+    """Per-launch PMC figures of the same build (profiles/r06/modes/<mode>/pmc_summary.json; separate
     rocprofv3 --pmc passes, tools/pmc_summary.py; none if that mode has no committed summary): HBM bytes =
     2 x FETCH_SIZE (gfx950 counts half of wide reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, and VALU
     wave-instructions per CU per clock."""
@@ -124,7 +124,7 @@ def kernel_pmc_report(mode):
     duration (rocprofv3 --kernel-trace --stats), HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE,
     MI355X_MICROARCH.md gfx950 correction), achieved HBM GB/s, VALU issue (wave-instructions per CU per
     clock; 1.0 = every SIMD issuing a wave64 VALU op every 4 clocks) and the fraction of wave-cycles
-    waiting.  Read from profiles/r05/modes/<mode>/ (committed evidence of the same build)."""
+    waiting.  Read from profiles/r06/modes/<mode>/ (committed evidence of the same build)."""
     import csv
     d = os.path.join(PROFILE_DIR, mode)
     try:
@@ -155,7 +155,7 @@ def kernel_pmc_report(mode):
             row["wait_frac"] = round(c.get("SQ_WAIT_ANY", 0) / c["SQ_WAVE_CYCLES"], 3)
         short = name.split("(")[0].replace("void ", "")
         out[short] = row
-    return {"source": f"profiles/r05/modes/{mode}/ (rocprofv3 kernel stats + PMC passes)", "kernels": out}
+    return {"source": f"profiles/r06/modes/{mode}/ (rocprofv3 kernel stats + PMC passes)", "kernels": out}
 
 
 def cpu_info():
@@ -893,7 +893,7 @@ def main():
     ap.add_argument("--rlc-inflight", type=int, default=1,
                     help="RLC mode: engines (own streams, partial buffers) taking cc_set_concurrency slots in "
                          "turn; 1 = the pipelined single engine (measured the same as 2 and 3: "
-                         "profiles/r05/modes2)")
+                         "profiles/r05/modes2; with pinned seed staging again 5.68 / 5.68 M/s: profiles/r06/base)")
     ap.add_argument("--mode", choices=["verify", "verify-g1", "verify-pervk", "verify-pervk-g1", "rlc", "aggregate",
                                        "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
     args = ap.parse_args()
