@@ -206,6 +206,10 @@ def _dist_setup():
         import torch.distributed as dist
         if BACKEND == "nccl":  # RCCL over xGMI: one GPU per rank
             torch.cuda.set_device(local)
+        else:
+            # gloo: a rehearsal of the multi-rank path (barriers, max over ranks, RLC all-gather through host
+            # memory); with fewer GPUs than ranks the ranks share them (device_count touches no GPU here)
+            local = local % max(1, torch.cuda.device_count())
         dist.init_process_group(BACKEND)
     return world, rank, local, dist
 

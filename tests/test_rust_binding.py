@@ -106,3 +106,16 @@ def test_safe_wrappers_guard_every_length_the_c_side_reads():
                 assert g in body, (fn, g)
     assert "x.len() == ob && y.len() == q * ob" in _fn_body(h, "set_verkey")
     assert "g_tilde.len(), self.oth_bytes()" in _fn_body(h, "set_params")
+
+
+def test_single_credential_stays_on_the_reference_cpu_path():
+    """INTEGRATION.md §3: one Signature::verify through the engine (~2.1 ms) is not faster than the
+    reference's own CPU verify on one thread (~1.9 ms), so below GPU_MIN_BATCH the shim calls the
+    reference's verify (signature.rs:473) and only batches reach cc_verify_batch."""
+    b = open(os.path.join(RS, "batch.rs")).read()
+    m = re.search(r"pub const GPU_MIN_BATCH: usize = (\d+);", b)
+    assert m and int(m.group(1)) == 2
+    body = _fn_body(b, "verify_batch")
+    cut = body.index("if sigs.len() < GPU_MIN_BATCH")
+    assert cut < body.index("cc_verify_batch(")
+    assert ".verify(m, vk, params)" in body[cut:body.index("cc_verify_batch(")]
