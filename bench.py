@@ -313,16 +313,18 @@ def rand_fr(rng):
 CORRUPT_KINDS = ("sigma2+G", "msg+1", "swapped", "sigma1=O", "sigma2=O", "wrong vk")
 
 
-def make_verify_batch(ctx, mode, n, q, seed, bad_every=16):
+def make_verify_batch(ctx, mode, n, q, seed, bad_every=16, key_seed=None):
     """one shared verkey AGGREGATED 3-of-5 (Shamir-shared issuer keys, the
     product's Verkey::aggregate on the GPU, checked against x g~ before use); per-credential messages
     uniform; sigma_1 = k G, sigma_2 = k (x + sum y_j m_j) G.  Every bad_every-th credential is corrupted,
     the kinds split evenly over CORRUPT_KINDS: sigma_2 + G, one m_j + 1, sigma_1 <-> sigma_2 swapped,
     sigma_1 = O, sigma_2 = O, signed under another verkey.  mode 0 = SigG2 (sigma in G2), 1 = SigG1.
-    bad_every = 0: all valid."""
+    bad_every = 0: all valid.  key_seed: the issuer keys and g~ drawn from their own seed (the ranks of an
+    RLC job verify under ONE verkey: every rank's finish pairs the gathered window sums with its own g~),
+    the credentials from `seed`."""
     import numpy as np
     import coconut
-    rng = np.random.default_rng(seed)
+    rng = np.random.default_rng(seed if key_seed is None else key_seed)
     og, sg = (1, 2) if mode == 0 else (2, 1)
     gen = {1: coconut.G1_GENERATOR, 2: coconut.G2_GENERATOR}
     ob, sb = (97, 192) if mode == 0 else (192, 97)
@@ -345,6 +347,8 @@ def make_verify_batch(ctx, mode, n, q, seed, bad_every=16):
                                                               [x * gk % R_ORDER] + [v * gk % R_ORDER for v in y]))
     if X + Y != want:
         raise SystemExit("aggregated verkey differs from g~ * master secret — refusing to build the batch")
+    if key_seed is not None:
+        rng = np.random.default_rng(seed)
     m = [[rand_fr(rng) for _ in range(q)] for _ in range(n)]
     ks = [rand_fr(rng) or 1 for _ in range(n)]
     x_other = (x + 0x5EED) % R_ORDER
@@ -708,7 +712,7 @@ def bench_rlc(args):
     dev = torch.device("cuda", local)
     n, q = args.n or 131072, 16
     ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
-    batch = make_verify_batch(ctx, 0, n, q, seed=3000 + rank, bad_every=0)
+    batch = make_verify_batch(ctx, 0, n, q, seed=3000 + rank, bad_every=0, key_seed=3000)
     ctx.set_params(batch["g_tilde"])
     ctx.set_table_bits(vk_bits_for(args), 0)
     ctx.set_verkey(batch["X"], batch["Y"])
