@@ -6,6 +6,7 @@
 # limit; the first failure ends the script.
 #   TESTS="tests/test_gpu_parity.py" KEXPR="pervk" MODES="verify-pervk" ARGS_LIST="--inflight 2;--inflight 1" \
 #     PROF=1 bash tools/gpu_ab6.sh <tag>
+# PREV_ENV="COCONUT_VKAGG_BA=0": the prev side is the current build with that environment (a runtime switch)
 set -o pipefail
 TAG=${1:-ab}
 OUT=$(pwd)/gpurun_out/$TAG
@@ -28,10 +29,14 @@ for m in ${MODES:-verify}; do
     for k in 1 2; do
       for v in prev cur; do
         lib=$R/coconut-rust_amd/libcoconut_hip.so
-        [ $v = prev ] && lib=$R/coconut-rust_amd/libcoconut_hip_prev.so
+        penv=()
+        if [ $v = prev ]; then
+          # PREV_ENV="VAR=value": the prev side is the current build under that environment
+          if [ -n "${PREV_ENV:-}" ]; then penv=($PREV_ENV); else lib=$R/coconut-rust_amd/libcoconut_hip_prev.so; fi
+        fi
         [ -f "$lib" ] || continue
         f="$OUT/${m}_a${a}_${v}.$k.json"
-        COCONUT_HIP_LIB=$lib timeout -k 10 400 python -u bench.py --mode $m --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-pcie --no-sigg1 $args > "$f" 2> "${f%.json}.err" || { tail -20 "${f%.json}.err"; exit 1; }
+        env "${penv[@]}" COCONUT_HIP_LIB=$lib timeout -k 10 400 python -u bench.py --mode $m --steps ${STEPS:-20} --warmup 3 --no-cpu-baseline --no-pcie --no-sigg1 $args > "$f" 2> "${f%.json}.err" || { tail -20 "${f%.json}.err"; exit 1; }
         python3 -c "import json,sys;d=json.load(open('$f'));k=d.get('kernels',{});print('[ab] $m [$args] $v $k', d['value'], d['ms_per_step'], {x:(y.get('ms') if isinstance(y, dict) else y) for x,y in k.items()})"
       done
     done
