@@ -712,7 +712,7 @@ def bench_rlc(args):
     dev = torch.device("cuda", local)
     n, q = args.n or 131072, 16
     ctx = coconut.Context(local, coconut.GroupMode.SIG_G2)
-    batch = make_verify_batch(ctx, 0, n, q, seed=3000 + rank, bad_every=0, key_seed=3000)
+    batch = make_verify_batch(ctx, 0, n, q, seed=3000 + rank, bad_every=0, key_seed=2999)
     ctx.set_params(batch["g_tilde"])
     ctx.set_table_bits(vk_bits_for(args), 0)
     ctx.set_verkey(batch["X"], batch["Y"])
