@@ -34,6 +34,9 @@
  * any mix of streams see the context's workspaces in program order.
  * Errors mirror the reference's failure modes (src/errors.rs:6-24): where the reference panics
  * (assert!/unwrap) the C ABI returns a code instead.
+ * Empty batches: every batch entry point checks its context state and lengths first (CC_ERR_STATE,
+ * CC_ERR_LEN, CC_ERR_BASES_EXPS, CC_ERR_THRESHOLD), then returns CC_OK for n = 0 without reading,
+ * writing or launching anything; its buffer pointers may then be NULL (tests/test_gpu_empty.py).
  */
 #ifndef COCONUT_HIP_H
 #define COCONUT_HIP_H
