@@ -100,9 +100,13 @@ def buf(b):
     """bytes/bytearray/numpy -> (ctypes pointer, keepalive)."""
     if b is None:
         return None, None
-    if isinstance(b, (bytes, bytearray)):
-        cb = ctypes.create_string_buffer(bytes(b), len(b)) if len(b) else ctypes.create_string_buffer(1)
-        return ctypes.cast(cb, c_p), cb
     import numpy as np
+    if isinstance(b, (bytes, bytearray)):
+        if not len(b):
+            cb = ctypes.create_string_buffer(1)
+            return ctypes.cast(cb, c_p), cb
+        # no copy: every buffer this passes is a `const` input of the C ABI (read during the call only)
+        a = np.frombuffer(b, dtype=np.uint8)
+        return ctypes.c_void_p(a.ctypes.data), a
     a = np.ascontiguousarray(b)
     return ctypes.c_void_p(a.ctypes.data), a
