@@ -907,7 +907,9 @@ def main():
                          "profiles/r05/modes2; with pinned seed staging again 5.68 / 5.68 M/s: profiles/r06/base)")
     ap.add_argument("--mode", choices=["verify", "verify-g1", "verify-pervk", "verify-pervk-g1", "rlc", "aggregate",
                                        "aggregate-g1", "pok", "pok-g1", "stub"], default="verify")
-    args = ap.parse_args()
+    # a relaunched rank takes the launching command's arguments from the environment (see below)
+    relaunched = os.environ.get("COCONUT_BENCH_ARGV") if "WORLD_SIZE" in os.environ else None
+    args = ap.parse_args(json.loads(relaunched) if relaunched else None)
     if args.backend:
         BACKEND = args.backend
         os.environ["COCONUT_BENCH_BACKEND"] = args.backend  # inherited by the relaunched ranks
@@ -915,8 +917,11 @@ def main():
         # one process per GPU: relaunch under torch.distributed.run BEFORE any GPU call (no exec from a
         # process that touched the GPU: this one has not), and exit with its status
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
-        return subprocess.call(cmd)
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)]
+        # the bench's own arguments travel in the environment: torch.distributed.run's parser reads the
+        # words after the script too, and rejects an abbreviation of its own options (`--n`) there
+        env = dict(os.environ, COCONUT_BENCH_ARGV=json.dumps(sys.argv[1:]))
+        return subprocess.call(cmd, env=env)
     if args.mode == "stub":
         return bench_stub(args)
     if args.mode == "verify":

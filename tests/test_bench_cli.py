@@ -13,7 +13,10 @@ from conftest import ROOT
 def test_bench_gpus2_relaunch_reports_two_ranks():
     env = dict(os.environ, CUDA_VISIBLE_DEVICES="")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
-                        "--mode", "stub", "--steps", "3", "--warmup", "1"], cwd=ROOT, env=env,
+                        "--mode", "stub", "--steps", "3", "--warmup", "1",
+                        # `--n` abbreviates several of torch.distributed.run's options: the relaunch must
+                        # not hand it to that parser (bench.py passes its arguments in the environment)
+                        "--n", "64"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
