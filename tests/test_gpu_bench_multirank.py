@@ -38,3 +38,11 @@ def test_bench_verify_two_ranks():
 def test_bench_rlc_two_ranks():
     d = _bench("--mode", "rlc", "--n", "8192")
     assert d["n_gpus"] == 2 and d["value"] > 0
+
+
+@pytest.mark.parametrize("mode,n", [("verify-pervk", "4096"), ("aggregate", "256"), ("pok", "4096")])
+def test_bench_other_modes_two_ranks(mode, n):
+    """The other sharded modes (bench_modes.py) through the same relaunch and clock."""
+    extra = ["--iss-bits", "8"] if mode == "aggregate" else []
+    d = _bench("--mode", mode, "--n", n, *extra)
+    assert d["n_gpus"] == 2 and d["value"] > 0
