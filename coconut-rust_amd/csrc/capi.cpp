@@ -300,6 +300,14 @@ static void wait_slots(cc_ctx* c, hipStream_t st) { c->pool.wait_all(c->dev, st)
 // are freed or rebuilt: tables, params, workspaces)
 static void drain_slots(cc_ctx* c) { c->pool.drain(c->dev); }
 
+// Argument ceilings of the batch entry points (coconut_hip.h CC_MAX_BATCH etc.): every size product the
+// host computes (n x q x 192 bytes, n x len x 8, grid dimensions) stays far inside size_t and the launch
+// limits, so a garbage count is CC_ERR_DECODE before anything is allocated, copied or launched.
+constexpr size_t kMaxBatch = CC_MAX_BATCH;  // credentials / proofs / points per call
+constexpr size_t kMaxIds = CC_MAX_IDS;      // ids per credential (aggregation `len`)
+constexpr size_t kMaxParts = CC_MAX_PARTS;  // gathered partials of one RLC finish
+constexpr size_t kMaxQ = CC_MAX_Q;          // messages per credential (cc_set_verkey's bound)
+
 struct StreamOrder {
     cc_ctx* c;
     hipStream_t st;
@@ -873,6 +881,7 @@ cc_status cc_verify_batch_device(cc_ctx* c, size_t n, size_t q, const uint8_t* d
     if (!c || (n && (!d_s1 || !d_s2 || !d_verdicts))) return CC_ERR_DECODE;
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
     if (q != c->q) return CC_ERR_LEN;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
@@ -889,6 +898,7 @@ cc_status cc_verify_batch_pervk_device(cc_ctx* c, size_t n, size_t q, const uint
     if (!c || q > 4096 || (n && (!d_s1 || !d_s2 || !d_vkX || !d_verdicts || (q && (!d_msgs || !d_vkY)))))
         return CC_ERR_DECODE;
     if (!c->have_params) return CC_ERR_STATE;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
@@ -994,6 +1004,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
                                 void* stream) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || !seed32 || !d_partial || (n && (!d_s1 || !d_s2 || (q && !d_msgs)))) return CC_ERR_DECODE;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;
     if (q != c->q) return CC_ERR_LEN;
     HIPCK(hipSetDevice(c->device));
@@ -1040,7 +1051,7 @@ cc_status cc_rlc_partial_device(cc_ctx* c, size_t n, size_t q, uint64_t base_ind
 cc_status cc_rlc_finish_device(cc_ctx* c, size_t nparts, const uint32_t* d_partials, uint8_t* d_accept,
                                uint8_t* d_gt, void* stream) {
     c = primary(c);  // a device set forwards to its first device
-    if (!c || !nparts || !d_partials || !d_accept) return CC_ERR_DECODE;
+    if (!c || !nparts || nparts > kMaxParts || !d_partials || !d_accept) return CC_ERR_DECODE;
     if (!c->have_params || !c->have_vk) return CC_ERR_STATE;  // the window pairs' P_w come with the verkey
     HIPCK(hipSetDevice(c->device));
     // the finish owns its buffers (Fp12 values, window-pair operands, fexp scratch, flag) and reads only
@@ -1104,6 +1115,7 @@ cc_status cc_verify_batch(cc_ctx* c, size_t n, size_t q, const uint8_t* s1, cons
         if (!c->have_vk) return CC_ERR_STATE;
         if (q != c->q) return CC_ERR_LEN;
     }
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     if (!c->peers.empty()) return multi_verify(c, n, q, s1, s2, msgs, vkX, vkY, verdicts, gt, rlc);
     HIPCK(hipSetDevice(c->device));
@@ -1153,6 +1165,7 @@ cc_status cc_fixed_base_mul(cc_ctx* c, int group, const uint8_t* base, size_t n,
                             uint8_t* out) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || !base || (n && (!scalars || !out)) || (group != 1 && group != 2)) return CC_ERR_DECODE;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     size_t eb = group == 1 ? 97 : 192, aw = aff_words(group);
@@ -1203,7 +1216,9 @@ cc_status cc_signature_aggregate_batch_device(cc_ctx* c, size_t n, size_t len, s
                                               uint8_t* d_out_s2, void* stream) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!d_ids || !d_s1 || !d_s2 || !d_out_s1 || !d_out_s2))) return CC_ERR_DECODE;
+    if (len > kMaxIds) return CC_ERR_DECODE;
     if (len < t || len == 0) return CC_ERR_THRESHOLD;  // reference: assert!(sigs.len() >= threshold)
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
@@ -1218,7 +1233,9 @@ cc_status cc_signature_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t
                                        const uint8_t* s1, const uint8_t* s2, uint8_t* out_s1, uint8_t* out_s2) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!ids || !s1 || !s2 || !out_s1 || !out_s2))) return CC_ERR_DECODE;
+    if (len > kMaxIds) return CC_ERR_DECODE;
     if (len < t || len == 0) return CC_ERR_THRESHOLD;  // reference: assert!(sigs.len() >= threshold) + sigs[0]
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     size_t sb = (size_t)sig_bytes(c->mode);
@@ -1247,7 +1264,9 @@ cc_status cc_verkey_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, s
                                     const uint8_t* X, const uint8_t* Y, uint8_t* outX, uint8_t* outY) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!ids || !X || !outX || (q && (!Y || !outY))))) return CC_ERR_DECODE;
+    if (len > kMaxIds) return CC_ERR_DECODE;
     if (len < t || len == 0) return CC_ERR_THRESHOLD;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     size_t ob = (size_t)oth_bytes(c->mode);
@@ -1284,6 +1303,7 @@ cc_status cc_verkey_aggregate_batch(cc_ctx* c, size_t n, size_t len, size_t t, s
 cc_status cc_subgroup_check(cc_ctx* c, int group, size_t n, const uint8_t* points, uint8_t* status) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || (group != 1 && group != 2) || (n && (!points || !status))) return CC_ERR_DECODE;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     return subgroup_host(c, group, n, points, status);
@@ -1306,6 +1326,7 @@ static cc_status stage_messages(cc_ctx* c, size_t n, const uint8_t* data, const 
 cc_status cc_hash_to_curve(cc_ctx* c, int group, size_t n, const uint8_t* data, const uint64_t* offsets, uint8_t* out) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || (group != 1 && group != 2) || (n && (!offsets || !out))) return CC_ERR_DECODE;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     const size_t eb = group == 1 ? 97 : 192;
@@ -1326,6 +1347,7 @@ cc_status cc_hash_to_curve(cc_ctx* c, int group, size_t n, const uint8_t* data, 
 cc_status cc_hash_msg(cc_ctx* c, size_t n, const uint8_t* data, const uint64_t* offsets, uint8_t* out48) {
     c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!offsets || !out48))) return CC_ERR_DECODE;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     DevBuf d_data, d_off, d_out;
@@ -1373,7 +1395,9 @@ cc_status cc_blind_sign_batch(cc_ctx* c, size_t n, size_t q, size_t k, const uin
     if (!c || !x || (q && !y) || (n && (!commitment || !out_h || !out_c1 || !out_c2 || (k && !ciphertexts) ||
                                         (q > k && !known))))
         return CC_ERR_DECODE;
+    if (q > kMaxQ) return CC_ERR_DECODE;
     if (k > q) return CC_ERR_LEN;  // reference: hidden + known == y.len() (assert_eq!)
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     const size_t sb = (size_t)sig_bytes(c->mode), t = k + 1;
@@ -1420,7 +1444,9 @@ cc_status cc_sigreq_verify_batch(cc_ctx* c, size_t n, size_t q, size_t k, const 
     if (!c || !g || (k && !hvec) ||
         (n && (!commitment || !elgamal_pk || !proofs || !chal || !verdicts || (k && !ciphertexts) || (q > k && !known))))
         return CC_ERR_DECODE;
+    if (q > kMaxQ) return CC_ERR_DECODE;
     if (k > q) return CC_ERR_LEN;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     const size_t sb = (size_t)sig_bytes(c->mode);
@@ -1454,10 +1480,12 @@ cc_status cc_vss_verify_batch(cc_ctx* c, size_t n, size_t t, const uint8_t* g, c
                               const uint8_t* commitments, size_t n_sets, const uint32_t* set_of, const uint64_t* ids,
                               const uint8_t* shares, uint8_t* verdicts) {
     c = primary(c);  // a device set forwards to its first device
-    if (!c || !g || !h || (n && (!commitments || !set_of || !ids || !shares || !verdicts)) || t == 0 || t > 4096)
+    if (!c || !g || !h || (n && (!commitments || !set_of || !ids || !shares || !verdicts)) || t == 0 || t > 4096 ||
+        n > kMaxBatch || n_sets > kMaxBatch)
         return CC_ERR_DECODE;
     for (size_t i = 0; i < n; i++)
         if (set_of[i] >= n_sets) return CC_ERR_DECODE;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
@@ -1581,7 +1609,9 @@ cc_status cc_verkey_aggregate_ids_device(cc_ctx* c, size_t n, size_t len, size_t
     c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!d_ids || !d_outX || (c->iss_q && !d_outY)))) return CC_ERR_DECODE;
     if (!c->iss_n) return CC_ERR_STATE;
+    if (len > kMaxIds) return CC_ERR_DECODE;
     if (len < t || len == 0) return CC_ERR_THRESHOLD;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
@@ -1602,7 +1632,9 @@ cc_status cc_aggregate_credential_batch_device(cc_ctx* c, size_t n, size_t len, 
     if (!c || (n && (!d_ids || !d_s1 || !d_s2 || !d_out_s1 || !d_out_s2 || !d_outX || (c->iss_q && !d_outY))))
         return CC_ERR_DECODE;
     if (!c->iss_n) return CC_ERR_STATE;
+    if (len > kMaxIds) return CC_ERR_DECODE;
     if (len < t || len == 0) return CC_ERR_THRESHOLD;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
@@ -1650,7 +1682,9 @@ cc_status cc_verkey_aggregate_ids(cc_ctx* c, size_t n, size_t len, size_t t, con
     c = primary(c);  // a device set forwards to its first device
     if (!c || (n && (!ids || !outX || (c->iss_q && !outY)))) return CC_ERR_DECODE;
     if (!c->iss_n) return CC_ERR_STATE;
+    if (len > kMaxIds) return CC_ERR_DECODE;
     if (len < t || len == 0) return CC_ERR_THRESHOLD;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     for (size_t i = 0; i < n; i++)
         for (size_t k = 0; k < t; k++)
@@ -1734,6 +1768,7 @@ cc_status cc_pok_verify_batch_device(cc_ctx* c, size_t n, size_t q, size_t r, si
     cc_status s = check_revealed(q, r, rev_idx, idx);
     if (s) return s;
     if (nresp != q - r + 1) return CC_ERR_BASES_EXPS;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
@@ -1774,6 +1809,7 @@ cc_status cc_pok_verify_batch(cc_ctx* c, size_t n, size_t q, size_t r, size_t nr
     cc_status s = check_revealed(q, r, rev_idx, idx);
     if (s) return s;
     if (nresp != q - r + 1) return CC_ERR_BASES_EXPS;
+    if (n > kMaxBatch) return CC_ERR_DECODE;
     if (!n) return CC_OK;
     HIPCK(hipSetDevice(c->device));
     drain_slots(c);  // concurrent device batches still using slot 0's workspaces (cc_set_concurrency)

@@ -37,6 +37,10 @@
  * Empty batches: every batch entry point checks its context state and lengths first (CC_ERR_STATE,
  * CC_ERR_LEN, CC_ERR_BASES_EXPS, CC_ERR_THRESHOLD), then returns CC_OK for n = 0 without reading,
  * writing or launching anything; its buffer pointers may then be NULL (tests/test_gpu_empty.py).
+ * Ceilings: n <= CC_MAX_BATCH credentials / proofs / points per call, an aggregation's ids per
+ * credential (len) <= CC_MAX_IDS, q <= CC_MAX_Q messages, an RLC finish's gathered partials <=
+ * CC_MAX_PARTS; a larger count is CC_ERR_DECODE before anything is read, allocated or launched (the
+ * byte counts the library derives from them then never overflow).
  */
 #ifndef COCONUT_HIP_H
 #define COCONUT_HIP_H
@@ -47,6 +51,11 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+
+#define CC_MAX_BATCH ((size_t)1 << 26)
+#define CC_MAX_IDS ((size_t)1 << 16)
+#define CC_MAX_Q ((size_t)4096)
+#define CC_MAX_PARTS ((size_t)1 << 16)
 
 typedef enum {
     CC_OK = 0,

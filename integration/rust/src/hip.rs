@@ -8,6 +8,11 @@ use std::os::raw::{c_char, c_int, c_void};
 #[repr(C)] pub struct CcCtx { _p: [u8; 0] }
 pub const CC_SIG_G2: c_int = 0;   // reference default feature (lib.rs:3-4)
 pub const CC_SIG_G1: c_int = 1;
+// argument ceilings (coconut_hip.h CC_MAX_*): a larger count is CC_ERR_DECODE
+pub const CC_MAX_BATCH: usize = 1 << 26;
+pub const CC_MAX_IDS: usize = 1 << 16;
+pub const CC_MAX_Q: usize = 4096;
+pub const CC_MAX_PARTS: usize = 1 << 16;
 
 extern "C" {
     pub fn cc_status_str(status: c_int) -> *const c_char;

@@ -1,4 +1,4 @@
-"""Empty batches through every batch entry point of include/coconut_hip.h.
+"""Empty batches and argument ceilings through the batch entry points of include/coconut_hip.h.
 
 The contract the header's entry points share: a call validates its context state and its lengths first
 (the reference's own errors: UnsupportedNoOfMessages, UnequalNoOfBasesExponents, the threshold assert
@@ -101,3 +101,22 @@ def test_empty_batch_still_needs_state():
         assert lib.cc_pok_verify_batch(c.h, 0, 2, 0, 3, N, N, N, N, N, N, N, N, N, N) == ERR_STATE
     finally:
         c.close()
+
+
+def test_counts_past_the_ceilings_are_decode_errors(ctx):
+    """coconut_hip.h CC_MAX_*: a count past its ceiling is CC_ERR_DECODE before anything is read,
+    allocated or launched — here with real (tiny) host buffers that a missing check would overrun."""
+    lib, h, q = _lib(), ctx.h, 6
+    DECODE = -4
+    big = (1 << 26) + 1
+    tiny = ctypes.create_string_buffer(64)
+    t = ctypes.cast(tiny, ctypes.c_void_p)
+    assert lib.cc_verify_batch(h, big, q, t, t, t, N, N, t, N, 0) == DECODE
+    assert lib.cc_pok_verify_batch(h, big, q, 0, q + 1, t, t, t, t, t, t, N, N, t, N) == DECODE
+    assert lib.cc_signature_aggregate_batch(h, big, 3, 3, t, t, t, t, t) == DECODE
+    assert lib.cc_verkey_aggregate_ids(h, big, 3, 3, t, t, t) == DECODE
+    assert lib.cc_verkey_aggregate_ids(h, 1, (1 << 16) + 1, 3, t, t, t) == DECODE  # len past CC_MAX_IDS
+    assert lib.cc_fixed_base_mul(h, 1, t, big, t, t) == DECODE
+    assert lib.cc_subgroup_check(h, 1, big, t, t) == DECODE
+    assert lib.cc_rlc_finish_device(h, (1 << 16) + 1, t, t, N, N) == DECODE
+    assert lib.cc_blind_sign_batch(h, 1, 4097, 1, t, t, t, t, t, t, t, t) == DECODE  # q past CC_MAX_Q
