@@ -110,3 +110,12 @@ def buf(b):
         return ctypes.c_void_p(a.ctypes.data), a
     a = np.ascontiguousarray(b)
     return ctypes.c_void_p(a.ctypes.data), a
+
+
+def need(b, nbytes: int, what: str):
+    """The byte count the C ABI will read from `b` (it trusts the caller's counts): a shorter buffer
+    is CC_ERR_DECODE here instead of a read past its end there."""
+    if nbytes > 0 and (b is None or len(b) < nbytes):
+        from .errors import CoconutError
+        got = 0 if b is None else len(b)
+        raise CoconutError(-4, f"{what}: {got} bytes, the call reads {nbytes}")

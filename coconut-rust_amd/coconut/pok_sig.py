@@ -13,7 +13,7 @@ from typing import Dict, List, Union
 
 import numpy as np
 
-from ._lib import buf, check, lib
+from ._lib import buf, check, lib, need
 from .errors import CoconutError
 from .signature import GT_BYTES, Context, Params, Verkey, fr_bytes
 
@@ -43,6 +43,11 @@ def pok_verify_batch(ctx: Context, n: int, q: int, revealed_idx, nresp: int, sig
                      want_gt: bool = False):
     """Batch PoK verify against the context's params and shared verkey."""
     r = len(revealed_idx)
+    sb, ob = ctx.mode.sig_bytes, ctx.mode.other_bytes
+    for v, nb, what in ((sigma1, n * sb, "sigma'_1"), (sigma2, n * sb, "sigma'_2"), (J, n * ob, "J"),
+                        (T, n * ob, "commitment"), (responses, n * nresp * 48, "responses"),
+                        (chal, n * 48, "challenges"), (revealed_msgs, n * r * 48, "revealed messages")):
+        need(v, nb, what)
     idx = np.ascontiguousarray(np.asarray(revealed_idx, dtype=np.uint64)) if r else np.zeros(1, np.uint64)
     verdicts = np.zeros(max(n, 1), dtype=np.uint8)
     gts = np.zeros(max(n, 1) * GT_BYTES, dtype=np.uint8) if want_gt else None

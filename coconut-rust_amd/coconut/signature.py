@@ -21,7 +21,7 @@ from typing import List, Sequence, Tuple, Union
 
 import numpy as np
 
-from ._lib import buf, check, lib
+from ._lib import need, buf, check, lib
 from .errors import CoconutError
 
 FR_BYTES = 48
@@ -164,6 +164,7 @@ class Context:
     def set_params(self, g_tilde: bytes):
         if self._gtilde == g_tilde:
             return
+        need(g_tilde, self.mode.other_bytes, "g_tilde")
         p, keep = buf(g_tilde)
         self._gtilde = None
         try:
@@ -179,6 +180,7 @@ class Context:
         if self._vk == key:
             return
         q = len(Yb) // self.mode.other_bytes
+        need(X, self.mode.other_bytes, "X~")
         px, k1 = buf(X)
         py, k2 = buf(Yb)
         self._vk = None  # a failed call leaves the context without a verkey
@@ -189,6 +191,9 @@ class Context:
         """Issuer verkey table (cc_set_issuers): ids[k] is issuer k's signer id, X n x OtherGroup,
         Y n x q x OtherGroup; then verkey_aggregate_ids takes id lists only."""
         ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64))
+        ob = self.mode.other_bytes
+        need(X, len(ids) * ob, "issuer X~")
+        need(Y, len(ids) * q * ob, "issuer Y~")
         px, k1 = buf(X)
         py, k2 = buf(Y)
         check(lib.cc_set_issuers(self.h, len(ids), q, ctypes.c_void_p(ids.ctypes.data), px, py), "cc_set_issuers")
@@ -245,6 +250,13 @@ def verify_batch(ctx: Context, n: int, q: int, sigma1: bytes, sigma2: bytes, msg
     if vk is not None and len(vk[0]) == ob and n != 1:
         ctx.set_verkey(vk[0], vk[1])
         vk = None
+    sb = ctx.mode.sig_bytes
+    need(sigma1, n * sb, "sigma_1")
+    need(sigma2, n * sb, "sigma_2")
+    need(msgs, n * q * 48, "messages")
+    if vk is not None:
+        need(vk[0], n * ob, "X~ per credential")
+        need(vk[1], n * q * ob, "Y~ per credential")
     verdicts = np.zeros(max(n, 1), dtype=np.uint8)
     gts = np.zeros(max(n, 1) * GT_BYTES, dtype=np.uint8) if want_gt else None
     p1, k1 = buf(sigma1)
@@ -264,6 +276,8 @@ def verify_batch(ctx: Context, n: int, q: int, sigma1: bytes, sigma2: bytes, msg
 def signature_aggregate_batch(ctx: Context, n: int, length: int, t: int, ids, sigma1: bytes, sigma2: bytes):
     sb = ctx.mode.sig_bytes
     ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64).reshape(n, length))
+    need(sigma1, n * length * sb, "sigma_1")
+    need(sigma2, n * length * sb, "sigma_2")
     o1 = np.zeros(max(n, 1) * sb, dtype=np.uint8)
     o2 = np.zeros(max(n, 1) * sb, dtype=np.uint8)
     p1, k1 = buf(sigma1)
@@ -279,6 +293,8 @@ def verkey_aggregate_batch(ctx: Context, n: int, length: int, t: int, q: int, id
     ids = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64).reshape(n, length))
     oX = np.zeros(max(n, 1) * ob, dtype=np.uint8)
     oY = np.zeros(max(n * q, 1) * ob, dtype=np.uint8)
+    need(X, n * length * ob, "X~")
+    need(Y, n * length * q * ob, "Y~")
     px, k1 = buf(X)
     py, k2 = buf(Y)
     check(lib.cc_verkey_aggregate_batch(ctx.h, n, length, t, q, ctypes.c_void_p(ids.ctypes.data), px, py,
@@ -362,6 +378,7 @@ def fixed_base_mul(ctx: Context, group: int, base: bytes, scalars: bytes) -> byt
     """out_i = k_i * base on the GPU (group 1 = G1, 2 = G2); scalars n x 48 B big-endian."""
     n = len(scalars) // FR_BYTES
     eb = G1_BYTES if group == 1 else G2_BYTES
+    need(base, eb, "base point")
     out = np.zeros(max(n, 1) * eb, dtype=np.uint8)
     pb, k1 = buf(base)
     ps, k2 = buf(scalars)

@@ -120,3 +120,23 @@ def test_counts_past_the_ceilings_are_decode_errors(ctx):
     assert lib.cc_subgroup_check(h, 1, big, t, t) == DECODE
     assert lib.cc_rlc_finish_device(h, (1 << 16) + 1, t, t, N, N) == DECODE
     assert lib.cc_blind_sign_batch(h, 1, 4097, 1, t, t, t, t, t, t, t, t) == DECODE  # q past CC_MAX_Q
+
+
+def test_python_mirror_checks_buffer_lengths(ctx):
+    """The Python mirror checks every byte count the C ABI will read (the C side trusts the caller's
+    counts): a short buffer is CoconutError(Decode) before the call, not a read past its end."""
+    import coconut
+    from coconut import CoconutError, CoconutErrorKind
+    q, sb = 6, 192
+    s = bytes(4 * sb)
+    with pytest.raises(CoconutError) as e:
+        coconut.verify_batch(ctx, 5, q, s, s, bytes(5 * q * 48))  # 4 sigmas for a batch of 5
+    assert e.value.kind == CoconutErrorKind.Decode
+    with pytest.raises(CoconutError):
+        coconut.verify_batch(ctx, 4, q, s, s, bytes(4 * q * 48 - 1))  # one message byte short
+    with pytest.raises(CoconutError):
+        coconut.fixed_base_mul(ctx, 1, bytes(96), bytes(48))  # a 96-byte G1 base (97 expected)
+    from coconut.pok_sig import pok_verify_batch
+    with pytest.raises(CoconutError):
+        pok_verify_batch(ctx, 2, q, [], q + 1, s, s, bytes(2 * 97), bytes(2 * 97), bytes(2 * (q + 1) * 48 - 48),
+                         bytes(2 * 48), b"")
