@@ -8,7 +8,7 @@ from typing import List, Sequence
 
 import numpy as np
 
-from ._lib import buf, check, lib
+from ._lib import buf, check, lib, need
 from .signature import Context
 
 
@@ -20,8 +20,12 @@ def blind_sign_batch(ctx: Context, q: int, k: int, commitments: Sequence[bytes],
     cm = b"".join(commitments)
     kn = b"".join(m for row in known for m in row)
     ct = b"".join(a + b for row in ciphertexts for a, b in row)
+    yb = b"".join(y)
+    for v, nb, what in ((cm, n * sb, "commitments"), (kn, n * max(q - k, 0) * 48, "known messages"),
+                        (ct, n * k * 2 * sb, "ciphertexts"), (x, 48, "x"), (yb, q * 48, "y")):
+        need(v, nb, what)
     outs = [np.zeros(max(n, 1) * sb, dtype=np.uint8) for _ in range(3)]
-    keep = [buf(v) for v in (cm, kn, ct, x, b"".join(y))]
+    keep = [buf(v) for v in (cm, kn, ct, x, yb)]
     check(lib.cc_blind_sign_batch(ctx.h, n, q, k, keep[0][0], keep[1][0] if kn else None, keep[2][0] if ct else None,
                                   keep[3][0], keep[4][0], *[ctypes.c_void_p(o.ctypes.data) for o in outs]),
           "cc_blind_sign_batch")
@@ -39,8 +43,15 @@ def sigreq_verify_batch(ctx: Context, q: int, k: int, g: bytes, h: Sequence[byte
         raise ValueError(f"each proof must be {pb} bytes")
     kn = b"".join(m for row in known for m in row)
     ct = b"".join(a + b for row in ciphertexts for a, b in row)
-    keep = [buf(v) for v in (g, b"".join(h[:k]), b"".join(commitments), kn, ct, b"".join(elgamal_pks),
-                             b"".join(proofs), b"".join(chals))]
+    sb = ctx.mode.sig_bytes
+    parts = (g, b"".join(h[:k]), b"".join(commitments), kn, ct, b"".join(elgamal_pks), b"".join(proofs),
+             b"".join(chals))
+    for v, nb, what in zip(parts, (sb, k * sb, n * sb, n * max(q - k, 0) * 48, n * k * 2 * sb, n * sb, n * pb,
+                                   n * 48),
+                           ("g", "h", "commitments", "known messages", "ciphertexts", "ElGamal keys", "proofs",
+                            "challenges")):
+        need(v, nb, what)
+    keep = [buf(v) for v in parts]
     v = np.zeros(max(n, 1), dtype=np.uint8)
     ptr = [kp[0] for kp in keep]
     check(lib.cc_sigreq_verify_batch(ctx.h, n, q, k, ptr[0], ptr[1] if k else None, ptr[2], ptr[3] if kn else None,
@@ -57,6 +68,11 @@ def vss_verify_batch(ctx: Context, t: int, g: bytes, h: bytes, commitment_sets: 
     so = np.ascontiguousarray(np.asarray(set_of, dtype=np.uint32))
     iv = np.ascontiguousarray(np.asarray(ids, dtype=np.uint64))
     sh = b"".join(a + b for a, b in shares)
+    for v, nb, what in ((g, 97, "g"), (h, 97, "h"), (cm, len(commitment_sets) * t * 97, "commitments"),
+                        (sh, n * 96, "shares")):
+        need(v, nb, what)
+    if len(so) < n:
+        need(None, n, "set_of")
     keep = [buf(v) for v in (g, h, cm, sh)]
     v = np.zeros(max(n, 1), dtype=np.uint8)
     check(lib.cc_vss_verify_batch(ctx.h, n, t, keep[0][0], keep[1][0], keep[2][0], len(commitment_sets),
